@@ -1,0 +1,203 @@
+"""oracle/oracle.py — TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of ``oracle/build/liboracle.so`` (the CPU restatement in ``oracle.hpp``). Only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import this module;
+the product package (``lbfgs-ffnn_amd/``) never does.
+
+Every function mirrors a reference entry point; citations are in ``oracle.hpp``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+ACTS = {"linear": 0, "tanh": 1, "relu": 2, "sigmoid": 3}
+
+_dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_fp = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_ip = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_lp = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    if os.path.isdir("/root/reference"):
+        subprocess.run(["make", "-s", "-C", _HERE, "ref"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        L.oracle_param_count.restype = C.c_longlong
+        L.oracle_param_count.argtypes = [C.c_int, _ip, _ip]
+        L.oracle_init_params_cpu.argtypes = [C.c_int, _ip, _ip, C.c_uint, _dp]
+        L.oracle_init_params_cuda.argtypes = [C.c_int, _ip, _ip, C.c_uint, _fp]
+        L.oracle_loss_grad.restype = C.c_double
+        L.oracle_loss_grad.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_void_p, C.c_longlong, C.c_double,
+                                       C.c_void_p]
+        L.oracle_loss_grad_f32.restype = C.c_double
+        L.oracle_loss_grad_f32.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, _dp]
+        L.oracle_loss.restype = C.c_double
+        L.oracle_loss.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_void_p]
+        L.oracle_two_loop.argtypes = [C.c_int, C.c_longlong, C.c_int, _dp, _dp, _dp, _dp, _dp]
+        L.oracle_lbfgs_wolfe_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_int, C.c_int,
+                                             C.c_double, C.c_int, _dp, C.POINTER(C.c_int), C.POINTER(C.c_long),
+                                             C.POINTER(C.c_long), C.POINTER(C.c_double)]
+        L.oracle_lbfgs_armijo_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_int, C.c_int,
+                                              C.c_double, C.c_int, C.c_double, C.c_double, C.c_int, _dp,
+                                              C.POINTER(C.c_int)]
+        L.oracle_slbfgs_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_int, C.c_double,
+                                        C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, _dp,
+                                        C.POINTER(C.c_int), C.c_void_p, C.c_longlong]
+        L.oracle_lbfgs_testfn.restype = C.c_double
+        L.oracle_lbfgs_testfn.argtypes = [C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.c_double, C.POINTER(C.c_int)]
+        L.oracle_sample_indices.argtypes = [C.c_longlong, C.c_int, C.c_uint, C.c_int, _lp]
+        L.oracle_synth_mnist.argtypes = [C.c_longlong, C.c_int, C.c_int, C.c_uint, _dp, _dp]
+        L.oracle_ring_trace.argtypes = [C.c_int, C.c_int, _ip, _ip]
+        L.oracle_num_threads.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+class Net:
+    """Layer spec: dims = [In, h1, ..., Out], acts = per-layer activation names."""
+
+    def __init__(self, dims, acts):
+        self.dims = np.ascontiguousarray(dims, dtype=np.int32)
+        self.acts = np.ascontiguousarray([ACTS[a] if isinstance(a, str) else int(a) for a in acts], dtype=np.int32)
+        self.nl = len(acts)
+        assert len(dims) == self.nl + 1
+
+    @property
+    def nparams(self) -> int:
+        return int(lib().oracle_param_count(self.nl, self.dims, self.acts))
+
+    def init_cpu(self, seed: int = 123) -> np.ndarray:
+        out = np.empty(self.nparams, np.float64)
+        lib().oracle_init_params_cpu(self.nl, self.dims, self.acts, seed, out)
+        return out
+
+    def init_cuda(self, seed: int = 123) -> np.ndarray:
+        out = np.empty(self.nparams, np.float32)
+        lib().oracle_init_params_cuda(self.nl, self.dims, self.acts, seed, out)
+        return out
+
+    def loss_grad(self, P, X, Y, idx=None, lam: float = 0.0):
+        P = np.ascontiguousarray(P, np.float64)
+        X = np.ascontiguousarray(X, np.float64)
+        Y = np.ascontiguousarray(Y, np.float64)
+        g = np.empty(self.nparams, np.float64)
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, np.int64)
+            B = len(idx)
+            ip = idx.ctypes.data
+        else:
+            B = X.shape[0]
+            ip = None
+        l = lib().oracle_loss_grad(self.nl, self.dims, self.acts, P, X, Y, ip, B, lam, g.ctypes.data)
+        return l, g
+
+    def loss_grad_f32(self, P, X, Y):
+        g = np.empty(self.nparams, np.float64)
+        l = lib().oracle_loss_grad_f32(self.nl, self.dims, self.acts, np.ascontiguousarray(P, np.float64),
+                                       np.ascontiguousarray(X, np.float64), np.ascontiguousarray(Y, np.float64),
+                                       X.shape[0], g)
+        return l, g
+
+    def loss(self, P, X, Y, want_out=False):
+        out = np.empty((X.shape[0], self.dims[-1]), np.float64) if want_out else None
+        l = lib().oracle_loss(self.nl, self.dims, self.acts, np.ascontiguousarray(P, np.float64),
+                              np.ascontiguousarray(X, np.float64), np.ascontiguousarray(Y, np.float64), X.shape[0],
+                              out.ctypes.data if want_out else None)
+        return (l, out) if want_out else l
+
+    def lbfgs_wolfe(self, P, X, Y, m=10, max_iters=20, tol=0.0, fp32=False):
+        P = np.array(P, np.float64, copy=True)
+        rec = np.zeros((max_iters, 6), np.float64)
+        it, nf, nb, ms = C.c_int(0), C.c_long(0), C.c_long(0), C.c_double(0)
+        lib().oracle_lbfgs_wolfe_mlp(self.nl, self.dims, self.acts, P, np.ascontiguousarray(X, np.float64),
+                                     np.ascontiguousarray(Y, np.float64), X.shape[0], m, max_iters, tol, int(fp32),
+                                     rec, C.byref(it), C.byref(nf), C.byref(nb), C.byref(ms))
+        return P, rec[: it.value], dict(iters=it.value, n_fwd=nf.value, n_bwd=nb.value, ms=ms.value)
+
+    def lbfgs_armijo(self, P, X, Y, m=10, max_iters=20, tol=0.0, max_ls=20, c1=1e-4, rho=0.5, fp32=False):
+        P = np.array(P, np.float64, copy=True)
+        rec = np.zeros((max_iters, 6), np.float64)
+        it = C.c_int(0)
+        lib().oracle_lbfgs_armijo_mlp(self.nl, self.dims, self.acts, P, np.ascontiguousarray(X, np.float64),
+                                      np.ascontiguousarray(Y, np.float64), X.shape[0], m, max_iters, tol, max_ls, c1,
+                                      rho, int(fp32), rec, C.byref(it))
+        return P, rec[: it.value]
+
+    def slbfgs(self, P, X, Y, epochs=2, tol=0.0, M=10, L=10, b=32, bH=16, step=0.02, lam=1e-4, fp32=False,
+               want_idx=False):
+        P = np.array(P, np.float64, copy=True)
+        rec = np.zeros((epochs, 6), np.float64)
+        it = C.c_int(0)
+        N = X.shape[0]
+        cap = 0
+        idx = None
+        if want_idx:
+            m = max(1, N // b)
+            cap = epochs * (m * b + (m // max(L, 1) + 1) * bH)
+            idx = np.full(cap, -1, np.int64)
+        lib().oracle_slbfgs_mlp(self.nl, self.dims, self.acts, P, np.ascontiguousarray(X, np.float64),
+                                np.ascontiguousarray(Y, np.float64), N, epochs, tol, M, L, b, bH, step, lam, int(fp32),
+                                rec, C.byref(it), idx.ctypes.data if want_idx else None, cap)
+        if want_idx:
+            idx = idx[idx >= 0]
+        return P, rec[: it.value], idx
+
+
+def two_loop(mode: int, S, Y, rho, g):
+    S = np.ascontiguousarray(S, np.float64)
+    Y = np.ascontiguousarray(Y, np.float64)
+    k, n = S.shape if S.ndim == 2 else (0, len(g))
+    out = np.empty(len(g), np.float64)
+    if k == 0:
+        S = np.zeros((1, len(g)))
+        Y = np.zeros((1, len(g)))
+    lib().oracle_two_loop(mode, len(g), k, S, Y, np.ascontiguousarray(rho if k else [0.0], np.float64),
+                          np.ascontiguousarray(g, np.float64), out)
+    return out
+
+
+def lbfgs_testfn(fid: int, x0, m=16, max_iters=4000, tol=1e-12):
+    x = np.array(x0, np.float64, copy=True)
+    it = C.c_int(0)
+    gn = lib().oracle_lbfgs_testfn(fid, len(x), x, m, max_iters, tol, C.byref(it))
+    return x, gn, it.value
+
+
+def sample_indices(N: int, b: int, seed: int = 123, calls: int = 1) -> np.ndarray:
+    out = np.empty(calls * b, np.int64)
+    lib().oracle_sample_indices(N, b, seed, calls, out)
+    return out.reshape(calls, b)
+
+
+def synth_mnist(N: int, In: int = 784, classes: int = 10, seed: int = 123):
+    X = np.empty((N, In), np.float64)
+    Y = np.empty((N, classes), np.float64)
+    lib().oracle_synth_mnist(N, In, classes, seed, X, Y)
+    return X, Y
+
+
+def ring_trace(cap: int, npush: int):
+    out = np.empty(npush * cap, np.int32)
+    heads = np.empty(npush, np.int32)
+    lib().oracle_ring_trace(cap, npush, out, heads)
+    return heads, out.reshape(npush, cap)
+
+
+def num_threads() -> int:
+    return int(lib().oracle_num_threads())
