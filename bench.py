@@ -1,0 +1,180 @@
+"""Benchmark: full-batch L-BFGS iterations/s on the BASELINE.json headline workload.
+
+Workload (BASELINE.json configs[1]): 784-128-10 MLP (ReLU, Linear), full-batch L-BFGS m=10 with the
+reference's CPU semantics (Wolfe line search, lbfgs.hpp:38-100), N = 60000 synthetic MNIST-shaped
+samples (SURVEY.md §8(d) recipe), fp32, tolerance 0 (fixed iteration count). A "step" = one L-BFGS
+iteration (two-loop direction + line-search trials, each a fused loss+grad evaluation).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+With N > 1 the 60000 samples are split into contiguous shards (strong scaling; one RCCL all-reduce
+of [grad | loss] per evaluation). Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import __graft_entry__  # noqa: E402
+
+METRIC = "L-BFGS iters/sec + grad-eval GFLOP/s, 784-128-10 MLP full-batch"
+REF_GPU_ITERS_PER_S = 139.1      # L-BFGS m=10, 784-128-10, N=60000 (sm_86, fp32 cuBLAS)
+FP32_MFMA_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix peak (dense)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--samples", type=int, default=60000)
+    ap.add_argument("--dims", type=str, default="784,128,10")
+    ap.add_argument("--acts", type=str, default="relu,linear")
+    ap.add_argument("--m", type=int, default=10)
+    ap.add_argument("--line-search", type=str, default="wolfe")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=8)
+    ap.add_argument("--pmc-json", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(dims, acts, N, m, iters):
+    """The oracle (fp64 C++/OpenMP restatement of the reference CPU path, literal call pattern incl. its
+    redundant f/grad re-evaluations) timed on this host; bounded sample of the same workload."""
+    O = __graft_entry__.load_oracle()
+    O.lib()
+    X, Y = O.synth_mnist(N)
+    net = O.Net(dims, acts)
+    P = net.init_cpu(123)
+    _, rec, info = net.lbfgs_wolfe(P, X, Y, m=m, max_iters=iters)
+    ms = info["ms"]
+    return dict(value=round(iters / (ms / 1e3), 4), unit="iters/s", cores=O.num_threads(), kind="port",
+                sample=f"{iters} L-BFGS iterations (Wolfe, m={m}) of the {'-'.join(map(str, dims))} MLP at "
+                       f"N={N}, fp64 oracle (oracle/oracle.hpp) with the reference's f/grad call pattern "
+                       f"({info['n_fwd']} forward, {info['n_bwd']} backward passes), "
+                       f"{O.num_threads()} OpenMP threads, {ms / 1e3:.1f} s")
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    pkg = __graft_entry__.load_package()
+    dims = [int(x) for x in a.dims.split(",")]
+    acts = a.acts.split(",")
+    N = a.samples
+
+    ctx = pkg.Context(local)
+    if world > 1:
+        uid = [pkg.Context.unique_id() if rank == 0 else None]
+        torch.distributed.broadcast_object_list(uid, src=0)
+        ctx.comm_init(world, rank, uid[0])
+    Xh, Yh = pkg.synth_mnist(N, dims[0], dims[-1], 123)
+    lo, hi = N * rank // world, N * (rank + 1) // world
+    X = torch.from_numpy(Xh[lo:hi]).cuda()
+    Y = torch.from_numpy(Yh[lo:hi]).cuda()
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    torch.cuda.synchronize()
+
+    run = pkg.LbfgsRun(net, P, X, Y, n_global=N, line_search=a.line_search, m=a.m, max_iters=1 << 30, tol=0.0,
+                       record_cap=a.warmup + a.steps + 8)
+    run.iterate(a.warmup)
+    evals0 = run.info.n_evals
+    ctx.prof_enable(True)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    run.iterate(a.steps)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    barrier()
+    prof = ctx.prof_read()
+    ctx.prof_enable(False)
+    evals = run.info.n_evals - evals0
+    iters_done = run.hist.size - a.warmup
+
+    if rank == 0:
+        F = pkg.grad_flops_per_sample(dims) * N            # algorithmic flops per full-batch evaluation
+        gflops = evals * F / elapsed / 1e9
+        # dominant kernel: largest total time in the timed region (HIP events on the library stream)
+        name, (ms, cnt) = max(prof.items(), key=lambda kv: kv[1][0])
+        avg_s = ms / 1e3 / cnt
+        kind, layer = name.split("[")[0], int(name.split("[")[1].rstrip("]"))
+        n_loc = hi - lo
+        In, Out = dims[layer], dims[layer + 1]
+        if kind in ("gemm_fwd", "gemm_dw", "gemm_dx"):
+            flops = 2.0 * n_loc * In * Out                    # per launch, per rank
+            roof = dict(bound="mfma", achieved=round(flops / avg_s / 1e12, 3), peak=FP32_MFMA_PEAK_TFLOPS,
+                        unit="TFLOP/s")
+        else:
+            roof = dict(bound="hbm", achieved=None, peak=HBM_PEAK_GBS, unit="GB/s")
+        roof["frac"] = round(roof["achieved"] / roof["peak"], 4) if roof["achieved"] else None
+        roof["kernel"] = name
+        roof["avg_launch_us"] = round(avg_s * 1e6, 2)
+        roof["traffic"] = None
+        if os.path.exists(a.pmc_json):
+            try:
+                pm = json.load(open(a.pmc_json))
+                if pm.get("section") == name and pm.get("config") == f"{a.dims}:{N}:{world}":
+                    roof["traffic"] = pm.get("hbm_bytes_per_launch")
+            except Exception:
+                pass
+        ms_step = elapsed / max(iters_done, 1) * 1e3
+        value = iters_done / elapsed
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "iters/s",
+            "n_gpus": world,
+            "steps": iters_done,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / REF_GPU_ITERS_PER_S, 3),
+            "dtype": "fp32",
+            "data": "synthetic",
+            "config": {"workload": f"{a.dims} MLP ({a.acts}), full-batch L-BFGS m={a.m} "
+                                   f"({a.line_search} line search, CPU-reference semantics), N={N}",
+                       "global_batch": N, "parallelism": f"dp{world}"},
+            "grad_eval_gflops": round(gflops, 1),
+            "evals_per_iter": round(evals / max(iters_done, 1), 3),
+            "roofline": roof,
+            "kernel_ms_per_step": {k: round(v[0] / max(iters_done, 1), 4) for k, v in sorted(prof.items())},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(dims, acts, N, a.m, a.cpu_iters)
+        print(json.dumps(out), flush=True)
+    run.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

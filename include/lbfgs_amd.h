@@ -1,0 +1,176 @@
+/* include/lbfgs_amd.h — C ABI of the MI355X-native L-BFGS / S-LBFGS engine (liblbfgs_amd.so).
+ *
+ * Plain pointers and sizes only (no torch / HIP types in the signatures; a stream is passed as void*).
+ * Every entry point names the reference interface it replaces (paths relative to SignorB/lbfgs-FFNN).
+ * Conventions:
+ *   - return value: LBF_OK (0) or an error code; lbf_last_error() gives the message (thread-local).
+ *   - d_* arguments are device pointers (hipMalloc'd or torch tensors' data_ptr), h_* are host pointers.
+ *   - calls are asynchronous on the context stream unless they return a host value.
+ *   - parameter layout is the reference's flat vector: per layer [W (Out x In, column-major) | b (Out)]
+ *     (src/network.hpp:45-71, src/cuda/network.cuh:36-59); data X is In x N column-major and Y is
+ *     Out x N column-major, i.e. one sample per contiguous row of In (resp. Out) floats.
+ *   - one context per GPU, one host thread per context (the reference is single-threaded too,
+ *     src/cuda/common.cuh).
+ */
+#ifndef LBFGS_AMD_H
+#define LBFGS_AMD_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBF_OK 0
+#define LBF_ERR_INVALID 1 /* bad argument (reference: early return in lbfgs.cuh:45-48)          */
+#define LBF_ERR_HIP 2     /* HIP runtime error (reference: cuda_check abort, common.cuh:18-23)  */
+#define LBF_ERR_COMM 3    /* RCCL error                                                         */
+#define LBF_ERR_STATE 4   /* call out of order                                                  */
+
+/* Activation ids == the reference's ActivationType (src/cuda/kernels.cuh:53-58). */
+#define LBF_ACT_LINEAR 0
+#define LBF_ACT_TANH 1
+#define LBF_ACT_RELU 2
+#define LBF_ACT_SIGMOID 3
+
+/* Line-search / two-loop policies.
+ * WOLFE  = CPU semantics: src/minimizer/lbfgs.hpp:38-139 + full_batch_minimizer.hpp:126-157.
+ * ARMIJO = CUDA semantics: src/cuda/lbfgs.cuh:39-261. */
+#define LBF_LS_WOLFE 0
+#define LBF_LS_ARMIJO 1
+
+/* Parameter-initialisation streams (both libstdc++ mt19937, seed = UnifiedConfig::seed):
+ * CPU  = normal_distribution<double> over all params (src/network.hpp:45-71);
+ * CUDA = normal_distribution<float> over weights, zero biases (src/cuda/network.cuh:36-59). */
+#define LBF_INIT_CPU 0
+#define LBF_INIT_CUDA 1
+
+typedef struct lbf_ctx lbf_ctx;
+typedef struct lbf_mlp lbf_mlp;
+typedef struct lbf_lbfgs lbf_lbfgs;
+
+const char *lbf_last_error(void);
+const char *lbf_version(void);
+
+/* ---- context: device, stream, workspace, optional communicator --------------------------------
+ * Replaces CublasHandle (src/cuda/cublas_handle.cuh:22-39) + the implicit legacy stream. */
+int lbf_ctx_create(int device, void *stream /* hipStream_t or NULL = own stream */, lbf_ctx **out);
+int lbf_ctx_destroy(lbf_ctx *ctx);
+int lbf_ctx_sync(lbf_ctx *ctx);
+void *lbf_ctx_stream(lbf_ctx *ctx);
+
+/* ---- data-parallel communicator (RCCL over xGMI). New in this engine: the reference has no
+ * collective. One all-reduce of [grad | loss] per loss+grad evaluation. */
+int lbf_comm_unique_id(char out[128]);
+int lbf_comm_init(lbf_ctx *ctx, int nranks, int rank, const char id[128]);
+int lbf_comm_rank(lbf_ctx *ctx, int *rank, int *nranks);
+int lbf_allreduce_sum(lbf_ctx *ctx, float *d_buf, size_t count);
+
+/* ---- dense MLP --------------------------------------------------------------------------------
+ * Replaces CudaNetwork (src/cuda/network.cuh:21-158) / CudaDenseLayer (src/cuda/layer.cuh). */
+int lbf_mlp_create(lbf_ctx *ctx, int nlayers, const int *dims /* nlayers+1 */, const int *acts /* nlayers */,
+                   lbf_mlp **out);
+int lbf_mlp_destroy(lbf_mlp *net);
+long long lbf_mlp_param_count(const lbf_mlp *net);
+/* bindParams(seed) (network.cuh:36-59 / network.hpp:45-71): host libstdc++ RNG, upload to d_params. */
+int lbf_mlp_init_params(lbf_mlp *net, unsigned seed, int init_mode, float *d_params);
+/* Host-only form of the same draws (h_out holds lbf count of params); no device needed. */
+int lbf_init_params_host(int nlayers, const int *dims, const int *acts, unsigned seed, int init_mode, float *h_out);
+/* forward_only (network.cuh:79-88): d_out is batch x Out row-major (== Out x batch column-major). */
+int lbf_mlp_forward(lbf_mlp *net, const float *d_params, const float *d_X, long long batch, float *d_out);
+/* compute_loss_and_grad (network.cuh:97-119) == the LossGradFun of minimizer_base.cuh:15-16:
+ *   loss = 0.5*||net(X)-Y||^2 * inv_scale + 0.5*l2*||w||^2,  grad = dloss/dw (written to d_grad).
+ * inv_scale is 1/batch in the reference; under data parallelism pass 1/global_batch and the
+ * context's communicator sums the shards. d_idx (nullable) gathers rows of X/Y (S-LBFGS minibatches,
+ * unified_optimization.hpp:361-364). h_loss receives the loss (synchronises). */
+int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const float *d_X, const float *d_Y,
+                      const int *d_idx, long long batch, double inv_scale, double l2, double *h_loss);
+
+/* ---- two-loop recursion (src/minimizer/lbfgs.hpp:106-139 / s_lbfgs.hpp:106-136 /
+ * lbfgs.cuh:206-261) on an explicit history given in logical order (oldest first):
+ * d_S, d_Y are k x n row-major, h_rho[k]. mode: 0 = CPU (returns -Hg), 1 = S-LBFGS (returns +Hg,
+ * gamma guarded and clamped), 2 = CUDA (returns -Hg, gamma guarded). */
+int lbf_two_loop(lbf_ctx *ctx, long long n, int k, const float *d_S, const float *d_Y, const double *h_rho,
+                 const float *d_g, float *d_dir, int mode);
+
+/* ---- BLAS-1 with device-side deterministic fp64 reductions (replace kernels.cuh:14-50). */
+int lbf_dot(lbf_ctx *ctx, long long n, const float *d_x, const float *d_y, double *h_out);
+int lbf_nrm2(lbf_ctx *ctx, long long n, const float *d_x, double *h_out);
+int lbf_axpy(lbf_ctx *ctx, long long n, float alpha, const float *d_x, float *d_y);
+int lbf_scal(lbf_ctx *ctx, long long n, float alpha, float *d_x);
+
+/* ---- solvers --------------------------------------------------------------------------------- */
+typedef struct lbf_lbfgs_params {
+  int m;              /* history size (UnifiedConfig::m_param; LBFGS::setHistorySize lbfgs.hpp:29) */
+  int max_iters;      /* setMaxIterations                                                         */
+  double tol;         /* setTolerance: stop when ||g|| < tol                                      */
+  int line_search;    /* LBF_LS_WOLFE | LBF_LS_ARMIJO                                             */
+  int max_line_iters; /* 50 (full_batch_minimizer.hpp:116) | 20 (minimizer_base.cuh:63)           */
+  double c1, c2, rho; /* 1e-4, 0.9, 0.5 (full_batch_minimizer.hpp:113-115; minimizer_base.cuh:64)  */
+} lbf_lbfgs_params;
+
+typedef struct lbf_slbfgs_params {
+  int max_epochs;     /* UnifiedConfig::max_iters (outer iterations)                  */
+  double tol;         /* full-gradient norm tolerance (s_lbfgs.hpp:208)              */
+  int M, L, b, b_H;   /* m_param, L_param, batch_size, b_H_param (unified_optimization.hpp:325) */
+  double step;        /* learning_rate                                                */
+  double lambda;      /* L2, 1e-4 in the reference (unified_optimization.hpp:334)    */
+  unsigned seed;      /* kDefaultSeed = 123 (src/seed.hpp:4; s_lbfgs.hpp:183)        */
+  double fd_eps;      /* finite-difference HVP epsilon, 1e-4 (s_lbfgs.hpp:90)        */
+} lbf_slbfgs_params;
+
+/* Per-iteration history == IterationRecorder (src/iteration_recorder.hpp:13-146) plus extras.
+ * Host arrays of capacity cap; any pointer may be NULL. */
+typedef struct lbf_record {
+  double *loss, *grad_norm, *time_ms, *alpha;
+  int *ls_trials, *accepted;
+  int cap, size;
+} lbf_record;
+
+typedef struct lbf_solve_info {
+  int iterations;
+  long long n_evals;  /* fused loss+grad evaluations executed */
+  double final_loss, final_grad_norm;
+} lbf_solve_info;
+
+void lbf_lbfgs_default_params(lbf_lbfgs_params *p, int line_search);
+void lbf_slbfgs_default_params(lbf_slbfgs_params *p);
+
+/* Full-batch L-BFGS (CudaLBFGS::solve lbfgs.cuh:39-194 / LBFGS::solve lbfgs.hpp:38-100): params are
+ * updated in place. n_local rows of X/Y live on this rank; n_global = sum over ranks (the loss and
+ * gradient are means over n_global, matching the single-process reference). */
+int lbf_lbfgs_solve(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, const float *d_X,
+                    const float *d_Y, long long n_local, long long n_global, lbf_record *rec,
+                    lbf_solve_info *info);
+
+/* Stateful form for benchmarking: begin evaluates the start point; iterate runs up to iters more
+ * iterations (returns early on convergence); end releases the history. */
+int lbf_lbfgs_begin(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, const float *d_X,
+                    const float *d_Y, long long n_local, long long n_global, lbf_lbfgs **out);
+int lbf_lbfgs_iterate(lbf_lbfgs *s, int iters, lbf_record *rec, lbf_solve_info *info);
+int lbf_lbfgs_end(lbf_lbfgs *s);
+
+/* S-LBFGS (SLBFGS::stochastic_solve s_lbfgs.hpp:165-290 via UnifiedSLBFGS_CPU,
+ * unified_optimization.hpp:306-408). X/Y hold all N rows on every rank; minibatches are sampled on
+ * the host with the reference's libstdc++ stream and sliced across ranks. */
+int lbf_slbfgs_solve(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params, const float *d_X,
+                     const float *d_Y, long long N, lbf_record *rec, lbf_solve_info *info);
+
+/* ---- profiling: HIP-event timing of every kernel class on the context stream (benchmark use).
+ * Section id = kind*16 + layer; kinds: 0 fwd GEMM, 1 dW GEMM, 2 dX GEMM, 3 loss, 4 split-K reduce,
+ * 5 finalize, 6 Gram sweep, 7 coefficients, 8 combine sweep, 9 line-search axpy, 10 all-reduce.
+ * (The reference times whole iterations only: lbfgs.cuh:80-87, 176-182.) */
+int lbf_prof_enable(lbf_ctx *ctx, int on);
+int lbf_prof_read(lbf_ctx *ctx, int cap, int *ids, double *ms, long long *counts, int *n_out);
+
+/* ---- host helpers (not on the timed path) ------------------------------------------------------
+ * Synthetic MNIST-shaped data (SURVEY.md §8(d) recipe), row-major [N][In] / [N][classes]. */
+int lbf_synth_mnist(long long N, int In, int classes, unsigned seed, float *h_X, float *h_Y);
+/* Partial Fisher-Yates minibatch draws from one mt19937(seed) (s_lbfgs.hpp:141-160). */
+int lbf_sample_indices(long long N, int b, unsigned seed, int calls, long long *h_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LBFGS_AMD_H */

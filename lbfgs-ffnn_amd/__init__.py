@@ -1,0 +1,12 @@
+"""lbfgs-ffnn_amd — MI355X-native L-BFGS / S-LBFGS engine for dense FFNNs.
+
+Compute lives in ``build/liblbfgs_amd.so`` (hand-written HIP kernels for gfx950 behind the C ABI
+``include/lbfgs_amd.h``). This package is the host-side mirror of the reference's unified API.
+The directory name contains a hyphen, so load it with :func:`load` from the repo root helpers
+(``tests/conftest.py``, ``bench.py``, ``__graft_entry__.py``) under the module name ``lbfgs_ffnn_amd``.
+"""
+from ._lib import LIB_PATH, LbfError, lib  # noqa: F401
+from .engine import (Context, History, LbfgsRun, Mlp, grad_flops_per_sample, init_params_host, lbfgs_solve,  # noqa: F401
+                     sample_indices, slbfgs_solve, synth_mnist)
+from .unified import (IterationRecorder, UnifiedConfig, UnifiedDataset, UnifiedLauncher, UnifiedLBFGS,  # noqa: F401
+                      UnifiedSLBFGS, write_history_csv)

@@ -1,0 +1,440 @@
+// extern "C" surface of liblbfgs_amd.so (declared in include/lbfgs_amd.h). Every call converts
+// internal exceptions into a status code + thread-local message (the reference aborts instead:
+// src/cuda/common.cuh:18-23, cublas_handle.cuh:14-19).
+#include "../../include/lbfgs_amd.h"
+#include "host_rng.hpp"
+#include "runtime.hpp"
+#include "solvers.hpp"
+
+#include <cstring>
+#include <memory>
+#include <string>
+
+using namespace lbf;
+
+struct lbf_ctx {
+  Ctx c;
+  DevBuf<double> scal;
+  DevBuf<float> gscratch;
+};
+struct lbf_mlp {
+  lbf_ctx *ctx;
+  std::unique_ptr<Mlp> net;
+};
+struct lbf_lbfgs {
+  std::unique_ptr<LbfgsSolver> s;
+};
+
+namespace {
+thread_local std::string g_err;
+
+template <class F> int guard(F &&f) {
+  try {
+    f();
+    return LBF_OK;
+  } catch (const Error &e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const std::exception &e) {
+    g_err = e.what();
+    return LBF_ERR_INVALID;
+  } catch (...) {
+    g_err = "unknown error";
+    return LBF_ERR_INVALID;
+  }
+}
+
+void check_comm(ncclResult_t r, const char *what) {
+  if (r != ncclSuccess) throw Error(LBF_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
+}
+} // namespace
+
+extern "C" {
+
+const char *lbf_last_error(void) { return g_err.c_str(); }
+const char *lbf_version(void) { return "lbfgs_amd 0.1 (gfx950)"; }
+
+int lbf_ctx_create(int device, void *stream, lbf_ctx **out) {
+  return guard([&] {
+    LBF_REQUIRE(out, "out");
+    auto *c = new lbf_ctx();
+    c->c.device = device;
+    try {
+      c->c.set_device();
+      if (stream) {
+        c->c.stream = static_cast<hipStream_t>(stream);
+      } else {
+        LBF_HIP(hipStreamCreateWithFlags(&c->c.stream, hipStreamDefault)); // blocking: ordered with the legacy stream torch uses
+        c->c.own_stream = true;
+      }
+      c->scal.resize(SC_N);
+      LBF_HIP(hipMemset(c->scal.get(), 0, SC_N * sizeof(double)));
+    } catch (...) {
+      delete c;
+      throw;
+    }
+    *out = c;
+  });
+}
+
+int lbf_ctx_destroy(lbf_ctx *ctx) {
+  return guard([&] { delete ctx; });
+}
+
+int lbf_ctx_sync(lbf_ctx *ctx) {
+  return guard([&] {
+    LBF_REQUIRE(ctx, "ctx");
+    LBF_HIP(hipStreamSynchronize(ctx->c.stream));
+  });
+}
+
+void *lbf_ctx_stream(lbf_ctx *ctx) { return ctx ? static_cast<void *>(ctx->c.stream) : nullptr; }
+
+int lbf_comm_unique_id(char out[128]) {
+  return guard([&] {
+    ncclUniqueId id;
+    check_comm(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    static_assert(sizeof(id) <= 128, "unique id size");
+    std::memset(out, 0, 128);
+    std::memcpy(out, &id, sizeof(id));
+  });
+}
+
+int lbf_comm_init(lbf_ctx *ctx, int nranks, int rank, const char id[128]) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && nranks >= 1 && rank >= 0 && rank < nranks, "comm args");
+    ctx->c.set_device();
+    if (ctx->c.comm) {
+      (void)ncclCommDestroy(ctx->c.comm);
+      ctx->c.comm = nullptr;
+    }
+    if (nranks > 1) {
+      ncclUniqueId uid;
+      std::memcpy(&uid, id, sizeof(uid));
+      check_comm(ncclCommInitRank(&ctx->c.comm, nranks, uid, rank), "ncclCommInitRank");
+    }
+    ctx->c.rank = rank;
+    ctx->c.nranks = nranks;
+  });
+}
+
+int lbf_comm_rank(lbf_ctx *ctx, int *rank, int *nranks) {
+  return guard([&] {
+    LBF_REQUIRE(ctx, "ctx");
+    if (rank) *rank = ctx->c.rank;
+    if (nranks) *nranks = ctx->c.nranks;
+  });
+}
+
+int lbf_allreduce_sum(lbf_ctx *ctx, float *d_buf, size_t count) {
+  return guard([&] {
+    LBF_REQUIRE(ctx, "ctx");
+    ctx->c.set_device();
+    ctx->c.allreduce(d_buf, count);
+  });
+}
+
+int lbf_mlp_create(lbf_ctx *ctx, int nlayers, const int *dims, const int *acts, lbf_mlp **out) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && dims && acts && out, "null argument");
+    ctx->c.set_device();
+    auto *m = new lbf_mlp();
+    m->ctx = ctx;
+    try {
+      m->net.reset(new Mlp(&ctx->c, nlayers, dims, acts));
+    } catch (...) {
+      delete m;
+      throw;
+    }
+    *out = m;
+  });
+}
+
+int lbf_mlp_destroy(lbf_mlp *net) {
+  return guard([&] { delete net; });
+}
+
+long long lbf_mlp_param_count(const lbf_mlp *net) { return net ? (long long)net->net->nparams() : -1; }
+
+int lbf_mlp_init_params(lbf_mlp *net, unsigned seed, int init_mode, float *d_params) {
+  return guard([&] {
+    LBF_REQUIRE(net && d_params, "null argument");
+    LBF_REQUIRE(init_mode == LBF_INIT_CPU || init_mode == LBF_INIT_CUDA, "init_mode");
+    std::vector<float> h;
+    init_params_host(net->net->layers(), seed, init_mode, h);
+    net->ctx->c.set_device();
+    LBF_HIP(hipMemcpyAsync(d_params, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice,
+                           net->ctx->c.stream));
+    LBF_HIP(hipStreamSynchronize(net->ctx->c.stream));
+  });
+}
+
+int lbf_init_params_host(int nlayers, const int *dims, const int *acts, unsigned seed, int init_mode, float *h_out) {
+  return guard([&] {
+    LBF_REQUIRE(dims && acts && h_out && nlayers >= 1, "bad argument");
+    LBF_REQUIRE(init_mode == LBF_INIT_CPU || init_mode == LBF_INIT_CUDA, "init_mode");
+    std::vector<Layer> layers;
+    size_t off = 0;
+    for (int l = 0; l < nlayers; ++l) {
+      Layer L;
+      L.in = dims[l];
+      L.out = dims[l + 1];
+      L.act = acts[l];
+      L.off = off;
+      off += size_t(L.in + 1) * L.out;
+      layers.push_back(L);
+    }
+    std::vector<float> h;
+    init_params_host(layers, seed, init_mode, h);
+    std::copy(h.begin(), h.end(), h_out);
+  });
+}
+
+int lbf_mlp_forward(lbf_mlp *net, const float *d_params, const float *d_X, long long batch, float *d_out) {
+  return guard([&] {
+    LBF_REQUIRE(net && d_params && d_X && d_out && batch >= 0, "bad argument");
+    net->ctx->c.set_device();
+    const float *o = net->net->forward(d_params, d_X, nullptr, batch);
+    const int Out = net->net->layers().back().out;
+    LBF_HIP(hipMemcpyAsync(d_out, o, size_t(batch) * Out * sizeof(float), hipMemcpyDeviceToDevice,
+                           net->ctx->c.stream));
+  });
+}
+
+int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const float *d_X, const float *d_Y,
+                      const int *d_idx, long long batch, double inv_scale, double l2, double *h_loss) {
+  return guard([&] {
+    LBF_REQUIRE(net && d_params && d_grad && d_X && d_Y && batch >= 0, "bad argument");
+    lbf_ctx *c = net->ctx;
+    c->c.set_device();
+    const size_t n = net->net->nparams();
+    c->gscratch.ensure(n + 4);
+    net->net->loss_grad(d_params, c->gscratch.get(), d_X, d_Y, d_idx, batch, inv_scale, l2, nullptr, c->scal.get());
+    LBF_HIP(hipMemcpyAsync(d_grad, c->gscratch.get(), n * sizeof(float), hipMemcpyDeviceToDevice, c->c.stream));
+    if (h_loss) {
+      double tmp[SC_N];
+      LBF_HIP(hipMemcpyAsync(tmp, c->scal.get(), SC_N * sizeof(double), hipMemcpyDeviceToHost, c->c.stream));
+      LBF_HIP(hipStreamSynchronize(c->c.stream));
+      *h_loss = tmp[SC_LOSS];
+    }
+  });
+}
+
+int lbf_two_loop(lbf_ctx *ctx, long long n, int k, const float *d_S, const float *d_Y, const double *h_rho,
+                 const float *d_g, float *d_dir, int mode) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && d_g && d_dir && n > 0 && k >= 0 && k <= 128, "bad argument");
+    LBF_REQUIRE(k == 0 || (d_S && d_Y && h_rho), "history pointers");
+    LBF_REQUIRE(mode >= 0 && mode <= 2, "mode");
+    ctx->c.set_device();
+    hipStream_t s = ctx->c.stream;
+    const int policy = mode == 0 ? POL_CPU : (mode == 1 ? POL_SLBFGS : POL_CUDA);
+    const double dsign = mode == 1 ? 1.0 : -1.0;
+    History h(&ctx->c, k, n);
+    DevBuf<float> zero{size_t(n)};
+    LBF_HIP(hipMemsetAsync(zero.get(), 0, size_t(n) * sizeof(float), s));
+    for (int i = 0; i < k; ++i) {
+      GramArgs ga;
+      ga.policy = policy;
+      ga.has_pair = 1;
+      ga.sa = d_S + size_t(i) * n;
+      ga.sb = zero.get();
+      ga.ya = d_Y + size_t(i) * n;
+      ga.yb = zero.get();
+      h.update(ga, -1, 1, dsign); // -1: push unconditionally
+    }
+    if (k > 0)
+      LBF_HIP(hipMemcpyAsync(h.view().rho, h_rho, size_t(k) * sizeof(double), hipMemcpyHostToDevice, s));
+    GramArgs gg;
+    gg.policy = policy;
+    gg.has_g = 1;
+    gg.ga = d_g;
+    h.update(gg, 2, 1, dsign); // 2: direction without the solver's descent fallback
+    h.combine(d_g, d_dir, nullptr, nullptr, nullptr, false, 0.0);
+    LBF_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int lbf_dot(lbf_ctx *ctx, long long n, const float *d_x, const float *d_y, double *h_out) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && d_x && d_y && h_out && n >= 0, "bad argument");
+    ctx->c.set_device();
+    hipStream_t s = ctx->c.stream;
+    const int nw = dots_partials_wg(n);
+    ctx->c.part.ensure(size_t(nw));
+    ctx->c.red.ensure(1);
+    ctx->c.host.ensure(1);
+    dot_partials(s, n, d_x, d_y, ctx->c.part.get());
+    reduce_rows(s, ctx->c.part.get(), nw, 1, ctx->c.red.get());
+    LBF_HIP(hipMemcpyAsync(ctx->c.host.get(), ctx->c.red.get(), sizeof(double), hipMemcpyDeviceToHost, s));
+    LBF_HIP(hipStreamSynchronize(s));
+    *h_out = ctx->c.host[0];
+  });
+}
+
+int lbf_nrm2(lbf_ctx *ctx, long long n, const float *d_x, double *h_out) {
+  double d = 0;
+  int r = lbf_dot(ctx, n, d_x, d_x, &d);
+  if (r == LBF_OK && h_out) *h_out = std::sqrt(d);
+  return r;
+}
+
+int lbf_axpy(lbf_ctx *ctx, long long n, float alpha, const float *d_x, float *d_y) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && d_x && d_y && n >= 0, "bad argument");
+    ctx->c.set_device();
+    axpy(ctx->c.stream, n, alpha, d_x, d_y);
+  });
+}
+
+int lbf_scal(lbf_ctx *ctx, long long n, float alpha, float *d_x) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && d_x && n >= 0, "bad argument");
+    ctx->c.set_device();
+    scal(ctx->c.stream, n, alpha, d_x);
+  });
+}
+
+void lbf_lbfgs_default_params(lbf_lbfgs_params *p, int line_search) {
+  if (!p) return;
+  p->line_search = line_search;
+  if (line_search == LBF_LS_ARMIJO) { // minimizer_base.cuh:63-64, lbfgs.cuh:118 (m_ = 16)
+    p->m = 16;
+    p->max_iters = 200;
+    p->tol = 1e-6;
+    p->max_line_iters = 20;
+    p->c1 = 1e-4;
+    p->c2 = 0.9;
+    p->rho = 0.5;
+  } else { // full_batch_minimizer.hpp:107-116, lbfgs.hpp:142 (m = 16)
+    p->m = 16;
+    p->max_iters = 1000;
+    p->tol = 1e-10;
+    p->max_line_iters = 50;
+    p->c1 = 1e-4;
+    p->c2 = 0.9;
+    p->rho = 0.5;
+  }
+}
+
+void lbf_slbfgs_default_params(lbf_slbfgs_params *p) {
+  if (!p) return;
+  p->max_epochs = 1000; // stochastic_minimizer.hpp:44-47
+  p->tol = 1e-4;
+  p->M = 10;
+  p->L = 10;
+  p->b = 128;
+  p->b_H = 64;
+  p->step = 0.01;
+  p->lambda = 1e-4;
+  p->seed = 123;
+  p->fd_eps = 1e-4;
+}
+
+int lbf_lbfgs_begin(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, const float *d_X,
+                    const float *d_Y, long long n_local, long long n_global, lbf_lbfgs **out) {
+  return guard([&] {
+    LBF_REQUIRE(net && prm && out, "null argument");
+    LBF_REQUIRE(prm->m >= 0 && prm->m <= 128, "m in [0, 128]");
+    net->ctx->c.set_device();
+    auto *s = new lbf_lbfgs();
+    try {
+      s->s.reset(new LbfgsSolver(net->net.get(), *prm, d_params, d_X, d_Y, n_local, n_global));
+    } catch (...) {
+      delete s;
+      throw;
+    }
+    *out = s;
+  });
+}
+
+int lbf_lbfgs_iterate(lbf_lbfgs *s, int iters, lbf_record *rec, lbf_solve_info *info) {
+  return guard([&] {
+    LBF_REQUIRE(s && iters >= 0, "bad argument");
+    s->s->iterate(iters, rec);
+    s->s->info(info);
+  });
+}
+
+int lbf_lbfgs_end(lbf_lbfgs *s) {
+  return guard([&] { delete s; });
+}
+
+int lbf_lbfgs_solve(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, const float *d_X,
+                    const float *d_Y, long long n_local, long long n_global, lbf_record *rec,
+                    lbf_solve_info *info) {
+  // CudaMinimizerBase::solve contract (minimizer_base.cuh:54-59): n <= 0 or params == nullptr is a
+  // no-op with iterations() == 0 (lbfgs.cuh:45-48).
+  if (!net || !d_params || net->net->nparams() == 0) {
+    if (info) std::memset(info, 0, sizeof(*info));
+    return LBF_OK;
+  }
+  lbf_lbfgs *s = nullptr;
+  int r = lbf_lbfgs_begin(net, prm, d_params, d_X, d_Y, n_local, n_global, &s);
+  if (r != LBF_OK) return r;
+  r = lbf_lbfgs_iterate(s, prm->max_iters, rec, info);
+  lbf_lbfgs_end(s);
+  return r;
+}
+
+int lbf_slbfgs_solve(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params, const float *d_X,
+                     const float *d_Y, long long N, lbf_record *rec, lbf_solve_info *info) {
+  return guard([&] {
+    LBF_REQUIRE(net && prm, "null argument");
+    net->ctx->c.set_device();
+    SlbfgsSolver s(net->net.get(), *prm, d_params, d_X, d_Y, N);
+    s.run(rec);
+    s.info(info);
+  });
+}
+
+int lbf_prof_enable(lbf_ctx *ctx, int on) {
+  return guard([&] {
+    LBF_REQUIRE(ctx, "ctx");
+    ctx->c.prof.resolve();
+    ctx->c.prof.on = on != 0;
+    if (on) {
+      ctx->c.prof.ms.clear();
+      ctx->c.prof.cnt.clear();
+    }
+  });
+}
+
+int lbf_prof_read(lbf_ctx *ctx, int cap, int *ids, double *ms, long long *counts, int *n_out) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && n_out, "null argument");
+    ctx->c.set_device();
+    ctx->c.prof.resolve();
+    int k = 0;
+    for (size_t i = 0; i < ctx->c.prof.cnt.size(); ++i) {
+      if (ctx->c.prof.cnt[i] == 0) continue;
+      if (k < cap) {
+        if (ids) ids[k] = int(i);
+        if (ms) ms[k] = ctx->c.prof.ms[i];
+        if (counts) counts[k] = ctx->c.prof.cnt[i];
+      }
+      ++k;
+    }
+    *n_out = k;
+  });
+}
+
+int lbf_synth_mnist(long long N, int In, int classes, unsigned seed, float *h_X, float *h_Y) {
+  return guard([&] {
+    LBF_REQUIRE(N >= 0 && In > 0 && classes > 0 && h_X && h_Y, "bad argument");
+    synth_mnist_host(N, In, classes, seed, h_X, h_Y);
+  });
+}
+
+int lbf_sample_indices(long long N, int b, unsigned seed, int calls, long long *h_out) {
+  return guard([&] {
+    LBF_REQUIRE(N >= 0 && b >= 0 && calls >= 0 && h_out, "bad argument");
+    std::mt19937 rng(seed);
+    for (int c = 0; c < calls; ++c) {
+      auto v = sample_minibatch(size_t(N), size_t(b), rng);
+      for (size_t i = 0; i < v.size(); ++i) h_out[size_t(c) * b + i] = (long long)v[i];
+    }
+  });
+}
+
+} // extern "C"

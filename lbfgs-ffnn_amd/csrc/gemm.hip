@@ -1,0 +1,317 @@
+// fp32 MFMA GEMM for the FFNN layers (gfx950, wave64).
+//
+// Replaces the reference's three cublasSgemm calls per layer (src/cuda/layer.cuh:51-103) and the
+// add_bias / activation / activation_deriv kernels (src/cuda/kernels.cuh:74-133), which are fused
+// into the epilogues here:
+//   forward   Z = X * W + b, A = act(Z)            a_kc (X rows),  b mn-contiguous (W is [In][Out])
+//   dX        D = (dZ * W^T) .* act'(A_prev)        a_kc (dZ rows), b_kc (W rows)
+//   dW | db   [dW ; db] = [A_prev | 1]^T * dZ       both mn-contiguous, split-K over the batch
+//
+// MFMA: v_mfma_f32_32x32x2_f32 (exact f32 fma chain). Lane l feeds A[i = l&31][k = l>>5] and
+// B[k = l>>5][j = l&31]; accumulator register r of lane l is C[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31].
+// The k index inside a 32-deep LDS tile is permuted so lane half h always consumes k = 16h + s at
+// step s: a k-contiguous operand is then 16 consecutive floats per lane (4 x ds_read_b128) and an
+// mn-contiguous operand is one conflict-free ds_read_b32 per step.
+// Workgroup: 256 threads = 4 waves in a WM x WN grid, each wave TM x TN tiles of 32x32.
+#include "internal.hpp"
+#include "kernels.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace lbf {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float act_apply(int a, float x) {
+  switch (a) {
+  case ACT_TANH: return tanhf(x);
+  case ACT_RELU: return x > 0.0f ? x : 0.0f;
+  case ACT_SIGMOID: return 1.0f / (1.0f + expf(-x));
+  default: return x;
+  }
+}
+// Derivative expressed through the post-activation value y (src/cuda/kernels.cuh:109-133); equal to
+// the CPU path's act'(Z) (src/layer.hpp:16-47) in exact arithmetic.
+__device__ __forceinline__ float act_deriv_out(int a, float y) {
+  switch (a) {
+  case ACT_TANH: return 1.0f - y * y;
+  case ACT_RELU: return y > 0.0f ? 1.0f : 0.0f;
+  case ACT_SIGMOID: return y * (1.0f - y);
+  default: return 1.0f;
+  }
+}
+
+struct GemmK {
+  int M, N, K, k_chunk;
+  const float *A;
+  long long lda;
+  const int *a_idx;
+  int a_mvalid, a_ones, a_vec;
+  const float *B;
+  long long ldb;
+  int b_vec;
+  float *C;
+  long long ldc, slab_stride;
+  const float *bias;
+  int act;
+  const float *aux;
+  long long ldaux;
+  int aux_act;
+};
+
+// k-contiguous operand: R rows x 32 k. Thread chunk c -> row c>>3, k-quad c&7.
+template <int R, bool GATHER>
+__device__ __forceinline__ void load_kc(f32x4 (&r)[R / 32], const float *base, long long ld, const int *idx,
+                                        int row0, int rows, int k0, int kend, int vec) {
+#pragma unroll
+  for (int i = 0; i < R / 32; ++i) {
+    const int c = threadIdx.x + i * 256;
+    const int row = row0 + (c >> 3);
+    const int k = k0 + (c & 7) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < rows) {
+      const long long grow = GATHER ? (long long)idx[row] : (long long)row;
+      const float *p = base + grow * ld + k;
+      if (vec && k + 3 < kend) {
+        v = *reinterpret_cast<const f32x4 *>(p);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (k + j < kend) ? p[j] : 0.0f;
+      }
+    }
+    r[i] = v;
+  }
+}
+template <int R>
+__device__ __forceinline__ void store_kc(float *lds, const f32x4 (&r)[R / 32]) {
+  constexpr int LDK = 36;
+#pragma unroll
+  for (int i = 0; i < R / 32; ++i) {
+    const int c = threadIdx.x + i * 256;
+    *reinterpret_cast<f32x4 *>(lds + (c >> 3) * LDK + (c & 7) * 4) = r[i];
+  }
+}
+
+// mn-contiguous operand: 32 k-rows x R columns. Thread chunk c -> k-row c/(R/4), column quad c%(R/4).
+template <int R, bool GATHER>
+__device__ __forceinline__ void load_mc(f32x4 (&r)[R / 32], const float *base, long long ld, const int *idx,
+                                        int col0, int cvalid, int ones, int k0, int kend, int vec) {
+  constexpr int Q = R / 4;
+#pragma unroll
+  for (int i = 0; i < R / 32; ++i) {
+    const int c = threadIdx.x + i * 256;
+    const int k = k0 + c / Q;
+    const int col = col0 + (c % Q) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (k < kend) {
+      const long long grow = GATHER ? (long long)idx[k] : (long long)k;
+      const float *p = base + grow * ld + col;
+      if (vec && col + 3 < cvalid) {
+        v = *reinterpret_cast<const f32x4 *>(p);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (col + j < cvalid) ? p[j] : ((col + j == ones) ? 1.0f : 0.0f);
+      }
+    }
+    r[i] = v;
+  }
+}
+template <int R>
+__device__ __forceinline__ void store_mc(float *lds, const f32x4 (&r)[R / 32]) {
+  constexpr int Q = R / 4, LD = R + 4;
+#pragma unroll
+  for (int i = 0; i < R / 32; ++i) {
+    const int c = threadIdx.x + i * 256;
+    *reinterpret_cast<f32x4 *>(lds + (c / Q) * LD + (c % Q) * 4) = r[i];
+  }
+}
+
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32, LDK = BK + 4;
+  constexpr int ASZ = AKC ? BM * LDK : BK * (BM + 4);
+  constexpr int BSZ = BKC ? BN * LDK : BK * (BN + 4);
+  __shared__ __attribute__((aligned(16))) float lds[2 * (ASZ + BSZ)];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 31, lh = lane >> 5;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int kb = blockIdx.z * g.k_chunk;
+  const int ke = min(g.K, kb + g.k_chunk);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+  f32x4 ra[BM / 32], rb[BN / 32];
+  auto gload = [&](int k0) {
+    if constexpr (AKC) load_kc<BM, GATHER>(ra, g.A, g.lda, g.a_idx, m0, g.M, k0, ke, g.a_vec);
+    else load_mc<BM, GATHER>(ra, g.A, g.lda, g.a_idx, m0, g.a_mvalid, g.a_ones, k0, ke, g.a_vec);
+    if constexpr (BKC) load_kc<BN, false>(rb, g.B, g.ldb, nullptr, n0, g.N, k0, ke, g.b_vec);
+    else load_mc<BN, false>(rb, g.B, g.ldb, nullptr, n0, g.N, -1, k0, ke, g.b_vec);
+  };
+  auto sstore = [&](int buf) {
+    float *As = lds + buf * (ASZ + BSZ);
+    float *Bs = As + ASZ;
+    if constexpr (AKC) store_kc<BM>(As, ra);
+    else store_mc<BM>(As, ra);
+    if constexpr (BKC) store_kc<BN>(Bs, rb);
+    else store_mc<BN>(Bs, rb);
+  };
+  auto compute = [&](int buf) {
+    const float *As = lds + buf * (ASZ + BSZ);
+    const float *Bs = As + ASZ;
+    float af[TM][AKC ? 16 : 1], bf[TN][BKC ? 16 : 1];
+    if constexpr (AKC) {
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const float *p = As + (wm * TM * 32 + tm * 32 + li) * LDK + lh * 16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = *reinterpret_cast<const f32x4 *>(p + q * 4);
+          af[tm][q * 4 + 0] = v[0];
+          af[tm][q * 4 + 1] = v[1];
+          af[tm][q * 4 + 2] = v[2];
+          af[tm][q * 4 + 3] = v[3];
+        }
+      }
+    }
+    if constexpr (BKC) {
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const float *p = Bs + (wn * TN * 32 + tn * 32 + li) * LDK + lh * 16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = *reinterpret_cast<const f32x4 *>(p + q * 4);
+          bf[tn][q * 4 + 0] = v[0];
+          bf[tn][q * 4 + 1] = v[1];
+          bf[tn][q * 4 + 2] = v[2];
+          bf[tn][q * 4 + 3] = v[3];
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        if constexpr (AKC) av[tm] = af[tm][s];
+        else av[tm] = As[(lh * 16 + s) * (BM + 4) + wm * TM * 32 + tm * 32 + li];
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        if constexpr (BKC) bv[tn] = bf[tn][s];
+        else bv[tn] = Bs[(lh * 16 + s) * (BN + 4) + wn * TN * 32 + tn * 32 + li];
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+
+  if (kb < ke) {
+    gload(kb);
+    sstore(0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kb; k0 < ke; k0 += BK) {
+      const bool more = k0 + BK < ke;
+      if (more) gload(k0 + BK);
+      compute(buf);
+      if (more) sstore(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  // Epilogue: lanes 0-31 own consecutive columns -> each register row is a 128-B coalesced store.
+  float *C = g.C + (EPI == EPI_STORE ? (long long)blockIdx.z * g.slab_stride : 0LL);
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int n = n0 + wn * TN * 32 + tn * 32 + li;
+    if (n >= g.N) continue;
+    float bn = 0.0f;
+    if constexpr (EPI == EPI_FWD) bn = g.bias ? g.bias[n] : 0.0f;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= g.M) continue;
+        float v = acc[tm][tn][r];
+        if constexpr (EPI == EPI_FWD) v = act_apply(g.act, v + bn);
+        if constexpr (EPI == EPI_DX) v *= act_deriv_out(g.aux_act, g.aux[(long long)m * g.ldaux + n]);
+        C[(long long)m * g.ldc + n] = v;
+      }
+    }
+  }
+}
+
+namespace {
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI>
+void launch(hipStream_t s, const GemmDesc &d) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  GemmK k;
+  k.M = d.M;
+  k.N = d.N;
+  k.K = d.K;
+  k.k_chunk = d.splits > 1 ? d.k_chunk : d.K;
+  k.A = d.A;
+  k.lda = d.lda;
+  k.a_idx = d.a_idx;
+  k.a_mvalid = d.a_mvalid > 0 ? d.a_mvalid : d.M;
+  k.a_ones = d.a_ones;
+  k.a_vec = (d.lda % 4 == 0) && aligned16(d.A);
+  k.B = d.B;
+  k.ldb = d.ldb;
+  k.b_vec = (d.ldb % 4 == 0) && aligned16(d.B);
+  k.C = d.C;
+  k.ldc = d.ldc;
+  k.slab_stride = d.slab_stride;
+  k.bias = d.bias;
+  k.act = d.act;
+  k.aux = d.aux;
+  k.ldaux = d.ldaux;
+  k.aux_act = d.aux_act;
+  dim3 grid((d.N + BN - 1) / BN, (d.M + BM - 1) / BM, d.splits > 1 ? d.splits : 1);
+  if (d.a_idx)
+    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true>), grid, dim3(256), 0, s, k);
+  else
+    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false>), grid, dim3(256), 0, s, k);
+}
+
+template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const GemmDesc &d) {
+  if (d.N > 64) launch<2, 2, 2, 2, AKC, BKC, EPI>(s, d);       // 128 x 128
+  else if (d.N > 32) launch<2, 2, 2, 1, AKC, BKC, EPI>(s, d);  // 128 x 64
+  else launch<4, 1, 1, 1, AKC, BKC, EPI>(s, d);                // 128 x 32
+}
+
+} // namespace
+
+void gemm_tile_for(int N, int *BM, int *BN) {
+  *BM = 128;
+  *BN = N > 64 ? 128 : (N > 32 ? 64 : 32);
+}
+
+void gemm(hipStream_t s, const GemmDesc &d) {
+  if (d.M <= 0 || d.N <= 0) return;
+  if (d.epi == EPI_FWD && d.a_kc && !d.b_kc) dispatch_tile<true, false, EPI_FWD>(s, d);
+  else if (d.epi == EPI_DX && d.a_kc && d.b_kc) dispatch_tile<true, true, EPI_DX>(s, d);
+  else if (d.epi == EPI_STORE && !d.a_kc && !d.b_kc) dispatch_tile<false, false, EPI_STORE>(s, d);
+  else if (d.epi == EPI_STORE && d.a_kc && !d.b_kc) dispatch_tile<true, false, EPI_STORE>(s, d);
+  else throw std::runtime_error("gemm: unsupported operand/epilogue combination");
+  LBF_KERNEL_CHECK();
+}
+
+} // namespace lbf

@@ -1,0 +1,90 @@
+// Internal runtime support for liblbfgs_amd.so: error type, HIP checks, RAII device buffers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace lbf {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define LBF_HIP(expr)                                                                                        \
+  do {                                                                                                       \
+    hipError_t e_ = (expr);                                                                                  \
+    if (e_ != hipSuccess)                                                                                    \
+      throw ::lbf::Error(2, std::string("HIP error: ") + #expr + " -> " + hipGetErrorString(e_) + " (" +     \
+                                __FILE__ + ":" + std::to_string(__LINE__) + ")");                            \
+  } while (0)
+
+#define LBF_KERNEL_CHECK() LBF_HIP(hipGetLastError())
+
+#define LBF_REQUIRE(cond, msg)                                                                               \
+  do {                                                                                                       \
+    if (!(cond)) throw ::lbf::Error(1, std::string("invalid argument: ") + (msg));                           \
+  } while (0)
+
+// RAII device allocation (the reference's DeviceBuffer, src/cuda/device_buffer.cuh:7-96, minus the
+// synchronous copies: everything here is stream-ordered).
+template <class T> class DevBuf {
+public:
+  DevBuf() = default;
+  explicit DevBuf(size_t n) { resize(n); }
+  ~DevBuf() { release(); }
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  DevBuf(DevBuf &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+  DevBuf &operator=(DevBuf &&o) noexcept {
+    if (this != &o) { release(); p_ = o.p_; n_ = o.n_; o.p_ = nullptr; o.n_ = 0; }
+    return *this;
+  }
+  void resize(size_t n) {
+    if (n == n_) return;
+    release();
+    if (n) LBF_HIP(hipMalloc(&p_, n * sizeof(T)));
+    n_ = n;
+  }
+  void ensure(size_t n) { if (n > n_) resize(n); }
+  T *get() const { return p_; }
+  size_t size() const { return n_; }
+  void release() {
+    if (p_) (void)hipFree(p_);
+    p_ = nullptr;
+    n_ = 0;
+  }
+
+private:
+  T *p_ = nullptr;
+  size_t n_ = 0;
+};
+
+// Pinned host staging (status read-back, index uploads).
+template <class T> class PinnedBuf {
+public:
+  PinnedBuf() = default;
+  ~PinnedBuf() { if (p_) (void)hipHostFree(p_); }
+  PinnedBuf(const PinnedBuf &) = delete;
+  PinnedBuf &operator=(const PinnedBuf &) = delete;
+  void ensure(size_t n) {
+    if (n <= n_) return;
+    if (p_) (void)hipHostFree(p_);
+    LBF_HIP(hipHostMalloc(&p_, n * sizeof(T), hipHostMallocDefault));
+    n_ = n;
+  }
+  T *get() const { return p_; }
+  T &operator[](size_t i) { return p_[i]; }
+
+private:
+  T *p_ = nullptr;
+  size_t n_ = 0;
+};
+
+inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
+
+} // namespace lbf

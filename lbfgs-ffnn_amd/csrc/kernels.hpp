@@ -1,0 +1,170 @@
+// Kernel launcher interfaces (implemented in gemm.hip / vec_kernels.hip) and the device-resident
+// L-BFGS history layout shared by host and device code.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace lbf {
+
+enum Act : int { ACT_LINEAR = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_SIGMOID = 3 };
+
+// ------------------------------------------------------------------------------------------------
+// GEMM  C[M x N] (row-major, ldc) = op(A)[M x K] * op(B)[K x N]   (fp32 in, fp32 MFMA accumulate)
+//   a_kc: A stored k-contiguous   A[m*lda + k]  (else m-contiguous A[k*lda + m])
+//   b_kc: B stored k-contiguous   B[n*ldb + k]  (else n-contiguous B[k*ldb + n])
+//   a_idx: optional row gather of the stored A rows (k-contiguous: rows = m; m-contiguous: rows = k)
+//   a_mvalid / a_ones: m-contiguous A only — columns >= a_mvalid read 0 except column a_ones == 1
+//                      (turns dW = A^T dZ into [dW ; db] in one GEMM, the flat layer segment).
+// Epilogues: FWD   C = act(acc + bias[n])
+//            DX    C = acc * act'(aux[m*ldaux + n])       (act' from the post-activation value)
+//            STORE C(+ split*slab_stride) = acc           (split-K partial slabs)
+// ------------------------------------------------------------------------------------------------
+enum GemmEpi : int { EPI_FWD = 0, EPI_DX = 1, EPI_STORE = 2 };
+
+struct GemmDesc {
+  int M = 0, N = 0, K = 0;
+  const float *A = nullptr;
+  long long lda = 0;
+  bool a_kc = true;
+  const int *a_idx = nullptr;
+  int a_mvalid = 0, a_ones = -1;
+  const float *B = nullptr;
+  long long ldb = 0;
+  bool b_kc = false;
+  float *C = nullptr;
+  long long ldc = 0, slab_stride = 0;
+  int splits = 1, k_chunk = 0;
+  int epi = EPI_FWD;
+  const float *bias = nullptr;
+  int act = ACT_LINEAR;
+  const float *aux = nullptr;
+  long long ldaux = 0;
+  int aux_act = ACT_LINEAR;
+};
+
+void gemm(hipStream_t s, const GemmDesc &d);
+// Tile (BM, BN) the dispatcher picks for a given N (used by the split-K planner).
+void gemm_tile_for(int N, int *BM, int *BN);
+
+// ------------------------------------------------------------------------------------------------
+// Vector / reduction kernels (vec_kernels.hip). All reductions are deterministic: per-workgroup
+// fp64 partials written to memory, then summed in a fixed order by reduce_rows.
+// ------------------------------------------------------------------------------------------------
+// out[c] = sum_r P[r*ncols + c], r in [0, nrows), fixed order.    (one wave per column)
+void reduce_rows(hipStream_t s, const double *P, int nrows, int ncols, double *out);
+
+// Output layer: d = act_out(Z) already in A_out; diff = A_out - Y[idx? idx[b] : b];
+// dZ = diff * act'(A_out) * inv_scale ; per-WG partial of sum(diff^2) -> partials[wg].
+int loss_partials_wg(long long B, int Out);
+void loss_diff(hipStream_t s, const float *Aout, long long lda, const float *Y, long long ldy, const int *idx,
+               long long B, int Out, int act, double inv_scale, float *dZ, long long ldz, double *partials);
+
+// grad[e] = sum_s slab[s*stride + e] * scale (fixed order), e in [0, count)
+void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride, long long count, float *grad);
+
+// g += lambda*w (if lambda != 0); per-WG partials of (g.g, g.p, w.w) -> partials[wg*3 + {0,1,2}]
+int dots_partials_wg(long long n);
+void finalize_grad_dots(hipStream_t s, long long n, float *g, const float *w, double lambda, const float *p,
+                        double *partials);
+// generic: per-WG partials of x.y -> partials[wg]
+void dot_partials(hipStream_t s, long long n, const float *x, const float *y, double *partials);
+
+// scal[LOSS] = 0.5 * sse * inv_scale + 0.5*lambda*ww, with sse from sse_d (double) or, when sse_hilo
+// is non-null, sse = hilo[0] + hilo[1] (all-reduced split fp32 pair).
+void eval_status(hipStream_t s, const double *sse_d, const float *sse_hilo, double inv_scale, double lambda,
+                 double *scal);
+// hilo[0] = float(x), hilo[1] = float(x - hilo[0])
+void pack_hilo(hipStream_t s, const double *x, float *hilo);
+
+void axpy(hipStream_t s, long long n, float alpha, const float *x, float *y);
+void scal(hipStream_t s, long long n, float alpha, float *x);
+// y = x + alpha * p
+void axpy_to(hipStream_t s, long long n, const float *x, float alpha, const float *p, float *y);
+// u = (sum_i W[slot_i]) / cnt  in logical order, fp64 accumulation
+void average_slots(hipStream_t s, long long n, const float *W, long long ld, const int *h_slots, int cnt, float *u);
+// out = a + c*b
+void lincomb(hipStream_t s, long long n, const float *a, double c, const float *b, float *out);
+
+// ------------------------------------------------------------------------------------------------
+// Device-resident L-BFGS history ("vector-free" two-loop: Chen, Wang & Zhou, NIPS 2014).
+// Vectors s_i, y_i live in slots of S/Y (slots = m+1 so a rejected pair never clobbers live data);
+// the Gram matrices of all stored vectors are kept in fp64 and the two-loop recursion of the
+// reference runs on (2k+1) coefficients, so a direction costs two HBM sweeps of the history
+// (dots, then one linear combination) instead of 2k dependent dot/axpy launches.
+// ------------------------------------------------------------------------------------------------
+enum HistPolicy : int { POL_CPU = 0, POL_CUDA = 1, POL_SLBFGS = 2 };
+
+// istate (int32)
+enum { IST_COUNT = 0, IST_FREE = 1, IST_WSLOT = 2, IST_ORDER = 4 };
+// scal (fp64) block, read back to the host in one copy
+enum {
+  SC_GG = 0,      // g.g of the vector the direction was built for
+  SC_GTP = 1,     // g^T dir
+  SC_ALPHA0 = 2,  // first trial step (min(1, 1/||g||) at iteration 0, else 1)
+  SC_GAMMA = 3,
+  SC_YS = 4,      // y.s of the last pair
+  SC_ACCEPT = 5,  // last pair accepted
+  SC_COUNT = 6,   // live pairs
+  SC_RESET = 7,   // CUDA descent fallback fired
+  SC_LOSS = 8,    // last evaluation: loss
+  SC_TGG = 9,     //                  g.g
+  SC_TGP = 10,    //                  g.p
+  SC_WW = 11,     //                  w.w
+  SC_SSE = 12,    //                  local sum of squared errors (before reduction over ranks)
+  SC_N = 16
+};
+
+struct HistView {
+  int m = 0, slots = 0;
+  long long n = 0, ld = 0; // vector length, slot stride (floats)
+  float *S = nullptr, *Y = nullptr;
+  int *ist = nullptr;
+  double *rho = nullptr, *SS = nullptr, *SY = nullptr, *YY = nullptr, *gS = nullptr, *gY = nullptr;
+  double *coef = nullptr; // [2*slots + 1]: cs (logical), cy (logical), cg
+  double *scal = nullptr; // SC_N
+};
+
+struct GramArgs {
+  HistView h;
+  // pair: s = sa - sb ; y = (ya - yb) * yscale, written into slot ist[IST_WSLOT] (set by gram_select)
+  const float *sa = nullptr, *sb = nullptr, *ya = nullptr, *yb = nullptr;
+  double yscale = 1.0;
+  int has_pair = 0;
+  // vector: g = ga - gb + gc (gb, gc nullable), optionally materialised into g_out
+  const float *ga = nullptr, *gb = nullptr, *gc = nullptr;
+  float *g_out = nullptr;
+  int has_g = 0;
+  int reset = 0; // treat the history as empty before the push (CUDA reset_history)
+  int policy = POL_CPU;
+};
+// Number of fp64 partial columns per workgroup and the workgroup count for a given n.
+int gram_ncols(int m);
+int gram_nwg(long long n);
+// Chooses the write slot (device), then streams the history once computing all new dots.
+void gram_update(hipStream_t s, const GramArgs &a, double *partials);
+
+struct CoefArgs {
+  HistView h;
+  const double *dots = nullptr; // reduced gram output
+  int has_pair = 0, has_g = 0, reset = 0, policy = POL_CPU;
+  int want_dir = 1;
+  int iter = 1;
+  double dsign = -1.0;
+};
+void hist_coef(hipStream_t s, const CoefArgs &a);
+
+struct CombineArgs {
+  HistView h;
+  const float *g = nullptr; // the vector the direction was built for
+  float *dir = nullptr;     // nullable
+  const float *x_in = nullptr;
+  float *x_out = nullptr, *x_out2 = nullptr; // x_out = x_in + alpha*dir ; x_out2 = copy of x_out
+  int alpha_from_state = 1;                  // alpha = scal[SC_ALPHA0]
+  double alpha = 1.0;
+};
+void hist_combine(hipStream_t s, const CombineArgs &a);
+void hist_reset(hipStream_t s, const HistView &h);
+
+} // namespace lbf

@@ -1,0 +1,321 @@
+// Context, MLP evaluation plan and device history (see runtime.hpp).
+#include "runtime.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace lbf {
+
+// ------------------------------------------------------------------------------------------------
+// Ctx
+// ------------------------------------------------------------------------------------------------
+Ctx::~Ctx() {
+  if (comm) (void)ncclCommDestroy(comm);
+  if (own_stream && stream) (void)hipStreamDestroy(stream);
+}
+
+Profiler::~Profiler() {
+  for (auto e : pool) (void)hipEventDestroy(e);
+}
+
+size_t Profiler::mark(hipStream_t s) {
+  if (used == pool.size()) {
+    hipEvent_t e;
+    LBF_HIP(hipEventCreate(&e));
+    pool.push_back(e);
+  }
+  LBF_HIP(hipEventRecord(pool[used], s));
+  return used++;
+}
+
+void Profiler::resolve() {
+  if (recs.empty()) return;
+  LBF_HIP(hipEventSynchronize(pool[used - 1]));
+  for (auto &r : recs) {
+    float t = 0.f;
+    LBF_HIP(hipEventElapsedTime(&t, pool[r.a], pool[r.b]));
+    if (size_t(r.id) >= ms.size()) {
+      ms.resize(r.id + 1, 0.0);
+      cnt.resize(r.id + 1, 0);
+    }
+    ms[r.id] += t;
+    cnt[r.id] += 1;
+  }
+  recs.clear();
+  used = 0;
+}
+
+void Ctx::set_device() const { LBF_HIP(hipSetDevice(device)); }
+
+void Ctx::allreduce(float *buf, size_t count) {
+  if (nranks <= 1 || !comm) return;
+  ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat, ncclSum, comm, stream);
+  if (r != ncclSuccess) throw Error(3, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Mlp
+// ------------------------------------------------------------------------------------------------
+Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
+  LBF_REQUIRE(nl >= 1 && nl <= 16, "1..16 layers");
+  size_t off = 0;
+  for (int l = 0; l < nl; ++l) {
+    LBF_REQUIRE(dims[l] > 0 && dims[l + 1] > 0, "layer dims must be positive");
+    LBF_REQUIRE(acts[l] >= 0 && acts[l] <= 3, "activation id 0..3");
+    Layer L;
+    L.in = dims[l];
+    L.out = dims[l + 1];
+    L.act = acts[l];
+    L.off = off;
+    off += size_t(L.in + 1) * L.out;
+    layers_.push_back(L);
+  }
+  nparams_ = off;
+}
+
+// Split-K plan of every dW GEMM for batch B: aim for ~512 workgroups (2 per CU) per GEMM, k chunks
+// a multiple of the 32-deep LDS tile.
+void Mlp::plan(long long B) {
+  if (planned_ == B) return;
+  size_t slab = 0;
+  for (auto &L : layers_) {
+    int BM, BN;
+    gemm_tile_for(L.out, &BM, &BN);
+    const long long M = L.in + 1;
+    const long long tiles = cdiv(M, BM) * cdiv(L.out, BN);
+    long long splits = std::max(1LL, std::min(cdiv(512, tiles), cdiv(B, 128)));
+    long long kc = cdiv(cdiv(B, splits), 32) * 32;
+    if (kc <= 0) kc = 32;
+    splits = std::max(1LL, cdiv(B, kc));
+    L.splits = int(splits);
+    L.k_chunk = int(kc);
+    if (splits > 1) slab = std::max(slab, size_t(splits) * size_t(M) * L.out);
+  }
+  slab_.ensure(slab);
+  planned_ = B;
+}
+
+void Mlp::ensure(long long B) {
+  if (B > cap_) {
+    A_.clear();
+    D_.clear();
+    for (auto &L : layers_) {
+      A_.emplace_back(size_t(std::max(1LL, B)) * L.out);
+      D_.emplace_back(size_t(std::max(1LL, B)) * L.out);
+    }
+    cap_ = B;
+  }
+  plan(B);
+  const int nl = int(layers_.size());
+  loss_part_.ensure(size_t(loss_partials_wg(std::max(1LL, B), layers_[nl - 1].out)));
+  dots_part_.ensure(size_t(dots_partials_wg(nparams_)) * 3);
+  sse_.ensure(1);
+}
+
+const float *Mlp::forward(const float *P, const float *X, const int *idx, long long B) {
+  ensure(B);
+  hipStream_t s = ctx_->stream;
+  const float *in = X;
+  for (size_t l = 0; l < layers_.size(); ++l) {
+    const Layer &L = layers_[l];
+    GemmDesc d;
+    d.M = int(B);
+    d.N = L.out;
+    d.K = L.in;
+    d.A = in;
+    d.lda = L.in;
+    d.a_kc = true;
+    d.a_idx = (l == 0) ? idx : nullptr;
+    d.B = P + L.off; // W as [In][Out] row-major (column-major Out x In)
+    d.ldb = L.out;
+    d.b_kc = false;
+    d.C = A_[l].get();
+    d.ldc = L.out;
+    d.epi = EPI_FWD;
+    d.bias = P + L.off + size_t(L.in) * L.out;
+    d.act = L.act;
+    ProfScope ps(ctx_, PK_FWD, int(l));
+    gemm(s, d);
+    in = A_[l].get();
+  }
+  return in;
+}
+
+void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
+                    double inv_scale, double lambda, const float *pdir, double *scal) {
+  forward(P, X, idx, B);
+  hipStream_t s = ctx_->stream;
+  const int nl = int(layers_.size());
+  const Layer &Lo = layers_[nl - 1];
+  const int nloss = loss_partials_wg(std::max(1LL, B), Lo.out);
+  {
+    ProfScope ps(ctx_, PK_LOSS);
+    loss_diff(s, A_[nl - 1].get(), Lo.out, Y, Lo.out, idx, B, Lo.out, Lo.act, inv_scale, D_[nl - 1].get(), Lo.out,
+              loss_part_.get());
+  }
+  for (int l = nl - 1; l >= 0; --l) {
+    const Layer &L = layers_[l];
+    const float *Ain = (l == 0) ? X : A_[l - 1].get();
+    // [dW ; db] = [A_in | 1]^T dZ  (layer.cuh:81-84 + sum_rows_kernel kernels.cuh:144-153)
+    GemmDesc d;
+    d.M = L.in + 1;
+    d.N = L.out;
+    d.K = int(B);
+    d.A = Ain;
+    d.lda = L.in;
+    d.a_kc = false;
+    d.a_idx = (l == 0) ? idx : nullptr;
+    d.a_mvalid = L.in;
+    d.a_ones = L.in;
+    d.B = D_[l].get();
+    d.ldb = L.out;
+    d.b_kc = false;
+    d.epi = EPI_STORE;
+    d.ldc = L.out;
+    d.splits = L.splits;
+    d.k_chunk = L.k_chunk;
+    const long long seg = (long long)(L.in + 1) * L.out;
+    if (L.splits > 1) {
+      d.C = slab_.get();
+      d.slab_stride = seg;
+      {
+        ProfScope ps(ctx_, PK_DW, l);
+        gemm(s, d);
+      }
+      ProfScope ps(ctx_, PK_SLAB, l);
+      reduce_slabs(s, slab_.get(), L.splits, seg, seg, G + L.off);
+    } else {
+      d.C = G + L.off;
+      ProfScope ps(ctx_, PK_DW, l);
+      gemm(s, d);
+    }
+    if (l > 0) {
+      // dX = dZ W^T .* act'(A_prev)   (layer.cuh:89-103 fused with activation_deriv of layer l-1)
+      const Layer &P0 = layers_[l - 1];
+      GemmDesc x;
+      x.M = int(B);
+      x.N = L.in;
+      x.K = L.out;
+      x.A = D_[l].get();
+      x.lda = L.out;
+      x.a_kc = true;
+      x.B = P + L.off; // B[n=i][k=o] = W[i][o]
+      x.ldb = L.out;
+      x.b_kc = true;
+      x.C = D_[l - 1].get();
+      x.ldc = L.in;
+      x.epi = EPI_DX;
+      x.aux = A_[l - 1].get();
+      x.ldaux = L.in;
+      x.aux_act = P0.act;
+      ProfScope ps(ctx_, PK_DX, l);
+      gemm(s, x);
+    }
+  }
+  const float *hilo = nullptr;
+  {
+    ProfScope ps(ctx_, PK_FINAL, 0);
+    reduce_rows(s, loss_part_.get(), nloss, 1, sse_.get());
+    if (ctx_->nranks > 1) pack_hilo(s, sse_.get(), G + nparams_);
+  }
+  if (ctx_->nranks > 1) {
+    ProfScope ps(ctx_, PK_ALLREDUCE);
+    ctx_->allreduce(G, nparams_ + 2);
+    hilo = G + nparams_;
+  }
+  {
+    ProfScope ps(ctx_, PK_FINAL, 1);
+    const int nd = dots_partials_wg(nparams_);
+    finalize_grad_dots(s, nparams_, G, P, lambda, pdir, dots_part_.get());
+    reduce_rows(s, dots_part_.get(), nd, 3, scal + SC_TGG);
+    eval_status(s, sse_.get(), hilo, inv_scale, lambda, scal);
+  }
+  ++evals_;
+}
+
+// ------------------------------------------------------------------------------------------------
+// History
+// ------------------------------------------------------------------------------------------------
+History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
+  LBF_REQUIRE(m >= 0 && m <= 128, "history size m must be in [0, 128]");
+  const int slots = m + 1;
+  const long long ld = cdiv(n, 4) * 4;
+  S_.resize(size_t(slots) * ld);
+  Y_.resize(size_t(slots) * ld);
+  ist_.resize(IST_ORDER + slots + 4);
+  // dstate: rho | SS | SY | YY | gS | gY | coef(2*slots+1) | scal
+  const size_t nd = slots + 3 * size_t(slots) * slots + 2 * slots + (2 * slots + 1) + SC_N;
+  dstate_.resize(nd);
+  part_.resize(size_t(gram_nwg(n)) * gram_ncols(m));
+  red_.resize(size_t(gram_ncols(m)));
+  v_.m = m;
+  v_.slots = slots;
+  v_.n = n;
+  v_.ld = ld;
+  v_.S = S_.get();
+  v_.Y = Y_.get();
+  v_.ist = ist_.get();
+  double *p = dstate_.get();
+  v_.rho = p;
+  p += slots;
+  v_.SS = p;
+  p += size_t(slots) * slots;
+  v_.SY = p;
+  p += size_t(slots) * slots;
+  v_.YY = p;
+  p += size_t(slots) * slots;
+  v_.gS = p;
+  p += slots;
+  v_.gY = p;
+  p += slots;
+  v_.coef = p;
+  p += 2 * slots + 1;
+  v_.scal = p;
+  LBF_HIP(hipMemsetAsync(ist_.get(), 0, ist_.size() * sizeof(int), ctx_->stream));
+  LBF_HIP(hipMemsetAsync(dstate_.get(), 0, dstate_.size() * sizeof(double), ctx_->stream));
+  // the ring vectors are only ever read for live slots, but keep them defined
+  LBF_HIP(hipMemsetAsync(S_.get(), 0, S_.size() * sizeof(float), ctx_->stream));
+  LBF_HIP(hipMemsetAsync(Y_.get(), 0, Y_.size() * sizeof(float), ctx_->stream));
+}
+
+void History::reset() { hist_reset(ctx_->stream, v_); }
+
+void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
+  GramArgs g = g0;
+  g.h = v_;
+  hipStream_t s = ctx_->stream;
+  {
+    ProfScope ps(ctx_, PK_GRAM);
+    gram_update(s, g, part_.get());
+    reduce_rows(s, part_.get(), gram_nwg(v_.n), gram_ncols(v_.m), red_.get());
+  }
+  CoefArgs c;
+  c.h = v_;
+  c.dots = red_.get();
+  c.has_pair = g.has_pair;
+  c.has_g = g.has_g;
+  c.reset = g.reset;
+  c.policy = g.policy;
+  c.want_dir = want_dir;
+  c.iter = iter;
+  c.dsign = dsign;
+  ProfScope ps(ctx_, PK_COEF);
+  hist_coef(s, c);
+}
+
+void History::combine(const float *g, float *dir, const float *x_in, float *x_out, float *x_out2,
+                      bool alpha_from_state, double alpha) {
+  CombineArgs a;
+  a.h = v_;
+  a.g = g;
+  a.dir = dir;
+  a.x_in = x_in;
+  a.x_out = x_out;
+  a.x_out2 = x_out2;
+  a.alpha_from_state = alpha_from_state ? 1 : 0;
+  a.alpha = alpha;
+  ProfScope ps(ctx_, PK_COMBINE);
+  hist_combine(ctx_->stream, a);
+}
+
+} // namespace lbf

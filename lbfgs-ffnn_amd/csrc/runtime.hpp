@@ -1,0 +1,124 @@
+// Host runtime of liblbfgs_amd.so: context (device, stream, RCCL communicator), the MLP evaluation
+// plan, the device-resident L-BFGS history, and the solver drivers.
+#pragma once
+
+#include "internal.hpp"
+#include "kernels.hpp"
+
+#include <rccl/rccl.h>
+
+#include <memory>
+#include <vector>
+
+namespace lbf {
+
+// Per-kernel-class timing with HIP events on the launch stream (enabled by the benchmark only).
+enum ProfKind : int { PK_FWD = 0, PK_DW = 1, PK_DX = 2, PK_LOSS = 3, PK_SLAB = 4, PK_FINAL = 5, PK_GRAM = 6,
+                      PK_COEF = 7, PK_COMBINE = 8, PK_AXPY = 9, PK_ALLREDUCE = 10 };
+struct Profiler {
+  bool on = false;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  struct Rec { int id; size_t a, b; };
+  std::vector<Rec> recs;
+  std::vector<double> ms;      // by section id
+  std::vector<long long> cnt;  // by section id
+  ~Profiler();
+  size_t mark(hipStream_t s);
+  void resolve();
+};
+
+struct Ctx {
+  int device = 0;
+  Profiler prof;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  ncclComm_t comm = nullptr;
+  int rank = 0, nranks = 1;
+  // scratch for the BLAS-1 ABI helpers
+  DevBuf<double> part, red;
+  PinnedBuf<double> host;
+  ~Ctx();
+  void set_device() const;
+  void allreduce(float *buf, size_t count);
+};
+
+struct Layer {
+  int in, out, act;
+  size_t off;      // flat offset of the [(in+1) x out] segment
+  int splits = 1;  // split-K factor of the dW GEMM at the planned batch
+  int k_chunk = 0;
+};
+
+// RAII section: records an event pair around the enclosed launches when profiling is on.
+struct ProfScope {
+  Ctx *c;
+  int id;
+  size_t a = 0;
+  ProfScope(Ctx *ctx, int kind, int layer = 0) : c(ctx), id(kind * 16 + layer) {
+    if (c->prof.on) a = c->prof.mark(c->stream);
+  }
+  ~ProfScope() {
+    if (c->prof.on) c->prof.recs.push_back({id, a, c->prof.mark(c->stream)});
+  }
+};
+
+// Dense MLP (the reference's CudaNetwork, src/cuda/network.cuh:21-158) with a cached workspace.
+class Mlp {
+public:
+  Mlp(Ctx *ctx, int nl, const int *dims, const int *acts);
+  size_t nparams() const { return nparams_; }
+  const std::vector<Layer> &layers() const { return layers_; }
+  Ctx *ctx() const { return ctx_; }
+
+  // Forward only: activations of every layer into the workspace; returns the output buffer.
+  const float *forward(const float *P, const float *X, const int *idx, long long B);
+  // Fused loss + gradient (+ all-reduce over the communicator) + line-search dots.
+  //   G    : gradient output, must hold nparams()+2 floats (two extra words carry the loss for the
+  //          all-reduce).
+  //   pdir : optional direction for the g.p dot.
+  //   scal : device fp64 status block (SC_LOSS, SC_TGG, SC_TGP, SC_WW, SC_SSE written).
+  void loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
+                 double inv_scale, double lambda, const float *pdir, double *scal);
+  long long evals() const { return evals_; }
+
+private:
+  void ensure(long long B);
+  Ctx *ctx_;
+  std::vector<Layer> layers_;
+  size_t nparams_ = 0;
+  long long cap_ = -1, planned_ = -1;
+  std::vector<DevBuf<float>> A_, D_;
+  DevBuf<float> slab_;
+  DevBuf<double> loss_part_, dots_part_, sse_;
+  long long evals_ = 0;
+  void plan(long long B);
+};
+
+// Device-resident history of (s, y) pairs and its fp64 Gram state.
+class History {
+public:
+  History(Ctx *ctx, int m, long long n);
+  HistView view() const { return v_; }
+  void reset();
+  // Gram sweep + bookkeeping (+ direction coefficients when want_dir > 0).
+  void update(const GramArgs &g, int want_dir, int iter, double dsign);
+  void combine(const float *g, float *dir, const float *x_in, float *x_out, float *x_out2, bool alpha_from_state,
+               double alpha);
+  double *scal() const { return v_.scal; }
+  int m() const { return v_.m; }
+
+private:
+  Ctx *ctx_;
+  HistView v_;
+  DevBuf<float> S_, Y_;
+  DevBuf<int> ist_;
+  DevBuf<double> dstate_, part_, red_;
+};
+
+struct LbfgsRecordRow {
+  double loss, gnorm, time_ms, alpha;
+  int trials, accepted;
+};
+
+} // namespace lbf

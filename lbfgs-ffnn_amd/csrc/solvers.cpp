@@ -1,0 +1,458 @@
+// L-BFGS / S-LBFGS drivers (see solvers.hpp).
+#include "solvers.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <numeric>
+
+namespace lbf {
+
+namespace {
+long long round4(long long n) { return cdiv(n, 4) * 4; }
+} // namespace
+
+std::vector<size_t> sample_minibatch(size_t N, size_t b, std::mt19937 &rng) {
+  // s_lbfgs.hpp:141-160: partial Fisher-Yates over iota(N), uniform_int_distribution<size_t>(i, N-1).
+  if (N == 0 || b == 0) return {};
+  std::vector<size_t> idx(N);
+  std::iota(idx.begin(), idx.end(), 0);
+  if (b >= N) return idx;
+  for (size_t i = 0; i < b; ++i) {
+    std::uniform_int_distribution<size_t> dist(i, N - 1);
+    size_t j = dist(rng);
+    std::swap(idx[i], idx[j]);
+  }
+  idx.resize(b);
+  return idx;
+}
+
+// ================================================================================================
+// Full-batch L-BFGS
+// ================================================================================================
+LbfgsSolver::LbfgsSolver(Mlp *net, const lbf_lbfgs_params &prm, float *d_params, const float *X, const float *Y,
+                         long long n_local, long long n_global)
+    : net_(net), ctx_(net->ctx()), prm_(prm), user_params_(d_params), X_(X), Y_(Y), nloc_(n_local),
+      nglob_(n_global), n_((long long)net->nparams()), hist_(net->ctx(), prm.m, (long long)net->nparams()) {
+  LBF_REQUIRE(d_params && X && Y, "null pointer");
+  LBF_REQUIRE(n_local >= 0 && n_global > 0, "batch sizes");
+  LBF_REQUIRE(prm.max_line_iters >= 1, "max_line_iters >= 1");
+  for (int i = 0; i < 3; ++i) {
+    xbuf_[i].resize(size_t(round4(n_)));
+    gbuf_[i].resize(size_t(round4(n_ + 2)));
+  }
+  p_.resize(size_t(round4(n_)));
+  x_ = xbuf_[0].get();
+  xp_ = xbuf_[1].get();
+  xt_ = xbuf_[2].get();
+  g_ = gbuf_[0].get();
+  gp_ = gbuf_[1].get();
+  gt_ = gbuf_[2].get();
+  hs_.ensure(SC_N);
+  LBF_HIP(hipMemcpyAsync(x_, d_params, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, ctx_->stream));
+  // initial evaluation (lbfgs.hpp:44 / lbfgs.cuh:147)
+  eval(x_, g_, nullptr);
+  read_status();
+  loss_ = hs_[SC_LOSS];
+  lossf_ = float(loss_);
+  gg_ = hs_[SC_TGG];
+  t0_ = std::chrono::steady_clock::now();
+}
+
+void LbfgsSolver::eval(const float *x, float *g, const float *pdir) {
+  net_->loss_grad(x, g, X_, Y_, nullptr, nloc_, 1.0 / double(nglob_), 0.0, pdir, hist_.scal());
+}
+
+void LbfgsSolver::read_status() {
+  LBF_HIP(hipMemcpyAsync(hs_.get(), hist_.scal(), SC_N * sizeof(double), hipMemcpyDeviceToHost, ctx_->stream));
+  LBF_HIP(hipStreamSynchronize(ctx_->stream));
+}
+
+void LbfgsSolver::writeback() {
+  LBF_HIP(hipMemcpyAsync(user_params_, x_, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, ctx_->stream));
+  LBF_HIP(hipStreamSynchronize(ctx_->stream));
+}
+
+void LbfgsSolver::record(lbf_record *rec, double loss, double gnorm, double alpha, int trials, int accepted) {
+  if (!rec) return;
+  const int i = rec_idx_++;
+  if (i >= rec->cap) return;
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0_).count();
+  if (rec->loss) rec->loss[i] = loss;
+  if (rec->grad_norm) rec->grad_norm[i] = gnorm;
+  if (rec->time_ms) rec->time_ms[i] = ms;
+  if (rec->alpha) rec->alpha[i] = alpha;
+  if (rec->ls_trials) rec->ls_trials[i] = trials;
+  if (rec->accepted) rec->accepted[i] = accepted;
+  rec->size = std::max(rec->size, i + 1);
+}
+
+int LbfgsSolver::iterate(int iters, lbf_record *rec) {
+  ctx_->set_device();
+  rec_idx_ = rec ? rec->size : 0;
+  const int done = prm_.line_search == LBF_LS_ARMIJO ? iterate_armijo(iters, rec) : iterate_wolfe(iters, rec);
+  writeback();
+  return done;
+}
+
+// CPU semantics: LBFGS::solve (lbfgs.hpp:38-100) + FullBatchMinimizer::line_search
+// (full_batch_minimizer.hpp:126-157). Every f / Gradient call of the reference maps to a cached
+// fused evaluation: line_search's f(x), Gradient(x) are the previous accepted trial, the trial's
+// Gradient(x+ap) comes with its f, the post-search Gradient(x_new) and the recorder's f(x) are the
+// accepted trial's. Only an exhausted search (returns an alpha it never evaluated) costs one more.
+int LbfgsSolver::iterate_wolfe(int iters, lbf_record *rec) {
+  const double inf = std::numeric_limits<double>::infinity();
+  int k = 0;
+  for (; k < iters; ++k) {
+    if (std::sqrt(gg_) < prm_.tol) {
+      converged_ = true;
+      break;
+    }
+    GramArgs ga;
+    ga.policy = POL_CPU;
+    ga.has_g = 1;
+    ga.ga = g_;
+    if (pending_pair_) {
+      ga.has_pair = 1;
+      ga.sa = x_;
+      ga.sb = xp_;
+      ga.ya = g_;
+      ga.yb = gp_;
+    }
+    hist_.update(ga, 1, iter_, -1.0);
+    hist_.combine(g_, p_.get(), x_, xt_, nullptr, true, 0.0); // xt = x + alpha0 p
+    eval(xt_, gt_, p_.get());
+    read_status();
+    if (pending_pair_ && rec && rec->accepted && rec_idx_ > 0 && rec_idx_ - 1 < rec->cap)
+      rec->accepted[rec_idx_ - 1] = int(hs_[SC_ACCEPT]);
+    double alpha = hs_[SC_ALPHA0];
+    int trials = 0;
+    if (iter_ > 0) {
+      const double f_old = loss_, gfo = hs_[SC_GTP];
+      double amin = 0.0, amax = inf;
+      alpha = 1.0;
+      bool evaluated = true;
+      for (int i = 0; i < prm_.max_line_iters; ++i) {
+        if (!evaluated) {
+          {
+            ProfScope ps(ctx_, PK_AXPY);
+            axpy_to(ctx_->stream, n_, x_, float(alpha), p_.get(), xt_);
+          }
+          eval(xt_, gt_, p_.get());
+          read_status();
+          evaluated = true;
+        }
+        ++trials;
+        const double fn = hs_[SC_LOSS];
+        if (fn > f_old + prm_.c1 * alpha * gfo) {
+          amax = alpha;
+          alpha = prm_.rho * (amin + amax);
+          evaluated = false;
+          continue;
+        }
+        const double gnp = hs_[SC_TGP];
+        if (gnp < prm_.c2 * gfo) {
+          amin = alpha;
+          alpha = (amax == inf) ? alpha * 2 : prm_.rho * (amin + amax);
+          evaluated = false;
+          continue;
+        }
+        break;
+      }
+      if (!evaluated) { // exhausted: the returned alpha was never evaluated (lbfgs.hpp:67-70)
+        axpy_to(ctx_->stream, n_, x_, float(alpha), p_.get(), xt_);
+        eval(xt_, gt_, p_.get());
+        read_status();
+      }
+    }
+    std::swap(xp_, x_);
+    std::swap(x_, xt_); // x <- trial, xp <- old x, xt <- free
+    std::swap(gp_, g_);
+    std::swap(g_, gt_);
+    loss_ = hs_[SC_LOSS];
+    gg_ = hs_[SC_TGG];
+    pending_pair_ = prm_.m > 0;
+    record(rec, loss_, std::sqrt(gg_), alpha, trials, -1);
+    ++iter_;
+  }
+  return k;
+}
+
+// CUDA semantics: CudaLBFGS::solve (lbfgs.cuh:39-194), host scalars in fp32 like the reference.
+int LbfgsSolver::iterate_armijo(int iters, lbf_record *rec) {
+  int k = 0;
+  const float c1 = float(prm_.c1), rho = float(prm_.rho);
+  for (; k < iters; ++k) {
+    const float gnorm = float(std::sqrt(gg_));
+    if (gnorm < float(prm_.tol)) {
+      converged_ = true;
+      break;
+    }
+    GramArgs ga;
+    ga.policy = POL_CUDA;
+    ga.has_g = 1;
+    ga.ga = g_;
+    ga.reset = pending_reset_ ? 1 : 0;
+    if (pending_pair_) {
+      ga.has_pair = 1;
+      ga.sa = x_;
+      ga.sb = xp_;
+      ga.ya = g_;
+      ga.yb = gp_;
+    }
+    hist_.update(ga, 1, iter_, -1.0);
+    float alpha = (iter_ == 0) ? std::min(1.0f, 1.0f / gnorm) : 1.0f;
+    hist_.combine(g_, p_.get(), x_, xt_, nullptr, false, double(alpha));
+    eval(xt_, gt_, p_.get());
+    read_status();
+    if (pending_pair_ && rec && rec->accepted && rec_idx_ > 0 && rec_idx_ - 1 < rec->cap)
+      rec->accepted[rec_idx_ - 1] = int(hs_[SC_ACCEPT]);
+    const float gdp = float(hs_[SC_GTP]);
+    bool ok = false;
+    int trials = 0;
+    float lnew = 0.f, a_eval = alpha;
+    for (int ls = 0; ls < prm_.max_line_iters; ++ls) {
+      if (ls > 0) {
+        axpy_to(ctx_->stream, n_, x_, alpha, p_.get(), xt_);
+        eval(xt_, gt_, p_.get());
+        read_status();
+      }
+      ++trials;
+      a_eval = alpha;
+      lnew = float(hs_[SC_LOSS]);
+      if (lnew <= lossf_ + c1 * alpha * gdp) {
+        ok = true;
+        break;
+      }
+      const float den = 2.0f * (lnew - lossf_ - gdp * alpha);
+      bool fb = true;
+      if (std::fabs(den) > 1e-20f) {
+        const float na = -(gdp * alpha * alpha) / den;
+        if (na >= 0.1f * alpha && na <= 0.9f * alpha) {
+          alpha = na;
+          fb = false;
+        }
+      }
+      if (fb) alpha *= rho;
+    }
+    pending_reset_ = !ok; // lbfgs.cuh:147
+    std::swap(xp_, x_);
+    std::swap(x_, xt_);
+    std::swap(gp_, g_);
+    std::swap(g_, gt_);
+    lossf_ = lnew;
+    loss_ = hs_[SC_LOSS];
+    gg_ = hs_[SC_TGG];
+    pending_pair_ = prm_.m > 0;
+    record(rec, double(lnew), double(float(std::sqrt(gg_))), double(a_eval), trials, -1);
+    ++iter_;
+  }
+  return k;
+}
+
+void LbfgsSolver::info(lbf_solve_info *out) const {
+  if (!out) return;
+  out->iterations = iter_;
+  out->n_evals = net_->evals();
+  out->final_loss = loss_;
+  out->final_grad_norm = std::sqrt(gg_);
+}
+
+// ================================================================================================
+// S-LBFGS
+// ================================================================================================
+SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_params, const float *X, const float *Y,
+                           long long N)
+    : net_(net), ctx_(net->ctx()), prm_(prm), user_params_(d_params), X_(X), Y_(Y), N_(N),
+      n_((long long)net->nparams()), hist_(net->ctx(), prm.M, (long long)net->nparams()) {
+  LBF_REQUIRE(d_params && X && Y && N > 0, "null pointer / empty data");
+  LBF_REQUIRE(prm.b > 0 && prm.L > 0 && prm.L + 1 <= 64, "b > 0, 1 <= L <= 63");
+  const size_t nv = size_t(round4(n_)), ng = size_t(round4(n_ + 2));
+  w_.resize(nv);
+  wt_.resize(nv);
+  v_.resize(nv);
+  r_.resize(nv);
+  u_.resize(nv);
+  up_.resize(nv);
+  s_.resize(nv);
+  wp_.resize(nv);
+  wm_.resize(nv);
+  mu_.resize(ng);
+  g1_.resize(ng);
+  g2_.resize(ng);
+  gp_.resize(ng);
+  gm_.resize(ng);
+  wh_.resize(nv * size_t(prm.L + 1));
+  hs_.ensure(SC_N);
+}
+
+void SlbfgsSolver::eval_batch(const float *w, float *g, const int *d_idx, long long count, const float *pdir) {
+  (void)pdir;
+  net_->loss_grad(w, g, X_, Y_, d_idx, count, 1.0, prm_.lambda, nullptr, hist_.scal());
+}
+
+// SLBFGS::stochastic_solve (s_lbfgs.hpp:165-290) with the UnifiedSLBFGS_CPU closures
+// (unified_optimization.hpp:343-400). The host RNG stream is consumed in exactly the reference's
+// order; because no sample depends on device values, each epoch's index lists are drawn up front
+// and uploaded once, and the epoch then runs without a host synchronisation.
+int SlbfgsSolver::run(lbf_record *rec) {
+  ctx_->set_device();
+  hipStream_t s = ctx_->stream;
+  const int nr = ctx_->nranks, rk = ctx_->rank;
+  const long long In = net_->layers().front().in, Out = net_->layers().back().out;
+  const long long ld = round4(n_);
+  const int m_inner = int(std::max(1LL, N_ / prm_.b));
+  const int L = prm_.L;
+  std::mt19937 rng(prm_.seed);
+  LBF_HIP(hipMemcpyAsync(w_.get(), user_params_, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+  // full-batch shard of this rank
+  const long long lo = N_ * rk / nr, hi = N_ * (rk + 1) / nr;
+  const float *Xs = X_ + lo * In, *Ys = Y_ + lo * Out;
+  const double inv_full = 1.0 / double(N_);
+  auto eval_full = [&](const float *w, float *g) {
+    net_->loss_grad(w, g, Xs, Ys, nullptr, hi - lo, inv_full, prm_.lambda, nullptr, hist_.scal());
+  };
+  auto read = [&]() {
+    LBF_HIP(hipMemcpyAsync(hs_.get(), hist_.scal(), SC_N * sizeof(double), hipMemcpyDeviceToHost, s));
+    LBF_HIP(hipStreamSynchronize(s));
+  };
+  bool have_u = false, mu_valid = false;
+  const auto t0 = std::chrono::steady_clock::now();
+  int rec_i = rec ? rec->size : 0;
+  iters_ = 0;
+  while (iters_ < prm_.max_epochs) {
+    if (!mu_valid) {
+      eval_full(w_.get(), mu_.get());
+      read();
+    }
+    if (std::sqrt(hs_[SC_TGG]) < prm_.tol) break; // s_lbfgs.hpp:208
+    // --- draw this epoch's samples in reference order -------------------------------------------
+    std::vector<int> flat;
+    std::vector<std::pair<long long, long long>> mb(m_inner), hb(m_inner, {-1, 0});
+    bool u_seen = have_u;
+    int whist_size = 1;
+    for (int t = 0; t < m_inner; ++t) {
+      auto v = sample_minibatch(size_t(N_), size_t(prm_.b), rng);
+      mb[t] = {(long long)flat.size(), (long long)v.size()};
+      for (size_t x : v) flat.push_back(int(x));
+      whist_size = std::min(whist_size + 1, L + 1);
+      if (t > 0 && t % L == 0) {
+        if (u_seen) {
+          auto h = sample_minibatch(size_t(N_), size_t(prm_.b_H), rng);
+          hb[t] = {(long long)flat.size(), (long long)h.size()};
+          for (size_t x : h) flat.push_back(int(x));
+        }
+        u_seen = true;
+      }
+    }
+    int pick = -1;
+    if (whist_size >= 2) {
+      std::uniform_int_distribution<size_t> pk(0, size_t(whist_size) - 2); // s_lbfgs.hpp:266
+      pick = int(pk(rng));
+    }
+    idx_.ensure(std::max<size_t>(1, flat.size()));
+    if (!flat.empty())
+      LBF_HIP(hipMemcpyAsync(idx_.get(), flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    LBF_HIP(hipStreamSynchronize(s)); // flat is a pageable temporary
+    // --- epoch -----------------------------------------------------------------------------------
+    LBF_HIP(hipMemcpyAsync(wt_.get(), w_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+    int wh_head = 0, wh_count = 0; // ring of L+1 iterates (w_history)
+    auto wh_slot = [&](int logical) { return (wh_head + logical) % (L + 1); };
+    auto wh_push_slot = [&]() {
+      int slot;
+      if (wh_count < L + 1) {
+        slot = (wh_head + wh_count) % (L + 1);
+        ++wh_count;
+      } else {
+        slot = wh_head;
+        wh_head = (wh_head + 1) % (L + 1);
+      }
+      return slot;
+    };
+    {
+      const int slot = wh_push_slot();
+      LBF_HIP(hipMemcpyAsync(wh_.get() + slot * ld, wt_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice,
+                             s));
+    }
+    for (int t = 0; t < m_inner; ++t) {
+      const long long b = mb[t].second;
+      const long long o = mb[t].first + b * rk / nr, c = b * (rk + 1) / nr - b * rk / nr;
+      net_->loss_grad(wt_.get(), g1_.get(), X_, Y_, idx_.get() + o, c, 1.0 / double(b), prm_.lambda, nullptr,
+                      hist_.scal());
+      net_->loss_grad(w_.get(), g2_.get(), X_, Y_, idx_.get() + o, c, 1.0 / double(b), prm_.lambda, nullptr,
+                      hist_.scal());
+      GramArgs ga;
+      ga.policy = POL_SLBFGS;
+      ga.has_g = 1;
+      ga.ga = g1_.get();
+      ga.gb = g2_.get();
+      ga.gc = mu_.get();
+      ga.g_out = v_.get();
+      hist_.update(ga, 1, 1, +1.0);
+      const int slot = wh_push_slot();
+      // wt = wt - step * r ; w_history.push_back(wt)
+      hist_.combine(v_.get(), nullptr, wt_.get(), wt_.get(), wh_.get() + slot * ld, false, -prm_.step);
+      if (t > 0 && t % L == 0) {
+        int slots[64];
+        for (int i = 0; i < wh_count; ++i) slots[i] = wh_slot(i);
+        average_slots(s, n_, wh_.get(), ld, slots, wh_count, u_.get());
+        if (have_u) {
+          const long long hbn = hb[t].second;
+          const long long ho = hb[t].first + hbn * rk / nr, hc = hbn * (rk + 1) / nr - hbn * rk / nr;
+          const double eps = prm_.fd_eps;
+          lincomb(s, n_, u_.get(), -1.0, up_.get(), s_.get()); // s = u - u_prev
+          lincomb(s, n_, u_.get(), eps, s_.get(), wp_.get());
+          lincomb(s, n_, u_.get(), -eps, s_.get(), wm_.get());
+          net_->loss_grad(wp_.get(), gp_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda, nullptr,
+                          hist_.scal());
+          net_->loss_grad(wm_.get(), gm_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda, nullptr,
+                          hist_.scal());
+          GramArgs pa;
+          pa.policy = POL_SLBFGS;
+          pa.has_pair = 1;
+          pa.sa = u_.get();
+          pa.sb = up_.get();
+          pa.ya = gp_.get();
+          pa.yb = gm_.get();
+          pa.yscale = 1.0 / (2.0 * eps);
+          hist_.update(pa, 0, 1, +1.0);
+        }
+        LBF_HIP(hipMemcpyAsync(up_.get(), u_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+        have_u = true;
+      }
+    }
+    // anchor reset (s_lbfgs.hpp:265-270)
+    const float *anchor = pick >= 0 ? wh_.get() + wh_slot(pick) * ld : wt_.get();
+    LBF_HIP(hipMemcpyAsync(w_.get(), anchor, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+    // recorder (s_lbfgs.hpp:274-284): full loss and gradient at the new anchor == next epoch's mu
+    eval_full(w_.get(), mu_.get());
+    read();
+    mu_valid = true;
+    last_loss_ = hs_[SC_LOSS];
+    last_gnorm_ = std::sqrt(hs_[SC_TGG]);
+    if (rec && rec_i < rec->cap) {
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      if (rec->loss) rec->loss[rec_i] = last_loss_;
+      if (rec->grad_norm) rec->grad_norm[rec_i] = last_gnorm_;
+      if (rec->time_ms) rec->time_ms[rec_i] = ms;
+      if (rec->alpha) rec->alpha[rec_i] = prm_.step;
+      if (rec->ls_trials) rec->ls_trials[rec_i] = 0;
+      if (rec->accepted) rec->accepted[rec_i] = int(hs_[SC_COUNT]);
+      rec->size = std::max(rec->size, ++rec_i);
+    }
+    ++iters_;
+  }
+  LBF_HIP(hipMemcpyAsync(user_params_, w_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+  LBF_HIP(hipStreamSynchronize(s));
+  return iters_;
+}
+
+void SlbfgsSolver::info(lbf_solve_info *out) const {
+  if (!out) return;
+  out->iterations = iters_;
+  out->n_evals = net_->evals();
+  out->final_loss = last_loss_;
+  out->final_grad_norm = last_gnorm_;
+}
+
+} // namespace lbf

@@ -1,0 +1,708 @@
+// Memory-bound kernels of the L-BFGS step (gfx950, wave64): the MSE output layer, split-K slab
+// reduction, deterministic fp64 dot reductions, and the device-resident history (Gram sweep,
+// coefficient two-loop, linear-combination sweep).
+//
+// Replaces: diff_kernel / sum_rows_kernel (src/cuda/kernels.cuh:136-153), cublasSdot / Snrm2 / Saxpy /
+// Sscal with host pointer mode (kernels.cuh:28-50, every scalar a blocking device->host copy), and
+// CudaLBFGS::compute_direction_ring (src/cuda/lbfgs.cuh:206-261, 2k+2 blocking dots + 2k axpys).
+#include "internal.hpp"
+#include "kernels.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace lbf {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------------
+// wave / block reductions (fixed butterfly order -> bitwise reproducible)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Sum NV values over a 256- or 512-thread block; result valid in thread 0. scratch: NV*16 doubles.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double *scratch) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) scratch[i * 16 + wave] = v[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      double s = 0.0;
+      for (int w = 0; w < nw; ++w) s += scratch[i * 16 + w];
+      v[i] = s;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float act_deriv_out(int a, float y) {
+  switch (a) {
+  case ACT_TANH: return 1.0f - y * y;
+  case ACT_RELU: return y > 0.0f ? 1.0f : 0.0f;
+  case ACT_SIGMOID: return y * (1.0f - y);
+  default: return 1.0f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// reduce_rows: out[c] = sum_r P[r][c]   (one wave per column, lane-strided then butterfly)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const double *P, int nrows, int ncols, double *out) {
+  const int col = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (col >= ncols) return;
+  double s = 0.0;
+  for (int r = lane; r < nrows; r += 64) s += P[(long long)r * ncols + col];
+  s = wave_sum(s);
+  if (lane == 0) out[col] = s;
+}
+
+void reduce_rows(hipStream_t s, const double *P, int nrows, int ncols, double *out) {
+  if (ncols <= 0) return;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((ncols + 3) / 4), dim3(256), 0, s, P, nrows, ncols, out);
+  LBF_KERNEL_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Output layer: diff = A_out - Y ; dZ = diff * act'(A_out) * inv_scale ; partial sum(diff^2).
+// src/cuda/network.cuh:97-107 (diff, 0.5*dot(diff,diff)/B, diff*=1/B) and layer.cuh:72 (act').
+// ---------------------------------------------------------------------------------------------
+int loss_partials_wg(long long B, int Out) {
+  long long e = B * Out;
+  long long w = cdiv(e, 256 * 8);
+  return int(w < 1 ? 1 : (w > 1024 ? 1024 : w));
+}
+
+__global__ __launch_bounds__(256) void loss_diff_kernel(const float *A, long long lda, const float *Y, long long ldy,
+                                                        const int *idx, long long B, int Out, int act,
+                                                        double inv_scale, float *dZ, long long ldz,
+                                                        double *partials) {
+  __shared__ double scratch[16];
+  const long long total = B * Out;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  double acc[1] = {0.0};
+  const float sc = float(inv_scale);
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const long long b = e / Out;
+    const int o = int(e - b * Out);
+    const float a = A[b * lda + o];
+    const long long yr = idx ? (long long)idx[b] : b;
+    const float d = a - Y[yr * ldy + o];
+    acc[0] += double(d) * double(d);
+    dZ[b * ldz + o] = d * act_deriv_out(act, a) * sc;
+  }
+  block_sum<1>(acc, scratch);
+  if (threadIdx.x == 0) partials[blockIdx.x] = acc[0];
+}
+
+void loss_diff(hipStream_t s, const float *Aout, long long lda, const float *Y, long long ldy, const int *idx,
+               long long B, int Out, int act, double inv_scale, float *dZ, long long ldz, double *partials) {
+  hipLaunchKernelGGL(loss_diff_kernel, dim3(loss_partials_wg(B, Out)), dim3(256), 0, s, Aout, lda, Y, ldy, idx, B,
+                     Out, act, inv_scale, dZ, ldz, partials);
+  LBF_KERNEL_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// split-K slab reduction -> flat gradient segment
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float *slab, int splits, long long stride,
+                                                           long long count, float *grad) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  double s = 0.0;
+  for (int k = 0; k < splits; ++k) s += double(slab[k * stride + e]);
+  grad[e] = float(s);
+}
+
+void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride, long long count, float *grad) {
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(unsigned(cdiv(count, 256))), dim3(256), 0, s, slab, splits, stride,
+                     count, grad);
+  LBF_KERNEL_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// finalize: g += lambda*w (S-LBFGS L2 term, unified_optimization.hpp:375) ; partial (g.g, g.p, w.w)
+// ---------------------------------------------------------------------------------------------
+int dots_partials_wg(long long n) {
+  long long w = cdiv(n, 256 * 8);
+  return int(w < 1 ? 1 : (w > 512 ? 512 : w));
+}
+
+__global__ __launch_bounds__(256) void finalize_kernel(long long n, float *g, const float *w, double lambda,
+                                                       const float *p, double *partials) {
+  __shared__ double scratch[48];
+  double acc[3] = {0.0, 0.0, 0.0};
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float lf = float(lambda);
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    float gv = g[e];
+    const float wv = w ? w[e] : 0.0f;
+    if (lambda != 0.0) {
+      gv = gv + lf * wv;
+      g[e] = gv;
+    }
+    acc[0] += double(gv) * double(gv);
+    if (p) acc[1] += double(gv) * double(p[e]);
+    acc[2] += double(wv) * double(wv);
+  }
+  block_sum<3>(acc, scratch);
+  if (threadIdx.x == 0) {
+    partials[blockIdx.x * 3 + 0] = acc[0];
+    partials[blockIdx.x * 3 + 1] = acc[1];
+    partials[blockIdx.x * 3 + 2] = acc[2];
+  }
+}
+
+void finalize_grad_dots(hipStream_t s, long long n, float *g, const float *w, double lambda, const float *p,
+                        double *partials) {
+  hipLaunchKernelGGL(finalize_kernel, dim3(dots_partials_wg(n)), dim3(256), 0, s, n, g, w, lambda, p, partials);
+  LBF_KERNEL_CHECK();
+}
+
+__global__ __launch_bounds__(256) void dot_kernel(long long n, const float *x, const float *y, double *partials) {
+  __shared__ double scratch[16];
+  double acc[1] = {0.0};
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride)
+    acc[0] += double(x[e]) * double(y[e]);
+  block_sum<1>(acc, scratch);
+  if (threadIdx.x == 0) partials[blockIdx.x] = acc[0];
+}
+
+void dot_partials(hipStream_t s, long long n, const float *x, const float *y, double *partials) {
+  hipLaunchKernelGGL(dot_kernel, dim3(dots_partials_wg(n)), dim3(256), 0, s, n, x, y, partials);
+  LBF_KERNEL_CHECK();
+}
+
+__global__ void eval_status_kernel(const double *sse_d, const float *hilo, double inv_scale, double lambda,
+                                   double *scal) {
+  const double sse = hilo ? (double(hilo[0]) + double(hilo[1])) : sse_d[0];
+  scal[SC_SSE] = sse;
+  double loss = 0.5 * sse * inv_scale;
+  if (lambda != 0.0) loss += 0.5 * lambda * scal[SC_WW];
+  scal[SC_LOSS] = loss;
+}
+
+void eval_status(hipStream_t s, const double *sse_d, const float *sse_hilo, double inv_scale, double lambda,
+                 double *scal) {
+  hipLaunchKernelGGL(eval_status_kernel, dim3(1), dim3(1), 0, s, sse_d, sse_hilo, inv_scale, lambda, scal);
+  LBF_KERNEL_CHECK();
+}
+
+__global__ void pack_hilo_kernel(const double *x, float *hilo) {
+  const float hi = float(x[0]);
+  hilo[0] = hi;
+  hilo[1] = float(x[0] - double(hi));
+}
+void pack_hilo(hipStream_t s, const double *x, float *hilo) {
+  hipLaunchKernelGGL(pack_hilo_kernel, dim3(1), dim3(1), 0, s, x, hilo);
+  LBF_KERNEL_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// BLAS-1 style helpers (vectorised; n tail handled per element)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void axpy_to_kernel(long long n, const float *x, float alpha, const float *p,
+                                                      float *y) {
+  const long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (e + 3 < n) {
+    const f32x4 a = *reinterpret_cast<const f32x4 *>(x + e);
+    const f32x4 b = *reinterpret_cast<const f32x4 *>(p + e);
+    *reinterpret_cast<f32x4 *>(y + e) = a + alpha * b;
+  } else {
+    for (long long j = e; j < n; ++j) y[j] = x[j] + alpha * p[j];
+  }
+}
+void axpy_to(hipStream_t s, long long n, const float *x, float alpha, const float *p, float *y) {
+  hipLaunchKernelGGL(axpy_to_kernel, dim3(unsigned(cdiv(cdiv(n, 4), 256))), dim3(256), 0, s, n, x, alpha, p, y);
+  LBF_KERNEL_CHECK();
+}
+void axpy(hipStream_t s, long long n, float alpha, const float *x, float *y) { axpy_to(s, n, y, alpha, x, y); }
+
+__global__ __launch_bounds__(256) void scal_kernel(long long n, float alpha, float *x) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) x[e] *= alpha;
+}
+void scal(hipStream_t s, long long n, float alpha, float *x) {
+  hipLaunchKernelGGL(scal_kernel, dim3(unsigned(cdiv(n, 256))), dim3(256), 0, s, n, alpha, x);
+  LBF_KERNEL_CHECK();
+}
+
+__global__ __launch_bounds__(256) void lincomb_kernel(long long n, const float *a, double c, const float *b,
+                                                      float *out) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) out[e] = float(double(a[e]) + c * double(b[e]));
+}
+void lincomb(hipStream_t s, long long n, const float *a, double c, const float *b, float *out) {
+  hipLaunchKernelGGL(lincomb_kernel, dim3(unsigned(cdiv(n, 256))), dim3(256), 0, s, n, a, c, b, out);
+  LBF_KERNEL_CHECK();
+}
+
+// S-LBFGS iterate averaging (s_lbfgs.hpp:236-243): u = (sum_i w_i) / cnt in logical order.
+struct SlotList {
+  int cnt;
+  int slot[64];
+};
+__global__ __launch_bounds__(256) void average_kernel(long long n, const float *W, long long ld, SlotList sl,
+                                                      float *u) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  double s = 0.0;
+  for (int i = 0; i < sl.cnt; ++i) s += double(W[sl.slot[i] * ld + e]);
+  u[e] = float(s / double(sl.cnt));
+}
+void average_slots(hipStream_t s, long long n, const float *W, long long ld, const int *h_slots, int cnt, float *u) {
+  LBF_REQUIRE(cnt > 0 && cnt <= 64, "average_slots: 1..64 iterates supported (L+1 <= 64)");
+  SlotList sl;
+  sl.cnt = cnt;
+  for (int i = 0; i < cnt; ++i) sl.slot[i] = h_slots[i];
+  hipLaunchKernelGGL(average_kernel, dim3(unsigned(cdiv(n, 256))), dim3(256), 0, s, n, W, ld, sl, u);
+  LBF_KERNEL_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// History: Gram sweep.
+// Each workgroup owns a contiguous chunk of the n coordinates. Phase 1 forms the new vectors
+// (s = sa - sb, y = (ya - yb)*yscale, g = ga - gb + gc) for the chunk into LDS, writes s/y into the
+// ring slot (and g to g_out), and accumulates their 6 mutual dots. Phase 2 streams every live
+// history vector once (one wave per vector, 8 waves) against the three LDS vectors.
+// Partial columns per workgroup: live logical index i -> [S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g]
+// at 6*i..6*i+5 (i < m), then [s.s, s.y, y.y, g.s, g.y, g.g] at 6*m..6*m+5.
+// ---------------------------------------------------------------------------------------------
+static constexpr int GRAM_THREADS = 512;
+static constexpr long long GRAM_MAX_CHUNK = 4096; // 3 x 16 KB of LDS per workgroup
+
+int gram_ncols(int m) { return 6 * m + 6; }
+int gram_nwg(long long n) {
+  long long w = cdiv(n, 1024);
+  if (w > 2048) w = 2048;
+  long long need = cdiv(n, GRAM_MAX_CHUNK);
+  if (w < need) w = need;
+  return int(w < 1 ? 1 : w);
+}
+static long long gram_chunk(long long n, int nwg) { return cdiv(cdiv(n, nwg), 4) * 4; }
+
+__device__ __forceinline__ int hist_write_slot(const int *ist, int m, int policy, int reset) {
+  const int count = reset ? 0 : ist[IST_COUNT];
+  // CUDA semantics (lbfgs.cuh:149-169): the slot at hist_head is overwritten even when the pair is
+  // then rejected; when the ring is full that slot is the oldest live pair.
+  if (policy == POL_CUDA && count == m) return ist[IST_ORDER + 0];
+  return ist[IST_FREE];
+}
+
+__global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, long long chunk, double *partials) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  __shared__ double scratch[6 * 16];
+  float *ls = sh, *ly = sh + chunk, *lg = sh + 2 * chunk;
+  const HistView &h = a.h;
+  const int ncols = 6 * h.m + 6;
+  const long long e0 = (long long)blockIdx.x * chunk;
+  const long long e1 = min(h.n, e0 + chunk);
+  const int len = int(e1 > e0 ? e1 - e0 : 0);
+  const int w = hist_write_slot(h.ist, h.m, a.policy, a.reset);
+  const int count = a.reset ? 0 : h.ist[IST_COUNT];
+  if (blockIdx.x == 0 && threadIdx.x == 0) h.ist[IST_WSLOT] = w;
+
+  double self[6] = {0, 0, 0, 0, 0, 0};
+  float *Sw = h.S + (long long)w * h.ld + e0;
+  float *Yw = h.Y + (long long)w * h.ld + e0;
+  const float ysc = float(a.yscale);
+  for (int i = threadIdx.x; i < len; i += blockDim.x) {
+    const long long e = e0 + i;
+    float sv = 0.f, yv = 0.f, gv = 0.f;
+    if (a.has_pair) {
+      sv = a.sa[e] - a.sb[e];
+      yv = (a.ya[e] - a.yb[e]) * ysc;
+      Sw[i] = sv;
+      Yw[i] = yv;
+    }
+    if (a.has_g) {
+      gv = a.ga[e];
+      if (a.gb) gv = gv - a.gb[e];
+      if (a.gc) gv = gv + a.gc[e];
+      if (a.g_out) a.g_out[e] = gv;
+    }
+    ls[i] = sv;
+    ly[i] = yv;
+    lg[i] = gv;
+    const double s = sv, y = yv, g = gv;
+    self[0] += s * s;
+    self[1] += s * y;
+    self[2] += y * y;
+    self[3] += g * s;
+    self[4] += g * y;
+    self[5] += g * g;
+  }
+  block_sum<6>(self, scratch); // includes __syncthreads: LDS vectors complete after this
+  double *out = partials + (long long)blockIdx.x * ncols;
+  if (threadIdx.x == 0)
+    for (int j = 0; j < 6; ++j) out[6 * h.m + j] = self[j];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int v = wave; v < 2 * count; v += nw) {
+    const int li = v < count ? v : v - count;
+    const int slot = h.ist[IST_ORDER + li];
+    if (a.has_pair && slot == w) { // overwritten in this sweep (CUDA full ring): dots from the self block
+      if (lane == 0) {
+        out[6 * li + (v < count ? 0 : 1)] = 0.0;
+        out[6 * li + (v < count ? 2 : 3)] = 0.0;
+        out[6 * li + (v < count ? 4 : 5)] = 0.0;
+      }
+      continue;
+    }
+    const float *V = (v < count ? h.S : h.Y) + (long long)slot * h.ld + e0;
+    double ds = 0.0, dy = 0.0, dg = 0.0;
+    int i = lane * 4;
+    for (; i + 3 < len; i += 256) {
+      const f32x4 x = *reinterpret_cast<const f32x4 *>(V + i);
+      const f32x4 s4 = *reinterpret_cast<const f32x4 *>(ls + i);
+      const f32x4 y4 = *reinterpret_cast<const f32x4 *>(ly + i);
+      const f32x4 g4 = *reinterpret_cast<const f32x4 *>(lg + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double xv = x[j];
+        ds += xv * double(s4[j]);
+        dy += xv * double(y4[j]);
+        dg += xv * double(g4[j]);
+      }
+    }
+    for (int j = i; j < len && j < i + 4; ++j) {
+      const double xv = V[j];
+      ds += xv * double(ls[j]);
+      dy += xv * double(ly[j]);
+      dg += xv * double(lg[j]);
+    }
+    ds = wave_sum(ds);
+    dy = wave_sum(dy);
+    dg = wave_sum(dg);
+    if (lane == 0) {
+      const int c = v < count ? 0 : 1;
+      out[6 * li + c + 0] = ds;
+      out[6 * li + c + 2] = dy;
+      out[6 * li + c + 4] = dg;
+    }
+  }
+}
+
+void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
+  const int nwg = gram_nwg(a.h.n);
+  const long long chunk = gram_chunk(a.h.n, nwg);
+  const size_t shmem = size_t(3 * chunk) * sizeof(float);
+  hipLaunchKernelGGL(gram_kernel, dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
+  LBF_KERNEL_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// History: Gram bookkeeping + ring update (one wave).
+// Writes the new pair's rows of SS / SY / YY and the g-dots, applies the acceptance rule of the
+// policy (CPU lbfgs.hpp:77-84 ys > 1e-10; CUDA lbfgs.cuh:160 ys > 1e-10; S-LBFGS s_lbfgs.hpp:253
+// |ys| > 1e-10), and pushes/evicts like RingBuffer::push_back (ring_buffer.hpp:43-59).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void hist_update_kernel(const CoefArgs a) {
+  const HistView &h = a.h;
+  const int S_ = h.slots;
+  const int lane = threadIdx.x;
+  const int count0 = a.reset ? 0 : h.ist[IST_COUNT];
+  const int w = h.ist[IST_WSLOT];
+  const double *d = a.dots;
+  const double *self = d + 6 * h.m;
+  for (int i = lane; i < count0; i += 64) {
+    const int j = h.ist[IST_ORDER + i];
+    if (a.has_pair && j == w) continue;
+    if (a.has_pair) {
+      h.SS[w * S_ + j] = d[6 * i + 0];
+      h.SS[j * S_ + w] = d[6 * i + 0];
+      h.SY[w * S_ + j] = d[6 * i + 1]; // s_w . y_j
+      h.SY[j * S_ + w] = d[6 * i + 2]; // s_j . y_w
+      h.YY[w * S_ + j] = d[6 * i + 3];
+      h.YY[j * S_ + w] = d[6 * i + 3];
+    }
+    if (a.has_g) {
+      h.gS[j] = d[6 * i + 4];
+      h.gY[j] = d[6 * i + 5];
+    }
+  }
+  if (lane != 0) return;
+  if (a.has_pair) {
+    h.SS[w * S_ + w] = self[0];
+    h.SY[w * S_ + w] = self[1];
+    h.YY[w * S_ + w] = self[2];
+  }
+  if (a.has_g) {
+    if (a.has_pair) {
+      h.gS[w] = self[3];
+      h.gY[w] = self[4];
+    }
+    h.scal[SC_GG] = self[5];
+  }
+  int count = count0;
+  if (a.reset) h.ist[IST_COUNT] = 0;
+  if (a.has_pair) {
+    const double ys = self[1];
+    h.scal[SC_YS] = ys;
+    bool acc;
+    if (a.policy == POL_SLBFGS) acc = fabs(ys) > 1e-10;
+    else acc = ys > 1e-10;
+    if (a.want_dir < 0) acc = true; // explicit-history upload (lbf_two_loop): always push
+    h.scal[SC_ACCEPT] = acc ? 1.0 : 0.0;
+    if (acc) {
+      h.rho[w] = 1.0 / ys;
+      int *order = h.ist + IST_ORDER;
+      if (count < h.m) {
+        order[count] = w;
+        ++count;
+        if (a.policy != POL_CUDA || count < h.m) {
+          // next free slot: any of the m+1 slots not live
+          int f = 0;
+          for (; f < S_; ++f) {
+            bool live = false;
+            for (int q = 0; q < count; ++q) live |= (order[q] == f);
+            if (!live) break;
+          }
+          h.ist[IST_FREE] = f;
+        }
+      } else {
+        const int evicted = order[0];
+        for (int q = 0; q + 1 < h.m; ++q) order[q] = order[q + 1];
+        order[h.m - 1] = w;
+        if (w != evicted) h.ist[IST_FREE] = evicted;
+      }
+      h.ist[IST_COUNT] = count;
+    }
+  }
+  h.scal[SC_COUNT] = double(count);
+}
+
+// ---------------------------------------------------------------------------------------------
+// History: the two-loop recursion on coefficients (one wave).
+// With q = g - sum_j alpha_j y_j and z = gamma*q + sum_j (alpha_j - beta_j) s_j, the reference's
+// loops (lbfgs.hpp:119-136) become two triangular recurrences on the Gram entries:
+//   backward  alpha_i = rho_i * (gS_i - sum_{j>i} alpha_j SY[i][j])
+//   forward   beta_i  = rho_i * (gamma*(gY_i - sum_j alpha_j YY[i][j]) + sum_{j<i} (alpha_j-beta_j) SY[j][i])
+// and z has coefficients  cs_i = alpha_i - beta_i, cy_i = -gamma*alpha_i, cg = gamma.
+// Lane l keeps the running sum of row l; SY (live k x k) is staged in LDS.
+// ---------------------------------------------------------------------------------------------
+static constexpr int COEF_MAXK = 128;
+
+__global__ __launch_bounds__(64) void hist_dir_kernel(const CoefArgs a) {
+  extern __shared__ double sy[]; // k*k, sy[i*k + j] = s_i . y_j (logical)
+  __shared__ double alpha_s[COEF_MAXK], c_s[COEF_MAXK];
+  __shared__ int L[COEF_MAXK];
+  const HistView &h = a.h;
+  const int S_ = h.slots;
+  const int lane = threadIdx.x;
+  const int k = h.ist[IST_COUNT];
+  for (int i = lane; i < k; i += 64) L[i] = h.ist[IST_ORDER + i];
+  __syncthreads();
+  for (int e = lane; e < k * k; e += 64) {
+    const int i = e / k, j = e - i * k;
+    sy[e] = h.SY[L[i] * S_ + L[j]];
+  }
+  __syncthreads();
+  const double gg = h.scal[SC_GG];
+  double gamma = 1.0;
+  if (k > 0) {
+    const int last = L[k - 1];
+    const double ys = h.SY[last * S_ + last], yy = h.YY[last * S_ + last];
+    if (a.policy == POL_CPU) {
+      gamma = ys / yy; // lbfgs.hpp:127-128, no guard
+    } else if (a.policy == POL_CUDA) {
+      gamma = yy > 0.0 ? ys / yy : 1.0; // lbfgs.cuh:247
+    } else {
+      gamma = fabs(yy) < 1e-12 ? 1.0 : ys / yy; // s_lbfgs.hpp:119-126
+      gamma = fmin(fmax(gamma, 1e-6), 1e6);
+    }
+  }
+  // backward loop: r_l = gS_l - sum_{j>l} alpha_j SY[l][j]
+  constexpr int RPL = COEF_MAXK / 64; // rows per lane (2)
+  static_assert(RPL == 2, "row ownership below assumes two rows per lane");
+  double r[RPL];
+#pragma unroll
+  for (int q = 0; q < RPL; ++q) {
+    const int l = lane + 64 * q;
+    r[q] = l < k ? h.gS[L[l]] : 0.0;
+  }
+  for (int i = k - 1; i >= 0; --i) {
+    // owner of row i publishes alpha_i
+    if ((i & 63) == lane) {
+      const double ri = (i >> 6) == 0 ? r[0] : r[RPL - 1];
+      alpha_s[i] = h.rho[L[i]] * ri;
+    }
+    __syncthreads();
+    const double ai = alpha_s[i];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      const int l = lane + 64 * q;
+      if (l < i) r[q] -= ai * sy[l * k + i];
+    }
+  }
+  __syncthreads();
+  // forward loop: t_l = gamma*(gY_l - sum_j alpha_j YY[l][j]) ; then triangular update with SY[i][l]
+  double t[RPL];
+#pragma unroll
+  for (int q = 0; q < RPL; ++q) {
+    const int l = lane + 64 * q;
+    t[q] = 0.0;
+    if (l < k) {
+      double acc = h.gY[L[l]];
+      for (int j = 0; j < k; ++j) acc -= alpha_s[j] * h.YY[L[l] * S_ + L[j]];
+      t[q] = gamma * acc;
+    }
+  }
+  for (int i = 0; i < k; ++i) {
+    if ((i & 63) == lane) {
+      const double beta = h.rho[L[i]] * ((i >> 6) == 0 ? t[0] : t[RPL - 1]);
+      c_s[i] = alpha_s[i] - beta;
+    }
+    __syncthreads();
+    const double ci = c_s[i];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      const int l = lane + 64 * q;
+      if (l > i && l < k) t[q] += ci * sy[i * k + l];
+    }
+  }
+  __syncthreads();
+  // coefficients of z; direction = dsign * z
+  double ds = a.dsign;
+  double cg = gamma;
+  // g^T z = sum cs_i gS_i + cy_i gY_i + cg*gg
+  double part = 0.0;
+  for (int i = lane; i < k; i += 64) part += c_s[i] * h.gS[L[i]] - gamma * alpha_s[i] * h.gY[L[i]];
+  part = wave_sum(part);
+  double gTz = part + cg * gg;
+  bool fallback = false;
+  if (a.policy == POL_CUDA && a.want_dir == 1 && ds * gTz >= 0.0) {
+    // lbfgs.cuh:97-104: not a descent direction -> steepest descent and history reset
+    fallback = true;
+  }
+  if (fallback) {
+    for (int i = lane; i < k; i += 64) {
+      h.coef[i] = 0.0;
+      h.coef[S_ + i] = 0.0;
+    }
+    if (lane == 0) {
+      h.coef[2 * S_] = -1.0;
+      h.ist[IST_COUNT] = 0;
+      h.scal[SC_RESET] = 1.0;
+      h.scal[SC_COUNT] = 0.0;
+      h.scal[SC_GTP] = -gg;
+    }
+  } else {
+    for (int i = lane; i < k; i += 64) {
+      h.coef[i] = ds * c_s[i];
+      h.coef[S_ + i] = ds * (-gamma * alpha_s[i]);
+    }
+    if (lane == 0) {
+      h.coef[2 * S_] = ds * cg;
+      h.scal[SC_RESET] = 0.0;
+      h.scal[SC_GTP] = ds * gTz;
+    }
+  }
+  if (lane == 0) {
+    h.scal[SC_GAMMA] = gamma;
+    h.scal[SC_ALPHA0] = (a.iter == 0) ? fmin(1.0, 1.0 / sqrt(gg)) : 1.0;
+  }
+}
+
+void hist_coef(hipStream_t s, const CoefArgs &a) {
+  LBF_REQUIRE(a.h.m <= COEF_MAXK, "history size m must be <= 128");
+  hipLaunchKernelGGL(hist_update_kernel, dim3(1), dim3(64), 0, s, a);
+  LBF_KERNEL_CHECK();
+  if (a.want_dir > 0) {
+    const size_t shmem = size_t(a.h.m) * a.h.m * sizeof(double);
+    static bool attr_set = false;
+    if (!attr_set) {
+      LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(hist_dir_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, COEF_MAXK * COEF_MAXK * 8));
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(hist_dir_kernel, dim3(1), dim3(64), shmem, s, a);
+    LBF_KERNEL_CHECK();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// History: linear-combination sweep  dir = sum_i cs_i S_i + cy_i Y_i + cg g  (fp64 per element),
+// fused with the trial point x_out = x_in + alpha*dir (and an optional second copy).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
+  __shared__ double cs[COEF_MAXK], cy[COEF_MAXK];
+  __shared__ int L[COEF_MAXK];
+  const HistView &h = a.h;
+  const int S_ = h.slots;
+  const int k = h.ist[IST_COUNT];
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    cs[i] = h.coef[i];
+    cy[i] = h.coef[S_ + i];
+    L[i] = h.ist[IST_ORDER + i];
+  }
+  __syncthreads();
+  const double cg = h.coef[2 * S_];
+  const double alpha = a.alpha_from_state ? h.scal[SC_ALPHA0] : a.alpha;
+  const long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (e >= h.n) return;
+  if (e + 3 < h.n) {
+    const f32x4 g4 = *reinterpret_cast<const f32x4 *>(a.g + e);
+    double acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = cg * double(g4[j]);
+    for (int i = 0; i < k; ++i) {
+      const f32x4 s4 = *reinterpret_cast<const f32x4 *>(h.S + (long long)L[i] * h.ld + e);
+      const f32x4 y4 = *reinterpret_cast<const f32x4 *>(h.Y + (long long)L[i] * h.ld + e);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += cs[i] * double(s4[j]) + cy[i] * double(y4[j]);
+    }
+    f32x4 d4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d4[j] = float(acc[j]);
+    if (a.dir) *reinterpret_cast<f32x4 *>(a.dir + e) = d4;
+    if (a.x_out) {
+      const f32x4 x4 = *reinterpret_cast<const f32x4 *>(a.x_in + e);
+      const f32x4 o4 = x4 + float(alpha) * d4;
+      *reinterpret_cast<f32x4 *>(a.x_out + e) = o4;
+      if (a.x_out2) *reinterpret_cast<f32x4 *>(a.x_out2 + e) = o4;
+    }
+  } else {
+    for (long long q = e; q < h.n; ++q) {
+      double acc = cg * double(a.g[q]);
+      for (int i = 0; i < k; ++i)
+        acc += cs[i] * double(h.S[(long long)L[i] * h.ld + q]) + cy[i] * double(h.Y[(long long)L[i] * h.ld + q]);
+      const float d = float(acc);
+      if (a.dir) a.dir[q] = d;
+      if (a.x_out) {
+        const float o = a.x_in[q] + float(alpha) * d;
+        a.x_out[q] = o;
+        if (a.x_out2) a.x_out2[q] = o;
+      }
+    }
+  }
+}
+
+void hist_combine(hipStream_t s, const CombineArgs &a) {
+  LBF_REQUIRE(a.h.ld % 4 == 0, "history slot stride must be a multiple of 4");
+  hipLaunchKernelGGL(combine_kernel, dim3(unsigned(cdiv(cdiv(a.h.n, 4), 256))), dim3(256), 0, s, a);
+  LBF_KERNEL_CHECK();
+}
+
+__global__ void hist_reset_kernel(HistView h) {
+  h.ist[IST_COUNT] = 0;
+  h.ist[IST_FREE] = 0;
+  h.ist[IST_WSLOT] = 0;
+  h.scal[SC_COUNT] = 0.0;
+}
+void hist_reset(hipStream_t s, const HistView &h) {
+  hipLaunchKernelGGL(hist_reset_kernel, dim3(1), dim3(1), 0, s, h);
+  LBF_KERNEL_CHECK();
+}
+
+} // namespace lbf

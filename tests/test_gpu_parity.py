@@ -1,0 +1,236 @@
+"""GPU parity: HIP kernels (through the C ABI) vs the CPU oracle (fp64 restatement of the reference).
+
+Tolerances (fp32 compute vs fp64 reference):
+  loss: relative 1e-5; gradient: ||dg|| / ||g|| <= 1e-4; two-loop direction: ||dp|| / ||p|| <= 1e-5;
+  L-BFGS trajectory (Wolfe, CPU semantics): first 10 iterations' loss relative <= 1e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+LOSS_RTOL = 1e-5
+GRAD_RTOL = 1e-4
+DIR_RTOL = 1e-5
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
+
+
+def host(t):
+    return t.double().cpu().numpy()
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def random_problem(dims, N, seed=0, onehot=True):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((N, dims[0])).astype(np.float32).astype(np.float64)
+    if onehot:
+        Y = np.zeros((N, dims[-1]))
+        Y[np.arange(N), rng.integers(0, dims[-1], N)] = 1.0
+    else:
+        Y = rng.standard_normal((N, dims[-1])).astype(np.float32).astype(np.float64)
+    return X, Y
+
+
+NETS = [
+    ([784, 128, 10], ["relu", "linear"]),
+    ([784, 128, 64, 10], ["relu", "relu", "linear"]),
+    ([37, 50, 3], ["tanh", "sigmoid"]),
+    ([64, 96, 33, 1], ["sigmoid", "tanh", "linear"]),
+    ([129, 130, 65, 10], ["relu", "tanh", "linear"]),
+]
+
+
+@pytest.mark.parametrize("dims,acts", NETS)
+@pytest.mark.parametrize("N", [1, 31, 257, 1000])
+def test_loss_grad_matches_oracle(ctx, pkg, O, dims, acts, N):
+    X, Y = random_problem(dims, N, seed=N)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    loss, g = net.loss_grad(P, dev(X), dev(Y))
+    l_ref, g_ref = O.Net(dims, acts).loss_grad(host(P), X, Y)
+    assert abs(loss - l_ref) <= LOSS_RTOL * abs(l_ref)
+    assert rel(host(g), g_ref) <= GRAD_RTOL
+
+
+def test_forward_matches_oracle(ctx, pkg, O):
+    dims, acts = [784, 128, 10], ["relu", "linear"]
+    X, Y = random_problem(dims, 300, seed=3)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(7, "cuda")
+    out = host(net.forward(P, dev(X)))
+    _, out_ref = O.Net(dims, acts).loss(host(P), X, Y, want_out=True)
+    assert rel(out, out_ref) <= 1e-5
+
+
+def test_loss_grad_gather_and_l2(ctx, pkg, O):
+    """S-LBFGS batch_g: gathered minibatch rows + L2 term (unified_optimization.hpp:343-376)."""
+    dims, acts = [784, 64, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(500)
+    idx = O.sample_indices(500, 77, seed=123, calls=1)[0]
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    loss, g = net.loss_grad(P, dev(Xh), dev(Yh), idx=torch.from_numpy(idx.astype(np.int32)).cuda(), l2=1e-4)
+    l_ref, g_ref = O.Net(dims, acts).loss_grad(host(P), Xh.astype(np.float64), Yh.astype(np.float64), idx=idx,
+                                               lam=1e-4)
+    assert abs(loss - l_ref) <= LOSS_RTOL * abs(l_ref)
+    assert rel(host(g), g_ref) <= GRAD_RTOL
+
+
+def test_eval_is_deterministic(ctx, pkg):
+    """Fixed-order reductions: two evaluations of the same point are bitwise identical (the Wolfe
+    line search's cached f / grad reuse relies on it)."""
+    dims, acts = [784, 128, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(4096)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    X, Y = dev(Xh), dev(Yh)
+    l1, g1 = net.loss_grad(P, X, Y)
+    l2, g2 = net.loss_grad(P, X, Y)
+    assert l1 == l2
+    assert torch.equal(g1, g2)
+
+
+def make_history(n, k, seed=0):
+    rng = np.random.default_rng(seed)
+    d = rng.uniform(0.5, 2.0, n)
+    S = rng.standard_normal((k, n))
+    Yv = S * d + 0.01 * rng.standard_normal((k, n))   # positive curvature pairs
+    S = S.astype(np.float32).astype(np.float64)
+    Yv = Yv.astype(np.float32).astype(np.float64)
+    rho = 1.0 / np.einsum("ij,ij->i", S, Yv)
+    g = rng.standard_normal(n).astype(np.float32).astype(np.float64)
+    return S, Yv, rho, g
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("k", [0, 1, 5, 10, 50])
+@pytest.mark.parametrize("n", [1000, 100003])
+def test_two_loop_matches_oracle(ctx, O, mode, k, n):
+    S, Yv, rho, g = make_history(n, k, seed=k + n)
+    ref = O.two_loop(mode, S if k else np.zeros((0, n)), Yv if k else np.zeros((0, n)), rho, g)
+    out = ctx.two_loop(dev(S) if k else None, dev(Yv) if k else None, rho, dev(g), mode=mode)
+    assert rel(host(out), ref) <= DIR_RTOL
+
+
+def test_blas1(ctx):
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal(123457).astype(np.float32)
+    y = rng.standard_normal(123457).astype(np.float32)
+    dx, dy = dev(x), dev(y)
+    assert abs(ctx.dot(dx, dy) - float(np.dot(x.astype(np.float64), y))) < 1e-9 * 123457
+    assert abs(ctx.nrm2(dx) - float(np.linalg.norm(x.astype(np.float64)))) < 1e-9 * 400
+    ctx.axpy_(0.5, dx, dy)
+    assert np.allclose(host(dy), y + np.float32(0.5) * x, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("m", [5, 10])
+def test_lbfgs_wolfe_trajectory(ctx, pkg, O, m):
+    """CPU semantics (lbfgs.hpp:38-100 + full_batch_minimizer.hpp:126-157): fp32 GPU trajectory vs the
+    fp64 oracle, same seed/data. Early iterations agree to 1e-3; the line-search decisions match."""
+    dims, acts = [784, 32, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(256)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    P0 = host(P)
+    hist, info = pkg.lbfgs_solve(net, P, dev(Xh), dev(Yh), m=m, max_iters=20, tol=0.0)
+    _, rec, _ = O.Net(dims, acts).lbfgs_wolfe(P0, Xh.astype(np.float64), Yh.astype(np.float64), m=m,
+                                              max_iters=20)
+    assert len(hist["loss"]) == 20
+    r = np.abs(hist["loss"][:10] - rec[:10, 0]) / np.abs(rec[:10, 0])
+    assert r.max() <= 1e-3, r
+    assert np.array_equal(hist["ls_trials"][:10], rec[:10, 4].astype(int))
+    assert np.array_equal(hist["accepted"][:9], rec[:9, 3].astype(int))
+    # monotone decrease (Armijo condition) on the whole run
+    assert np.all(np.diff(hist["loss"]) <= 1e-7)
+
+
+def test_lbfgs_armijo_trajectory(ctx, pkg, O):
+    """CUDA semantics (lbfgs.cuh:39-194) vs the oracle's fp32 instantiation of the same algorithm."""
+    dims, acts = [784, 32, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(256)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cuda")
+    P0 = host(P)
+    hist, info = pkg.lbfgs_solve(net, P, dev(Xh), dev(Yh), line_search="armijo", m=10, max_iters=15, tol=0.0)
+    _, rec = O.Net(dims, acts).lbfgs_armijo(P0, Xh.astype(np.float64), Yh.astype(np.float64), m=10,
+                                            max_iters=15, fp32=True)
+    r = np.abs(hist["loss"][:8] - rec[:8, 0]) / np.abs(rec[:8, 0])
+    assert r.max() <= 1e-3, r
+    assert np.array_equal(hist["ls_trials"][:8], rec[:8, 4].astype(int))
+
+
+def test_slbfgs_matches_oracle(ctx, pkg, O):
+    """S-LBFGS (s_lbfgs.hpp:165-290): same host RNG stream, same sampled batches, same curvature pairs."""
+    dims, acts = [784, 16, 10], ["relu", "linear"]
+    N = 512
+    Xh, Yh = pkg.synth_mnist(N)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    P0 = host(P)
+    kw = dict(M=5, L=4, b=32, b_H=16, step=0.02)
+    hist, info = pkg.slbfgs_solve(net, P, dev(Xh), dev(Yh), max_epochs=2, tol=0.0, lam=1e-4, **kw)
+    _, rec, _ = O.Net(dims, acts).slbfgs(P0, Xh.astype(np.float64), Yh.astype(np.float64), epochs=2, tol=0.0,
+                                         M=5, L=4, b=32, bH=16, step=0.02, lam=1e-4)
+    assert len(hist["loss"]) == 2
+    r = np.abs(hist["loss"] - rec[:, 0]) / np.abs(rec[:, 0])
+    assert r.max() <= 1e-3, r
+    assert np.array_equal(hist["accepted"], rec[:, 3].astype(int))   # live pairs after each epoch
+
+
+def test_gradient_directional_derivative_full_size(ctx, pkg):
+    """Size-independent property at the BASELINE cfg-2 size (N = 60000): central difference of the loss
+    along a random direction equals g.d (no oracle needed at full size)."""
+    dims, acts = [784, 128, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(60000)
+    X, Y = dev(Xh), dev(Yh)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    loss, g = net.loss_grad(P, X, Y)
+    d = torch.randn_like(P, generator=torch.Generator(device="cuda").manual_seed(0))
+    d = d / d.norm()
+    eps = 1e-2
+    lp, _ = net.loss_grad(P + eps * d, X, Y)
+    lm, _ = net.loss_grad(P - eps * d, X, Y)
+    fd = (lp - lm) / (2 * eps)
+    gd = float((g.double() * d.double()).sum())
+    assert abs(fd - gd) <= 2e-3 * max(abs(gd), 1e-3), (fd, gd)
+
+
+def test_shard_sum_equals_full_batch(ctx, pkg):
+    """Data-parallel decomposition at full size: sum of per-shard gradients scaled by 1/N_global equals
+    the full-batch gradient (what the RCCL all-reduce computes)."""
+    dims, acts = [784, 128, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(60000)
+    X, Y = dev(Xh), dev(Yh)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    lf, gf = net.loss_grad(P, X, Y)
+    gs = torch.zeros_like(gf, dtype=torch.float64)
+    ls = 0.0
+    for r in range(8):
+        lo, hi = 60000 * r // 8, 60000 * (r + 1) // 8
+        l, g = net.loss_grad(P, X[lo:hi].contiguous(), Y[lo:hi].contiguous(), inv_scale=1.0 / 60000)
+        gs += g.double()
+        ls += l
+    assert abs(ls - lf) <= 1e-6 * abs(lf)
+    assert rel(gs.cpu().numpy(), host(gf)) <= 1e-5
+
+
+def test_lbfgs_full_size_decreases(ctx, pkg):
+    """cfg 2 (784-128-10, N=60000, m=10): 10 Wolfe iterations run and decrease the loss monotonically."""
+    dims, acts = [784, 128, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(60000)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    hist, info = pkg.lbfgs_solve(net, P, dev(Xh), dev(Yh), m=10, max_iters=10, tol=0.0)
+    assert len(hist["loss"]) == 10
+    assert np.all(np.diff(hist["loss"]) <= 0)
+    assert hist["loss"][-1] < 0.5 * hist["loss"][0]
