@@ -61,6 +61,14 @@ int loss_partials_wg(long long B, int Out);
 void loss_diff(hipStream_t s, const float *Aout, long long lda, const float *Y, long long ldy, const int *idx,
                long long B, int Out, int act, double inv_scale, float *dZ, long long ldz, double *partials);
 
+// Fused output layer (head.hip): forward + MSE + dZ + delta_prev + per-tile [dW ; db] slabs.
+bool head_supported(int H, int Out);
+int head_tile(int H);
+int head_nwg(long long B, int H);
+void head_fused(hipStream_t s, const float *A, int H, const float *P, int Out, const float *Y, const int *idx,
+                long long B, int act_out, int act_prev, double inv_scale, float *delta, float *slab,
+                double *sse_part);
+
 // grad[e] = sum_s slab[s*stride + e] * scale (fixed order), e in [0, count)
 void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride, long long count, float *grad);
 
@@ -75,6 +83,11 @@ void dot_partials(hipStream_t s, long long n, const float *x, const float *y, do
 // is non-null, sse = hilo[0] + hilo[1] (all-reduced split fp32 pair).
 void eval_status(hipStream_t s, const double *sse_d, const float *sse_hilo, double inv_scale, double lambda,
                  double *scal);
+// One-workgroup tail: reduce finalize dots (+ SSE partials unless hilo) and write SC_TGG/TGP/WW/SSE/LOSS.
+void eval_tail(hipStream_t s, const double *dots_part, int nd, const double *sse_part, int nsse, const float *hilo,
+               double inv_scale, double lambda, double *scal);
+// DP: reduce SSE partials into an fp32 (hi, lo) pair (all-reduced together with the gradient).
+void sse_pack(hipStream_t s, const double *sse_part, int nsse, float *hilo);
 // hilo[0] = float(x), hilo[1] = float(x - hilo[0])
 void pack_hilo(hipStream_t s, const double *x, float *hilo);
 
@@ -147,7 +160,8 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials);
 
 struct CoefArgs {
   HistView h;
-  const double *dots = nullptr; // reduced gram output
+  const double *partials = nullptr; // gram_update's per-workgroup partials [nwg][gram_ncols(m)]
+  int nwg = 0;
   int has_pair = 0, has_g = 0, reset = 0, policy = POL_CPU;
   int want_dir = 1;
   int iter = 1;

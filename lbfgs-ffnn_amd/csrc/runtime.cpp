@@ -2,6 +2,7 @@
 #include "runtime.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace lbf {
@@ -71,6 +72,8 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
     layers_.push_back(L);
   }
   nparams_ = off;
+  const char *nh = std::getenv("LBF_NO_HEAD");
+  use_head_ = !(nh && nh[0] == '1');
 }
 
 // Split-K plan of every dW GEMM for batch B: aim for ~512 workgroups (2 per CU) per GEMM, k chunks
@@ -107,16 +110,24 @@ void Mlp::ensure(long long B) {
   }
   plan(B);
   const int nl = int(layers_.size());
-  loss_part_.ensure(size_t(loss_partials_wg(std::max(1LL, B), layers_[nl - 1].out)));
+  const Layer &Lo = layers_[nl - 1];
+  size_t nloss = size_t(loss_partials_wg(std::max(1LL, B), Lo.out));
+  if (nl >= 2 && head_supported(Lo.in, Lo.out)) {
+    const size_t hw = size_t(head_nwg(B, Lo.in));
+    nloss = std::max(nloss, hw);
+    head_slab_.ensure(hw * size_t(Lo.in + 1) * Lo.out);
+  }
+  loss_part_.ensure(nloss);
   dots_part_.ensure(size_t(dots_partials_wg(nparams_)) * 3);
   sse_.ensure(1);
 }
 
-const float *Mlp::forward(const float *P, const float *X, const int *idx, long long B) {
+const float *Mlp::forward(const float *P, const float *X, const int *idx, long long B, int nrun) {
   ensure(B);
   hipStream_t s = ctx_->stream;
   const float *in = X;
-  for (size_t l = 0; l < layers_.size(); ++l) {
+  const size_t nr = nrun < 0 ? layers_.size() : size_t(nrun);
+  for (size_t l = 0; l < nr; ++l) {
     const Layer &L = layers_[l];
     GemmDesc d;
     d.M = int(B);
@@ -143,17 +154,32 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
 
 void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
                     double inv_scale, double lambda, const float *pdir, double *scal) {
-  forward(P, X, idx, B);
   hipStream_t s = ctx_->stream;
   const int nl = int(layers_.size());
   const Layer &Lo = layers_[nl - 1];
-  const int nloss = loss_partials_wg(std::max(1LL, B), Lo.out);
-  {
+  const bool fused = use_head_ && nl >= 2 && head_supported(Lo.in, Lo.out);
+  forward(P, X, idx, B, fused ? nl - 1 : nl);
+  int nloss, lstart;
+  if (fused) {
+    // last layer: forward + loss + dZ + delta + [dW ; db] partials in one kernel (head.hip)
+    nloss = head_nwg(B, Lo.in);
+    const long long seg = (long long)(Lo.in + 1) * Lo.out;
+    {
+      ProfScope ps(ctx_, PK_LOSS);
+      head_fused(s, A_[nl - 2].get(), Lo.in, P + Lo.off, Lo.out, Y, idx, B, Lo.act, layers_[nl - 2].act, inv_scale,
+                 D_[nl - 2].get(), head_slab_.get(), loss_part_.get());
+    }
+    ProfScope ps(ctx_, PK_SLAB, nl - 1);
+    reduce_slabs(s, head_slab_.get(), nloss, seg, seg, G + Lo.off);
+    lstart = nl - 2;
+  } else {
+    nloss = loss_partials_wg(std::max(1LL, B), Lo.out);
     ProfScope ps(ctx_, PK_LOSS);
     loss_diff(s, A_[nl - 1].get(), Lo.out, Y, Lo.out, idx, B, Lo.out, Lo.act, inv_scale, D_[nl - 1].get(), Lo.out,
               loss_part_.get());
+    lstart = nl - 1;
   }
-  for (int l = nl - 1; l >= 0; --l) {
+  for (int l = lstart; l >= 0; --l) {
     const Layer &L = layers_[l];
     const float *Ain = (l == 0) ? X : A_[l - 1].get();
     // [dW ; db] = [A_in | 1]^T dZ  (layer.cuh:81-84 + sum_rows_kernel kernels.cuh:144-153)
@@ -213,22 +239,20 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     }
   }
   const float *hilo = nullptr;
-  {
-    ProfScope ps(ctx_, PK_FINAL, 0);
-    reduce_rows(s, loss_part_.get(), nloss, 1, sse_.get());
-    if (ctx_->nranks > 1) pack_hilo(s, sse_.get(), G + nparams_);
-  }
   if (ctx_->nranks > 1) {
+    {
+      ProfScope ps(ctx_, PK_FINAL, 0);
+      sse_pack(s, loss_part_.get(), nloss, G + nparams_);
+    }
     ProfScope ps(ctx_, PK_ALLREDUCE);
-    ctx_->allreduce(G, nparams_ + 2);
+    ctx_->allreduce(G, nparams_ + 2); // one RCCL all-reduce of [grad | sse_hi | sse_lo]
     hilo = G + nparams_;
   }
   {
     ProfScope ps(ctx_, PK_FINAL, 1);
     const int nd = dots_partials_wg(nparams_);
     finalize_grad_dots(s, nparams_, G, P, lambda, pdir, dots_part_.get());
-    reduce_rows(s, dots_part_.get(), nd, 3, scal + SC_TGG);
-    eval_status(s, sse_.get(), hilo, inv_scale, lambda, scal);
+    eval_tail(s, dots_part_.get(), nd, loss_part_.get(), nloss, hilo, inv_scale, lambda, scal);
   }
   ++evals_;
 }
@@ -287,11 +311,11 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
   {
     ProfScope ps(ctx_, PK_GRAM);
     gram_update(s, g, part_.get());
-    reduce_rows(s, part_.get(), gram_nwg(v_.n), gram_ncols(v_.m), red_.get());
   }
   CoefArgs c;
   c.h = v_;
-  c.dots = red_.get();
+  c.partials = part_.get();
+  c.nwg = gram_nwg(v_.n);
   c.has_pair = g.has_pair;
   c.has_g = g.has_g;
   c.reset = g.reset;

@@ -72,7 +72,7 @@ public:
   Ctx *ctx() const { return ctx_; }
 
   // Forward only: activations of every layer into the workspace; returns the output buffer.
-  const float *forward(const float *P, const float *X, const int *idx, long long B);
+  const float *forward(const float *P, const float *X, const int *idx, long long B, int nrun = -1);
   // Fused loss + gradient (+ all-reduce over the communicator) + line-search dots.
   //   G    : gradient output, must hold nparams()+2 floats (two extra words carry the loss for the
   //          all-reduce).
@@ -89,7 +89,8 @@ private:
   size_t nparams_ = 0;
   long long cap_ = -1, planned_ = -1;
   std::vector<DevBuf<float>> A_, D_;
-  DevBuf<float> slab_;
+  DevBuf<float> slab_, head_slab_;
+  bool use_head_ = true; // fused output layer when the shape allows (LBF_NO_HEAD=1 disables)
   DevBuf<double> loss_part_, dots_part_, sse_;
   long long evals_ = 0;
   void plan(long long B);

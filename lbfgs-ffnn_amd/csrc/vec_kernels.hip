@@ -114,18 +114,32 @@ void loss_diff(hipStream_t s, const float *Aout, long long lda, const float *Y, 
 // ---------------------------------------------------------------------------------------------
 // split-K slab reduction -> flat gradient segment
 // ---------------------------------------------------------------------------------------------
+// Block = CW columns x (256/CW) split stripes; each thread sums its stripe, stripes combine in LDS in
+// a fixed order. CW = 64 for few splits (coalesced 256-B rows), 16 when splits are many (more
+// parallelism per column for the tall-and-thin slabs of small layers).
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float *slab, int splits, long long stride,
-                                                           long long count, float *grad) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= count) return;
+                                                           long long count, int cw, float *grad) {
+  __shared__ double part[256];
+  const int t = threadIdx.x;
+  const int nst = 256 / cw;
+  const long long col = (long long)blockIdx.x * cw + (t % cw);
+  const int stripe = t / cw;
   double s = 0.0;
-  for (int k = 0; k < splits; ++k) s += double(slab[k * stride + e]);
-  grad[e] = float(s);
+  if (col < count)
+    for (int k = stripe; k < splits; k += nst) s += double(slab[k * stride + col]);
+  part[t] = s;
+  __syncthreads();
+  if (stripe == 0 && col < count) {
+    double r = 0.0;
+    for (int q = 0; q < nst; ++q) r += part[q * cw + t];
+    grad[col] = float(r);
+  }
 }
 
 void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride, long long count, float *grad) {
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(unsigned(cdiv(count, 256))), dim3(256), 0, s, slab, splits, stride,
-                     count, grad);
+  const int cw = splits > 64 ? 16 : 64;
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(unsigned(cdiv(count, cw))), dim3(256), 0, s, slab, splits, stride,
+                     count, cw, grad);
   LBF_KERNEL_CHECK();
 }
 
@@ -402,117 +416,166 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// History: Gram bookkeeping + ring update (one wave).
-// Writes the new pair's rows of SS / SY / YY and the g-dots, applies the acceptance rule of the
-// policy (CPU lbfgs.hpp:77-84 ys > 1e-10; CUDA lbfgs.cuh:160 ys > 1e-10; S-LBFGS s_lbfgs.hpp:253
-// |ys| > 1e-10), and pushes/evicts like RingBuffer::push_back (ring_buffer.hpp:43-59).
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void hist_update_kernel(const CoefArgs a) {
-  const HistView &h = a.h;
-  const int S_ = h.slots;
-  const int lane = threadIdx.x;
-  const int count0 = a.reset ? 0 : h.ist[IST_COUNT];
-  const int w = h.ist[IST_WSLOT];
-  const double *d = a.dots;
-  const double *self = d + 6 * h.m;
-  for (int i = lane; i < count0; i += 64) {
-    const int j = h.ist[IST_ORDER + i];
-    if (a.has_pair && j == w) continue;
-    if (a.has_pair) {
-      h.SS[w * S_ + j] = d[6 * i + 0];
-      h.SS[j * S_ + w] = d[6 * i + 0];
-      h.SY[w * S_ + j] = d[6 * i + 1]; // s_w . y_j
-      h.SY[j * S_ + w] = d[6 * i + 2]; // s_j . y_w
-      h.YY[w * S_ + j] = d[6 * i + 3];
-      h.YY[j * S_ + w] = d[6 * i + 3];
-    }
-    if (a.has_g) {
-      h.gS[j] = d[6 * i + 4];
-      h.gY[j] = d[6 * i + 5];
-    }
-  }
-  if (lane != 0) return;
-  if (a.has_pair) {
-    h.SS[w * S_ + w] = self[0];
-    h.SY[w * S_ + w] = self[1];
-    h.YY[w * S_ + w] = self[2];
-  }
-  if (a.has_g) {
-    if (a.has_pair) {
-      h.gS[w] = self[3];
-      h.gY[w] = self[4];
-    }
-    h.scal[SC_GG] = self[5];
-  }
-  int count = count0;
-  if (a.reset) h.ist[IST_COUNT] = 0;
-  if (a.has_pair) {
-    const double ys = self[1];
-    h.scal[SC_YS] = ys;
-    bool acc;
-    if (a.policy == POL_SLBFGS) acc = fabs(ys) > 1e-10;
-    else acc = ys > 1e-10;
-    if (a.want_dir < 0) acc = true; // explicit-history upload (lbf_two_loop): always push
-    h.scal[SC_ACCEPT] = acc ? 1.0 : 0.0;
-    if (acc) {
-      h.rho[w] = 1.0 / ys;
-      int *order = h.ist + IST_ORDER;
-      if (count < h.m) {
-        order[count] = w;
-        ++count;
-        if (a.policy != POL_CUDA || count < h.m) {
-          // next free slot: any of the m+1 slots not live
-          int f = 0;
-          for (; f < S_; ++f) {
-            bool live = false;
-            for (int q = 0; q < count; ++q) live |= (order[q] == f);
-            if (!live) break;
-          }
-          h.ist[IST_FREE] = f;
-        }
-      } else {
-        const int evicted = order[0];
-        for (int q = 0; q + 1 < h.m; ++q) order[q] = order[q + 1];
-        order[h.m - 1] = w;
-        if (w != evicted) h.ist[IST_FREE] = evicted;
-      }
-      h.ist[IST_COUNT] = count;
-    }
-  }
-  h.scal[SC_COUNT] = double(count);
-}
-
-// ---------------------------------------------------------------------------------------------
-// History: the two-loop recursion on coefficients (one wave).
-// With q = g - sum_j alpha_j y_j and z = gamma*q + sum_j (alpha_j - beta_j) s_j, the reference's
-// loops (lbfgs.hpp:119-136) become two triangular recurrences on the Gram entries:
+// History step (one workgroup): (A) reduce the Gram sweep's per-workgroup partials, (B) write the
+// new pair's Gram rows and g-dots, apply the acceptance rule of the policy (CPU lbfgs.hpp:77-84
+// ys > 1e-10; CUDA lbfgs.cuh:160 ys > 1e-10; S-LBFGS s_lbfgs.hpp:253 |ys| > 1e-10) and push/evict
+// like RingBuffer::push_back (ring_buffer.hpp:43-59), (C) run the two-loop recursion on
+// coefficients. With q = g - sum_j alpha_j y_j and z = gamma*q + sum_j (alpha_j - beta_j) s_j, the
+// reference's loops (lbfgs.hpp:119-136) are two triangular recurrences on Gram entries:
 //   backward  alpha_i = rho_i * (gS_i - sum_{j>i} alpha_j SY[i][j])
 //   forward   beta_i  = rho_i * (gamma*(gY_i - sum_j alpha_j YY[i][j]) + sum_{j<i} (alpha_j-beta_j) SY[j][i])
-// and z has coefficients  cs_i = alpha_i - beta_i, cy_i = -gamma*alpha_i, cg = gamma.
-// Lane l keeps the running sum of row l; SY (live k x k) is staged in LDS.
+// and z = sum_i (alpha_i - beta_i) s_i - gamma*alpha_i y_i + gamma*g. Entries that involve the slot
+// written in this step come from the freshly reduced dots (LDS), never from global memory written by
+// this same kernel. Lane l of wave 0 owns rows l and l+64 of the recurrences; the per-step scalar
+// travels by __shfl.
 // ---------------------------------------------------------------------------------------------
 static constexpr int COEF_MAXK = 128;
 
-__global__ __launch_bounds__(64) void hist_dir_kernel(const CoefArgs a) {
-  extern __shared__ double sy[]; // k*k, sy[i*k + j] = s_i . y_j (logical)
-  __shared__ double alpha_s[COEF_MAXK], c_s[COEF_MAXK];
-  __shared__ int L[COEF_MAXK];
+__global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
+  extern __shared__ double sy[]; // [k][k] live s_i . y_j after the push (logical order)
+  __shared__ double dots[6 * COEF_MAXK + 6];
+  __shared__ double gS_l[COEF_MAXK], gY_l[COEF_MAXK], rho_l[COEF_MAXK], alpha_l[COEF_MAXK], c_l[COEF_MAXK];
+  __shared__ int L0[COEF_MAXK + 1], L[COEF_MAXK + 1], inv0[COEF_MAXK + 1];
+  __shared__ int s_count0, s_w, s_k;
+  __shared__ double s_rhow;
   const HistView &h = a.h;
-  const int S_ = h.slots;
-  const int lane = threadIdx.x;
-  const int k = h.ist[IST_COUNT];
-  for (int i = lane; i < k; i += 64) L[i] = h.ist[IST_ORDER + i];
+  const int S_ = h.slots, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t == 0) {
+    s_count0 = a.reset ? 0 : h.ist[IST_COUNT];
+    s_w = h.ist[IST_WSLOT];
+  }
+  for (int i = t; i < S_; i += 256) inv0[i] = -1;
   __syncthreads();
-  for (int e = lane; e < k * k; e += 64) {
-    const int i = e / k, j = e - i * k;
-    sy[e] = h.SY[L[i] * S_ + L[j]];
+  const int count0 = s_count0, w = s_w;
+  for (int i = t; i < count0; i += 256) {
+    const int j = h.ist[IST_ORDER + i];
+    L0[i] = j;
+    inv0[j] = i;
+  }
+  // ---- A: reduce the columns in use (one wave per column, fixed order) ----
+  const int ncols = 6 * h.m + 6;
+  const int nneed = 6 * count0 + 6;
+  for (int q = wave; q < nneed; q += 4) {
+    const int col = q < 6 * count0 ? q : 6 * h.m + (q - 6 * count0);
+    double s = 0.0;
+    for (int r = lane; r < a.nwg; r += 64) s += a.partials[(long long)r * ncols + col];
+    s = wave_sum(s);
+    if (lane == 0) dots[col] = s;
   }
   __syncthreads();
-  const double gg = h.scal[SC_GG];
+  const double *self = dots + 6 * h.m;
+  // ---- B: Gram rows of the new pair and the g-dots -> global (consumed by later steps) ----
+  if (wave == 0) {
+    for (int i = lane; i < count0; i += 64) {
+      const int j = L0[i];
+      if (a.has_pair && j == w) continue;
+      if (a.has_pair) {
+        h.SS[w * S_ + j] = dots[6 * i + 0];
+        h.SS[j * S_ + w] = dots[6 * i + 0];
+        h.SY[w * S_ + j] = dots[6 * i + 1]; // s_w . y_j
+        h.SY[j * S_ + w] = dots[6 * i + 2]; // s_j . y_w
+        h.YY[w * S_ + j] = dots[6 * i + 3];
+        h.YY[j * S_ + w] = dots[6 * i + 3];
+      }
+      if (a.has_g) {
+        h.gS[j] = dots[6 * i + 4];
+        h.gY[j] = dots[6 * i + 5];
+      }
+    }
+  }
+  if (t == 0) {
+    if (a.has_pair) {
+      h.SS[w * S_ + w] = self[0];
+      h.SY[w * S_ + w] = self[1];
+      h.YY[w * S_ + w] = self[2];
+      if (a.has_g) {
+        h.gS[w] = self[3];
+        h.gY[w] = self[4];
+      }
+    }
+    if (a.has_g) h.scal[SC_GG] = self[5];
+    int count = count0;
+    for (int i = 0; i < count0; ++i) L[i] = L0[i];
+    s_rhow = (a.has_pair && w < S_) ? h.rho[w] : 0.0;
+    if (a.reset) h.ist[IST_COUNT] = 0;
+    if (a.has_pair) {
+      const double ys = self[1];
+      h.scal[SC_YS] = ys;
+      bool acc = (a.policy == POL_SLBFGS) ? fabs(ys) > 1e-10 : ys > 1e-10;
+      if (a.want_dir < 0) acc = true; // explicit-history upload (lbf_two_loop): always push
+      h.scal[SC_ACCEPT] = acc ? 1.0 : 0.0;
+      if (acc) {
+        s_rhow = 1.0 / ys;
+        h.rho[w] = s_rhow;
+        if (count < h.m) {
+          L[count++] = w;
+          if (a.policy != POL_CUDA || count < h.m) {
+            int f = 0; // next free slot: any of the m+1 slots not live
+            for (; f < S_; ++f) {
+              bool live = false;
+              for (int q = 0; q < count; ++q) live |= (L[q] == f);
+              if (!live) break;
+            }
+            h.ist[IST_FREE] = f;
+          }
+        } else {
+          const int evicted = L[0];
+          for (int q = 0; q + 1 < h.m; ++q) L[q] = L[q + 1];
+          L[h.m - 1] = w;
+          if (w != evicted) h.ist[IST_FREE] = evicted;
+        }
+        for (int q = 0; q < count; ++q) h.ist[IST_ORDER + q] = L[q];
+        h.ist[IST_COUNT] = count;
+      }
+    }
+    h.scal[SC_COUNT] = double(count);
+    s_k = count;
+  }
+  __syncthreads();
+  if (a.want_dir <= 0) return;
+
+  // ---- C1: stage the live quantities ----
+  const int k = s_k;
+  auto SYv = [&](int p, int q) -> double { // s_p . y_q
+    if (a.has_pair) {
+      if (p == w && q == w) return self[1];
+      if (p == w) return dots[6 * inv0[q] + 1];
+      if (q == w) return dots[6 * inv0[p] + 2];
+    }
+    return h.SY[p * S_ + q];
+  };
+  auto YYv = [&](int p, int q) -> double {
+    if (a.has_pair) {
+      if (p == w && q == w) return self[2];
+      if (p == w) return dots[6 * inv0[q] + 3];
+      if (q == w) return dots[6 * inv0[p] + 3];
+    }
+    return h.YY[p * S_ + q];
+  };
+  for (int e = t; e < k * k; e += 256) {
+    const int i = e / k, j = e - i * k;
+    sy[e] = SYv(L[i], L[j]);
+  }
+  for (int i = t; i < k; i += 256) {
+    const int j = L[i];
+    const bool fresh = a.has_pair && j == w;
+    if (a.has_g) {
+      gS_l[i] = fresh ? self[3] : dots[6 * inv0[j] + 4];
+      gY_l[i] = fresh ? self[4] : dots[6 * inv0[j] + 5];
+    } else {
+      gS_l[i] = h.gS[j];
+      gY_l[i] = h.gY[j];
+    }
+    rho_l[i] = fresh ? s_rhow : h.rho[j];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+
+  // ---- C2: the recurrences (wave 0) ----
+  const double gg = a.has_g ? self[5] : h.scal[SC_GG];
   double gamma = 1.0;
   if (k > 0) {
-    const int last = L[k - 1];
-    const double ys = h.SY[last * S_ + last], yy = h.YY[last * S_ + last];
+    const double ys = sy[(k - 1) * k + (k - 1)], yy = YYv(L[k - 1], L[k - 1]);
     if (a.policy == POL_CPU) {
       gamma = ys / yy; // lbfgs.hpp:127-128, no guard
     } else if (a.policy == POL_CUDA) {
@@ -522,93 +585,51 @@ __global__ __launch_bounds__(64) void hist_dir_kernel(const CoefArgs a) {
       gamma = fmin(fmax(gamma, 1e-6), 1e6);
     }
   }
-  // backward loop: r_l = gS_l - sum_{j>l} alpha_j SY[l][j]
-  constexpr int RPL = COEF_MAXK / 64; // rows per lane (2)
-  static_assert(RPL == 2, "row ownership below assumes two rows per lane");
-  double r[RPL];
-#pragma unroll
-  for (int q = 0; q < RPL; ++q) {
-    const int l = lane + 64 * q;
-    r[q] = l < k ? h.gS[L[l]] : 0.0;
-  }
+  double r0v = lane < k ? gS_l[lane] : 0.0, r1v = lane + 64 < k ? gS_l[lane + 64] : 0.0;
   for (int i = k - 1; i >= 0; --i) {
-    // owner of row i publishes alpha_i
-    if ((i & 63) == lane) {
-      const double ri = (i >> 6) == 0 ? r[0] : r[RPL - 1];
-      alpha_s[i] = h.rho[L[i]] * ri;
-    }
-    __syncthreads();
-    const double ai = alpha_s[i];
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-      const int l = lane + 64 * q;
-      if (l < i) r[q] -= ai * sy[l * k + i];
-    }
+    const double cand = rho_l[i] * ((i >> 6) == 0 ? r0v : r1v);
+    const double ai = __shfl(cand, i & 63, 64);
+    alpha_l[i] = ai; // every lane writes the same value: later reads follow the lane's own write
+    if (lane < i) r0v -= ai * sy[lane * k + i];
+    if (lane + 64 < i) r1v -= ai * sy[(lane + 64) * k + i];
   }
-  __syncthreads();
-  // forward loop: t_l = gamma*(gY_l - sum_j alpha_j YY[l][j]) ; then triangular update with SY[i][l]
-  double t[RPL];
-#pragma unroll
-  for (int q = 0; q < RPL; ++q) {
-    const int l = lane + 64 * q;
-    t[q] = 0.0;
-    if (l < k) {
-      double acc = h.gY[L[l]];
-      for (int j = 0; j < k; ++j) acc -= alpha_s[j] * h.YY[L[l] * S_ + L[j]];
-      t[q] = gamma * acc;
-    }
+  double t0v = 0.0, t1v = 0.0;
+  if (lane < k) {
+    double acc = gY_l[lane];
+    for (int j = 0; j < k; ++j) acc -= alpha_l[j] * YYv(L[lane], L[j]);
+    t0v = gamma * acc;
+  }
+  if (lane + 64 < k) {
+    double acc = gY_l[lane + 64];
+    for (int j = 0; j < k; ++j) acc -= alpha_l[j] * YYv(L[lane + 64], L[j]);
+    t1v = gamma * acc;
   }
   for (int i = 0; i < k; ++i) {
-    if ((i & 63) == lane) {
-      const double beta = h.rho[L[i]] * ((i >> 6) == 0 ? t[0] : t[RPL - 1]);
-      c_s[i] = alpha_s[i] - beta;
-    }
-    __syncthreads();
-    const double ci = c_s[i];
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-      const int l = lane + 64 * q;
-      if (l > i && l < k) t[q] += ci * sy[i * k + l];
-    }
+    const double cand = rho_l[i] * ((i >> 6) == 0 ? t0v : t1v);
+    const double ci = alpha_l[i] - __shfl(cand, i & 63, 64);
+    c_l[i] = ci;
+    if (lane > i && lane < k) t0v += ci * sy[i * k + lane];
+    if (lane + 64 > i && lane + 64 < k) t1v += ci * sy[i * k + lane + 64];
   }
-  __syncthreads();
-  // coefficients of z; direction = dsign * z
-  double ds = a.dsign;
-  double cg = gamma;
-  // g^T z = sum cs_i gS_i + cy_i gY_i + cg*gg
+  const double ds = a.dsign;
   double part = 0.0;
-  for (int i = lane; i < k; i += 64) part += c_s[i] * h.gS[L[i]] - gamma * alpha_s[i] * h.gY[L[i]];
-  part = wave_sum(part);
-  double gTz = part + cg * gg;
-  bool fallback = false;
-  if (a.policy == POL_CUDA && a.want_dir == 1 && ds * gTz >= 0.0) {
-    // lbfgs.cuh:97-104: not a descent direction -> steepest descent and history reset
-    fallback = true;
-  }
-  if (fallback) {
-    for (int i = lane; i < k; i += 64) {
-      h.coef[i] = 0.0;
-      h.coef[S_ + i] = 0.0;
-    }
-    if (lane == 0) {
-      h.coef[2 * S_] = -1.0;
-      h.ist[IST_COUNT] = 0;
-      h.scal[SC_RESET] = 1.0;
-      h.scal[SC_COUNT] = 0.0;
-      h.scal[SC_GTP] = -gg;
-    }
-  } else {
-    for (int i = lane; i < k; i += 64) {
-      h.coef[i] = ds * c_s[i];
-      h.coef[S_ + i] = ds * (-gamma * alpha_s[i]);
-    }
-    if (lane == 0) {
-      h.coef[2 * S_] = ds * cg;
-      h.scal[SC_RESET] = 0.0;
-      h.scal[SC_GTP] = ds * gTz;
-    }
+  for (int i = lane; i < k; i += 64) part += c_l[i] * gS_l[i] - gamma * alpha_l[i] * gY_l[i];
+  const double gTz = wave_sum(part) + gamma * gg;
+  // lbfgs.cuh:97-104 (CUDA semantics only): not a descent direction -> steepest descent + reset
+  const bool fallback = a.policy == POL_CUDA && a.want_dir == 1 && ds * gTz >= 0.0;
+  for (int i = lane; i < k; i += 64) {
+    h.coef[i] = fallback ? 0.0 : ds * c_l[i];
+    h.coef[S_ + i] = fallback ? 0.0 : ds * (-gamma * alpha_l[i]);
   }
   if (lane == 0) {
+    h.coef[2 * S_] = fallback ? -1.0 : ds * gamma;
+    h.scal[SC_RESET] = fallback ? 1.0 : 0.0;
+    h.scal[SC_GTP] = fallback ? -gg : ds * gTz;
+    if (fallback) {
+      h.ist[IST_COUNT] = 0;
+      h.scal[SC_COUNT] = 0.0;
+    }
+    h.scal[SC_GG] = gg;
     h.scal[SC_GAMMA] = gamma;
     h.scal[SC_ALPHA0] = (a.iter == 0) ? fmin(1.0, 1.0 / sqrt(gg)) : 1.0;
   }
@@ -616,21 +637,16 @@ __global__ __launch_bounds__(64) void hist_dir_kernel(const CoefArgs a) {
 
 void hist_coef(hipStream_t s, const CoefArgs &a) {
   LBF_REQUIRE(a.h.m <= COEF_MAXK, "history size m must be <= 128");
-  hipLaunchKernelGGL(hist_update_kernel, dim3(1), dim3(64), 0, s, a);
-  LBF_KERNEL_CHECK();
-  if (a.want_dir > 0) {
-    const size_t shmem = size_t(a.h.m) * a.h.m * sizeof(double);
-    static bool attr_set = false;
-    if (!attr_set) {
-      LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(hist_dir_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, COEF_MAXK * COEF_MAXK * 8));
-      attr_set = true;
-    }
-    hipLaunchKernelGGL(hist_dir_kernel, dim3(1), dim3(64), shmem, s, a);
-    LBF_KERNEL_CHECK();
+  static bool attr_set = false;
+  if (!attr_set) {
+    LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(hist_step_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, COEF_MAXK * COEF_MAXK * 8));
+    attr_set = true;
   }
+  const size_t shmem = size_t(a.h.m) * a.h.m * sizeof(double);
+  hipLaunchKernelGGL(hist_step_kernel, dim3(1), dim3(256), shmem, s, a);
+  LBF_KERNEL_CHECK();
 }
-
 // ---------------------------------------------------------------------------------------------
 // History: linear-combination sweep  dir = sum_i cs_i S_i + cy_i Y_i + cg g  (fp64 per element),
 // fused with the trial point x_out = x_in + alpha*dir (and an optional second copy).
@@ -702,6 +718,61 @@ __global__ void hist_reset_kernel(HistView h) {
 }
 void hist_reset(hipStream_t s, const HistView &h) {
   hipLaunchKernelGGL(hist_reset_kernel, dim3(1), dim3(1), 0, s, h);
+  LBF_KERNEL_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Evaluation tail (one workgroup): fixed-order reductions of the finalize dots (g.g, g.p, w.w) and,
+// on a single rank, of the SSE partials; then the loss (0.5*sse*inv_scale + 0.5*lambda*w.w).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void eval_tail_kernel(const double *dots_part, int nd, const double *sse_part,
+                                                        int nsse, const float *hilo, double inv_scale,
+                                                        double lambda, double *scal) {
+  __shared__ double v[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double s = 0.0;
+  if (wave < 3) {
+    for (int r = lane; r < nd; r += 64) s += dots_part[r * 3 + wave];
+  } else if (!hilo) {
+    for (int r = lane; r < nsse; r += 64) s += sse_part[r];
+  }
+  s = wave_sum(s);
+  if (lane == 0) v[wave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double sse = hilo ? (double(hilo[0]) + double(hilo[1])) : v[3];
+    scal[SC_TGG] = v[0];
+    scal[SC_TGP] = v[1];
+    scal[SC_WW] = v[2];
+    scal[SC_SSE] = sse;
+    double loss = 0.5 * sse * inv_scale;
+    if (lambda != 0.0) loss += 0.5 * lambda * v[2];
+    scal[SC_LOSS] = loss;
+  }
+}
+
+void eval_tail(hipStream_t s, const double *dots_part, int nd, const double *sse_part, int nsse, const float *hilo,
+               double inv_scale, double lambda, double *scal) {
+  hipLaunchKernelGGL(eval_tail_kernel, dim3(1), dim3(256), 0, s, dots_part, nd, sse_part, nsse, hilo, inv_scale,
+                     lambda, scal);
+  LBF_KERNEL_CHECK();
+}
+
+// Data-parallel: reduce this rank's SSE partials and store them as an fp32 (hi, lo) pair behind the
+// gradient, so one all-reduce of [grad | hi | lo] carries the loss with ~fp64 accuracy.
+__global__ __launch_bounds__(64) void sse_pack_kernel(const double *sse_part, int nsse, float *hilo) {
+  double s = 0.0;
+  for (int r = threadIdx.x; r < nsse; r += 64) s += sse_part[r];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) {
+    const float hi = float(s);
+    hilo[0] = hi;
+    hilo[1] = float(s - double(hi));
+  }
+}
+
+void sse_pack(hipStream_t s, const double *sse_part, int nsse, float *hilo) {
+  hipLaunchKernelGGL(sse_pack_kernel, dim3(1), dim3(64), 0, s, sse_part, nsse, hilo);
   LBF_KERNEL_CHECK();
 }
 

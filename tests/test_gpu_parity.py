@@ -45,6 +45,10 @@ NETS = [
     ([37, 50, 3], ["tanh", "sigmoid"]),
     ([64, 96, 33, 1], ["sigmoid", "tanh", "linear"]),
     ([129, 130, 65, 10], ["relu", "tanh", "linear"]),
+    # generic output path (no fused head): Out > 16, hidden > 256, single layer
+    ([784, 300, 20], ["relu", "linear"]),
+    ([16, 300, 4], ["tanh", "linear"]),
+    ([50, 7], ["sigmoid"]),
 ]
 
 
@@ -55,9 +59,14 @@ def test_loss_grad_matches_oracle(ctx, pkg, O, dims, acts, N):
     net = pkg.Mlp(ctx, dims, acts)
     P = net.init_params(123, "cpu")
     loss, g = net.loss_grad(P, dev(X), dev(Y))
-    l_ref, g_ref = O.Net(dims, acts).loss_grad(host(P), X, Y)
+    onet = O.Net(dims, acts)
+    l_ref, g_ref = onet.loss_grad(host(P), X, Y)
     assert abs(loss - l_ref) <= LOSS_RTOL * abs(l_ref)
-    assert rel(host(g), g_ref) <= GRAD_RTOL
+    # Tolerance = max(1e-4, 3x the rounding error of the reference algorithm itself run in fp32, i.e.
+    # the oracle's fp32 instantiation vs fp64): some shapes cancel heavily (784-300-20 on N(0,1)
+    # inputs loses ~4e-4 in ANY fp32 evaluation; the HIP result agrees with the fp32 oracle there).
+    _, g32 = onet.loss_grad_f32(host(P), X, Y)
+    assert rel(host(g), g_ref) <= max(GRAD_RTOL, 3.0 * rel(g32, g_ref))
 
 
 def test_forward_matches_oracle(ctx, pkg, O):
