@@ -150,6 +150,14 @@ int lbf_lbfgs_begin(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, 
 int lbf_lbfgs_iterate(lbf_lbfgs *s, int iters, lbf_record *rec, lbf_solve_info *info);
 int lbf_lbfgs_end(lbf_lbfgs *s);
 
+/* L-BFGS on an arbitrary objective given as a callback with the reference's LossGradFun contract
+ * (src/cuda/minimizer_base.cuh:15-16: loss returned, gradient written to device memory), i.e. the
+ * CudaMinimizerBase::solve(n, params, ..., loss_grad) entry point (minimizer_base.cuh:54-59). The
+ * history, two-loop and line-search state stay on the device; the callback is invoked once per trial. */
+typedef double (*lbf_loss_grad_fn)(void *user, const float *d_params, float *d_grad);
+int lbf_lbfgs_solve_fn(lbf_ctx *ctx, const lbf_lbfgs_params *prm, long long n, float *d_params,
+                       lbf_loss_grad_fn fn, void *user, lbf_record *rec, lbf_solve_info *info);
+
 /* S-LBFGS (SLBFGS::stochastic_solve s_lbfgs.hpp:165-290 via UnifiedSLBFGS_CPU,
  * unified_optimization.hpp:306-408). X/Y hold all N rows on every rank; minibatches are sampled on
  * the host with the reference's libstdc++ stream and sliced across ranks. */
@@ -162,6 +170,13 @@ int lbf_slbfgs_solve(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params
  * (The reference times whole iterations only: lbfgs.cuh:80-87, 176-182.) */
 int lbf_prof_enable(lbf_ctx *ctx, int on);
 int lbf_prof_read(lbf_ctx *ctx, int cap, int *ids, double *ms, long long *counts, int *n_out);
+
+/* ---- device memory, so C/C++ consumers need no HIP headers (the reference's DeviceBuffer,
+ * src/cuda/device_buffer.cuh:7-96). kind: 0 host->device, 1 device->host, 2 device->device;
+ * lbf_memcpy is ordered on the context stream and returns when the copy is complete. */
+int lbf_device_alloc(lbf_ctx *ctx, size_t bytes, void **out);
+int lbf_device_free(lbf_ctx *ctx, void *p);
+int lbf_memcpy(lbf_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
 
 /* ---- host helpers (not on the timed path) ------------------------------------------------------
  * Synthetic MNIST-shaped data (SURVEY.md §8(d) recipe), row-major [N][In] / [N][classes]. */

@@ -92,6 +92,11 @@ def lib():
                                       C.POINTER(_vp)]),
         "lbf_lbfgs_iterate": (C.c_int, [_vp, C.c_int, C.POINTER(Record), C.POINTER(SolveInfo)]),
         "lbf_lbfgs_end": (C.c_int, [_vp]),
+        "lbf_lbfgs_solve_fn": (C.c_int, [_vp, C.POINTER(LbfgsParams), C.c_longlong, _vp, _vp, _vp,
+                                         C.POINTER(Record), C.POINTER(SolveInfo)]),
+        "lbf_device_alloc": (C.c_int, [_vp, C.c_size_t, C.POINTER(_vp)]),
+        "lbf_device_free": (C.c_int, [_vp, _vp]),
+        "lbf_memcpy": (C.c_int, [_vp, _vp, _vp, C.c_size_t, C.c_int]),
         "lbf_slbfgs_solve": (C.c_int, [_vp, C.POINTER(SlbfgsParams), _vp, _vp, _vp, C.c_longlong, C.POINTER(Record),
                                        C.POINTER(SolveInfo)]),
         "lbf_prof_enable": (C.c_int, [_vp, C.c_int]),
@@ -111,7 +116,7 @@ EXPORTS = ("lbf_last_error lbf_version lbf_ctx_create lbf_ctx_destroy lbf_ctx_sy
            "lbf_comm_unique_id lbf_comm_init lbf_comm_rank lbf_allreduce_sum lbf_mlp_create lbf_mlp_destroy "
            "lbf_mlp_param_count lbf_mlp_init_params lbf_init_params_host lbf_mlp_forward lbf_mlp_loss_grad lbf_two_loop lbf_dot "
            "lbf_nrm2 lbf_axpy lbf_scal lbf_lbfgs_default_params lbf_slbfgs_default_params lbf_lbfgs_solve "
-           "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_slbfgs_solve lbf_prof_enable lbf_prof_read lbf_synth_mnist "
+           "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_prof_enable lbf_prof_read lbf_synth_mnist "
            "lbf_sample_indices").split()
 
 

@@ -22,6 +22,7 @@ struct lbf_mlp {
   std::unique_ptr<Mlp> net;
 };
 struct lbf_lbfgs {
+  std::unique_ptr<Objective> obj;
   std::unique_ptr<LbfgsSolver> s;
 };
 
@@ -337,9 +338,12 @@ int lbf_lbfgs_begin(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, 
     LBF_REQUIRE(net && prm && out, "null argument");
     LBF_REQUIRE(prm->m >= 0 && prm->m <= 128, "m in [0, 128]");
     net->ctx->c.set_device();
+    LBF_REQUIRE(d_params && d_X && d_Y, "null pointer");
+    LBF_REQUIRE(n_local >= 0 && n_global > 0, "batch sizes");
     auto *s = new lbf_lbfgs();
     try {
-      s->s.reset(new LbfgsSolver(net->net.get(), *prm, d_params, d_X, d_Y, n_local, n_global));
+      s->obj.reset(new MlpObjective(net->net.get(), d_X, d_Y, n_local, n_global));
+      s->s.reset(new LbfgsSolver(s->obj.get(), *prm, d_params));
     } catch (...) {
       delete s;
       throw;
@@ -375,6 +379,50 @@ int lbf_lbfgs_solve(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, 
   r = lbf_lbfgs_iterate(s, prm->max_iters, rec, info);
   lbf_lbfgs_end(s);
   return r;
+}
+
+int lbf_lbfgs_solve_fn(lbf_ctx *ctx, const lbf_lbfgs_params *prm, long long n, float *d_params,
+                       lbf_loss_grad_fn fn, void *user, lbf_record *rec, lbf_solve_info *info) {
+  if (!d_params || n <= 0) { // lbfgs.cuh:45-48
+    if (info) std::memset(info, 0, sizeof(*info));
+    return LBF_OK;
+  }
+  return guard([&] {
+    LBF_REQUIRE(ctx && prm && fn, "null argument");
+    LBF_REQUIRE(prm->m >= 0 && prm->m <= 128, "m in [0, 128]");
+    ctx->c.set_device();
+    CallbackObjective obj(&ctx->c, n, fn, user);
+    LbfgsSolver s(&obj, *prm, d_params);
+    s.iterate(prm->max_iters, rec);
+    s.info(info);
+  });
+}
+
+int lbf_device_alloc(lbf_ctx *ctx, size_t bytes, void **out) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && out, "null argument");
+    ctx->c.set_device();
+    *out = nullptr;
+    if (bytes) LBF_HIP(hipMalloc(out, bytes));
+  });
+}
+
+int lbf_device_free(lbf_ctx *ctx, void *p) {
+  return guard([&] {
+    LBF_REQUIRE(ctx, "ctx");
+    ctx->c.set_device();
+    if (p) LBF_HIP(hipFree(p));
+  });
+}
+
+int lbf_memcpy(lbf_ctx *ctx, void *dst, const void *src, size_t bytes, int kind) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && (bytes == 0 || (dst && src)) && kind >= 0 && kind <= 2, "bad argument");
+    ctx->c.set_device();
+    const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : (kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
+    if (bytes) LBF_HIP(hipMemcpyAsync(dst, src, bytes, k, ctx->c.stream));
+    LBF_HIP(hipStreamSynchronize(ctx->c.stream));
+  });
 }
 
 int lbf_slbfgs_solve(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params, const float *d_X,

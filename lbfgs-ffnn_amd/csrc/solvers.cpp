@@ -30,12 +30,20 @@ std::vector<size_t> sample_minibatch(size_t N, size_t b, std::mt19937 &rng) {
 // ================================================================================================
 // Full-batch L-BFGS
 // ================================================================================================
-LbfgsSolver::LbfgsSolver(Mlp *net, const lbf_lbfgs_params &prm, float *d_params, const float *X, const float *Y,
-                         long long n_local, long long n_global)
-    : net_(net), ctx_(net->ctx()), prm_(prm), user_params_(d_params), X_(X), Y_(Y), nloc_(n_local),
-      nglob_(n_global), n_((long long)net->nparams()), hist_(net->ctx(), prm.m, (long long)net->nparams()) {
-  LBF_REQUIRE(d_params && X && Y, "null pointer");
-  LBF_REQUIRE(n_local >= 0 && n_global > 0, "batch sizes");
+void CallbackObjective::eval(const float *x, float *g, const float *pdir, double *scal) {
+  LBF_HIP(hipStreamSynchronize(c->stream)); // x is complete before the host callback reads it
+  hl[0] = fn(user, x, g);
+  ++count;
+  const int nd = dots_partials_wg(nn);
+  finalize_grad_dots(c->stream, nn, g, x, 0.0, pdir, part.get());
+  eval_tail(c->stream, part.get(), nd, part.get(), 0, nullptr, 0.0, 0.0, scal);
+  LBF_HIP(hipMemcpyAsync(scal + SC_LOSS, hl.get(), sizeof(double), hipMemcpyHostToDevice, c->stream));
+}
+
+LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_params)
+    : obj_(obj), ctx_(obj->ctx()), prm_(prm), user_params_(d_params), n_(obj->n()),
+      hist_(obj->ctx(), prm.m, obj->n()) {
+  LBF_REQUIRE(d_params, "null pointer");
   LBF_REQUIRE(prm.max_line_iters >= 1, "max_line_iters >= 1");
   for (int i = 0; i < 3; ++i) {
     xbuf_[i].resize(size_t(round4(n_)));
@@ -59,9 +67,7 @@ LbfgsSolver::LbfgsSolver(Mlp *net, const lbf_lbfgs_params &prm, float *d_params,
   t0_ = std::chrono::steady_clock::now();
 }
 
-void LbfgsSolver::eval(const float *x, float *g, const float *pdir) {
-  net_->loss_grad(x, g, X_, Y_, nullptr, nloc_, 1.0 / double(nglob_), 0.0, pdir, hist_.scal());
-}
+void LbfgsSolver::eval(const float *x, float *g, const float *pdir) { obj_->eval(x, g, pdir, hist_.scal()); }
 
 void LbfgsSolver::read_status() {
   LBF_HIP(hipMemcpyAsync(hs_.get(), hist_.scal(), SC_N * sizeof(double), hipMemcpyDeviceToHost, ctx_->stream));
@@ -253,7 +259,7 @@ int LbfgsSolver::iterate_armijo(int iters, lbf_record *rec) {
 void LbfgsSolver::info(lbf_solve_info *out) const {
   if (!out) return;
   out->iterations = iter_;
-  out->n_evals = net_->evals();
+  out->n_evals = obj_->evals();
   out->final_loss = loss_;
   out->final_grad_norm = std::sqrt(gg_);
 }

@@ -9,12 +9,58 @@
 
 namespace lbf {
 
+// What the minimizer evaluates: the reference's LossGradFun (src/cuda/minimizer_base.cuh:15-16) plus the
+// dots the line search needs. eval() writes the gradient into g (n+2 floats) and SC_LOSS / SC_TGG /
+// SC_TGP (g.pdir) into the device status block scal, all on ctx()->stream.
+struct Objective {
+  virtual ~Objective() = default;
+  virtual Ctx *ctx() const = 0;
+  virtual long long n() const = 0;
+  virtual void eval(const float *x, float *g, const float *pdir, double *scal) = 0;
+  virtual long long evals() const = 0;
+};
+
+// The MLP's fused loss+grad over the rank's shard (mean over n_global samples).
+struct MlpObjective : Objective {
+  Mlp *net;
+  const float *X, *Y;
+  long long nloc, nglob;
+  MlpObjective(Mlp *m, const float *x, const float *y, long long nl, long long ng)
+      : net(m), X(x), Y(y), nloc(nl), nglob(ng) {}
+  Ctx *ctx() const override { return net->ctx(); }
+  long long n() const override { return (long long)net->nparams(); }
+  void eval(const float *x, float *g, const float *pdir, double *scal) override {
+    net->loss_grad(x, g, X, Y, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal);
+  }
+  long long evals() const override { return net->evals(); }
+};
+
+// A user callback with the reference's LossGradFun contract: returns the loss, writes the gradient
+// (device) for the device parameters it is given. Host-driven, so the stream is synchronised first.
+struct CallbackObjective : Objective {
+  Ctx *c;
+  long long nn;
+  double (*fn)(void *, const float *, float *);
+  void *user;
+  DevBuf<double> part;
+  PinnedBuf<double> hl;
+  long long count = 0;
+  CallbackObjective(Ctx *cx, long long n_, double (*f)(void *, const float *, float *), void *u)
+      : c(cx), nn(n_), fn(f), user(u) {
+    part.resize(size_t(dots_partials_wg(n_)) * 3);
+    hl.ensure(1);
+  }
+  Ctx *ctx() const override { return c; }
+  long long n() const override { return nn; }
+  void eval(const float *x, float *g, const float *pdir, double *scal) override;
+  long long evals() const override { return count; }
+};
+
 // Full-batch L-BFGS on the MLP. All vectors, the (s, y) ring and its Gram state stay on the device;
 // the host only reads a 16-double status block once per line-search trial.
 class LbfgsSolver {
 public:
-  LbfgsSolver(Mlp *net, const lbf_lbfgs_params &prm, float *d_params, const float *X, const float *Y,
-              long long n_local, long long n_global);
+  LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_params);
   // Runs up to `iters` iterations. Returns the number run (fewer on convergence).
   int iterate(int iters, lbf_record *rec);
   void info(lbf_solve_info *out) const;
@@ -28,12 +74,10 @@ private:
   int iterate_armijo(int iters, lbf_record *rec);
   void record(lbf_record *rec, double loss, double gnorm, double alpha, int trials, int accepted);
 
-  Mlp *net_;
+  Objective *obj_;
   Ctx *ctx_;
   lbf_lbfgs_params prm_;
   float *user_params_;
-  const float *X_, *Y_;
-  long long nloc_, nglob_;
   long long n_;
   History hist_;
   DevBuf<float> xbuf_[3], gbuf_[3], p_;

@@ -89,3 +89,12 @@ def test_flop_model():
     assert pkg.grad_flops_per_sample([784, 128, 64, 10]) == 454400
     assert pkg.grad_flops_per_sample([784, 512, 256, 10]) == 2407424
     assert pkg.grad_flops_per_sample([4096, 2048, 1024, 1]) == 46143488
+
+
+def test_cpp_header_compiles_with_plain_gxx(tmp_path):
+    """include/lbfgs_amd/hip_backend.hpp needs no HIP/Eigen/torch headers (C++17 + the C ABI)."""
+    src = tmp_path / "t.cpp"
+    src.write_text('#include "lbfgs_amd/hip_backend.hpp"\nint main(){ UnifiedConfig c; (void)c; return 0; }\n')
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", f"-I{os.path.join(ROOT, 'include')}",
+                        str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
