@@ -169,6 +169,9 @@ int lbf_slbfgs_solve(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params
  * 5 finalize, 6 Gram sweep, 7 coefficients, 8 combine sweep, 9 line-search axpy, 10 all-reduce.
  * (The reference times whole iterations only: lbfgs.cuh:80-87, 176-182.) */
 int lbf_prof_enable(lbf_ctx *ctx, int on);
+/* Restrict timing to one section id (-1: all). Two events per launch of that section only, so the
+ * timed region of a benchmark is not serialised by event packets around every kernel. */
+int lbf_prof_select(lbf_ctx *ctx, int section_id);
 int lbf_prof_read(lbf_ctx *ctx, int cap, int *ids, double *ms, long long *counts, int *n_out);
 
 /* ---- device memory, so C/C++ consumers need no HIP headers (the reference's DeviceBuffer,

@@ -448,6 +448,13 @@ int lbf_prof_enable(lbf_ctx *ctx, int on) {
   });
 }
 
+int lbf_prof_select(lbf_ctx *ctx, int section_id) {
+  return guard([&] {
+    LBF_REQUIRE(ctx, "ctx");
+    ctx->c.prof.only = section_id < 0 ? -1 : section_id;
+  });
+}
+
 int lbf_prof_read(lbf_ctx *ctx, int cap, int *ids, double *ms, long long *counts, int *n_out) {
   return guard([&] {
     LBF_REQUIRE(ctx && n_out, "null argument");

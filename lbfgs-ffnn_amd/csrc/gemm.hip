@@ -58,6 +58,7 @@ struct GemmK {
   const float *aux;
   long long ldaux;
   int aux_act;
+  const int *abort;
 };
 
 // k-contiguous operand: R rows x 32 k. Thread chunk c -> row c>>3, k-quad c&7.
@@ -133,6 +134,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
   constexpr int ASZ = AKC ? BM * LDK : BK * (BM + 4);
   constexpr int BSZ = BKC ? BN * LDK : BK * (BN + 4);
   __shared__ __attribute__((aligned(16))) float lds[2 * (ASZ + BSZ)];
+  if (g.abort && *g.abort) return;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -284,6 +286,7 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.aux = d.aux;
   k.ldaux = d.ldaux;
   k.aux_act = d.aux_act;
+  k.abort = d.abort;
   dim3 grid((d.N + BN - 1) / BN, (d.M + BM - 1) / BM, d.splits > 1 ? d.splits : 1);
   if (d.a_idx)
     hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true>), grid, dim3(256), 0, s, k);

@@ -60,7 +60,9 @@ __device__ __forceinline__ int round64(int x) { return (x + 63) & ~63; }
 
 __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const float *P, int Out, const float *Y,
                                                    const int *idx, long long B, int act_out, int act_prev,
-                                                   double inv_scale, float *delta, float *slab, double *sse_part) {
+                                                   double inv_scale, float *delta, float *slab, double *sse_part,
+                                                   const int *abort) {
+  if (abort && *abort) return;
   extern __shared__ __attribute__((aligned(16))) float sh[];
   const int Hp = round64(H);
   const int LDA = Hp + 4;
@@ -235,7 +237,7 @@ int head_nwg(long long B, int) {
 
 void head_fused(hipStream_t s, const float *A, int H, const float *P, int Out, const float *Y, const int *idx,
                 long long B, int act_out, int act_prev, double inv_scale, float *delta, float *slab,
-                double *sse_part) {
+                double *sse_part, const int *abort) {
   const int Hp = (H + 63) & ~63;
   const size_t shmem = (size_t(TB) * (Hp + 4) + size_t(16) * (Hp + 4) + size_t(Hp) * 16 + size_t(TB) * LDZ) *
                        sizeof(float);
@@ -246,7 +248,7 @@ void head_fused(hipStream_t s, const float *A, int H, const float *P, int Out, c
     set = true;
   }
   hipLaunchKernelGGL(head_kernel, dim3(head_nwg(B, H)), dim3(256), shmem, s, A, H, P, Out, Y, idx, B, act_out,
-                     act_prev, inv_scale, delta, slab, sse_part);
+                     act_prev, inv_scale, delta, slab, sse_part, abort);
   LBF_KERNEL_CHECK();
 }
 

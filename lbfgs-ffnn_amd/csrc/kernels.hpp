@@ -42,6 +42,7 @@ struct GemmDesc {
   const float *aux = nullptr;
   long long ldaux = 0;
   int aux_act = ACT_LINEAR;
+  const int *abort = nullptr; // speculative execution: the kernel is a no-op when *abort != 0
 };
 
 void gemm(hipStream_t s, const GemmDesc &d);
@@ -67,15 +68,16 @@ int head_tile(int H);
 int head_nwg(long long B, int H);
 void head_fused(hipStream_t s, const float *A, int H, const float *P, int Out, const float *Y, const int *idx,
                 long long B, int act_out, int act_prev, double inv_scale, float *delta, float *slab,
-                double *sse_part);
+                double *sse_part, const int *abort = nullptr);
 
 // grad[e] = sum_s slab[s*stride + e] * scale (fixed order), e in [0, count)
-void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride, long long count, float *grad);
+void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride, long long count, float *grad,
+                  const int *abort = nullptr);
 
 // g += lambda*w (if lambda != 0); per-WG partials of (g.g, g.p, w.w) -> partials[wg*3 + {0,1,2}]
 int dots_partials_wg(long long n);
 void finalize_grad_dots(hipStream_t s, long long n, float *g, const float *w, double lambda, const float *p,
-                        double *partials);
+                        double *partials, const int *abort = nullptr);
 // generic: per-WG partials of x.y -> partials[wg]
 void dot_partials(hipStream_t s, long long n, const float *x, const float *y, double *partials);
 
@@ -85,9 +87,9 @@ void eval_status(hipStream_t s, const double *sse_d, const float *sse_hilo, doub
                  double *scal);
 // One-workgroup tail: reduce finalize dots (+ SSE partials unless hilo) and write SC_TGG/TGP/WW/SSE/LOSS.
 void eval_tail(hipStream_t s, const double *dots_part, int nd, const double *sse_part, int nsse, const float *hilo,
-               double inv_scale, double lambda, double *scal);
+               double inv_scale, double lambda, double *scal, const int *abort = nullptr);
 // DP: reduce SSE partials into an fp32 (hi, lo) pair (all-reduced together with the gradient).
-void sse_pack(hipStream_t s, const double *sse_part, int nsse, float *hilo);
+void sse_pack(hipStream_t s, const double *sse_part, int nsse, float *hilo, const int *abort = nullptr);
 // hilo[0] = float(x), hilo[1] = float(x - hilo[0])
 void pack_hilo(hipStream_t s, const double *x, float *hilo);
 
@@ -126,8 +128,38 @@ enum {
   SC_TGP = 10,    //                  g.p
   SC_WW = 11,     //                  w.w
   SC_SSE = 12,    //                  local sum of squared errors (before reduction over ranks)
+  SC_FOLD = 13,   // speculative line search: loss of the last accepted iterate (fp64, Wolfe)
+  SC_FOLDF = 14,  //                          same, as the fp32 value the Armijo test uses
   SC_N = 16
 };
+
+// Speculative line search (LbfgsSolver::iterate_spec): after the first trial of an iteration, one
+// thread applies the host's acceptance test to the device status block, writes the outcome into a
+// host-mapped record and, on rejection or convergence, raises the abort flag so every launch already
+// queued behind it is a no-op until the host rolls back.
+struct SpecRecord {
+  double loss;        // trial loss (SC_LOSS)
+  double tgg;         // trial g.g  (SC_TGG)
+  double alpha0;      // SC_ALPHA0 (first trial step computed on the device)
+  double accept_prev; // SC_ACCEPT (whether the previous pair entered the ring)
+  int status;         // SPEC_ACCEPT / SPEC_CONVERGED / SPEC_REJECT
+  int seq;            // written last
+};
+enum { SPEC_ACCEPT = 1, SPEC_CONVERGED = 2, SPEC_REJECT = 3 };
+struct LsCtlArgs {
+  double *scal = nullptr;
+  int *abort = nullptr;
+  SpecRecord *rec = nullptr; // host-mapped
+  int seq = 0;
+  int armijo = 0;            // 0: Wolfe (lbfgs.hpp:49-70), 1: Armijo (lbfgs.cuh:159-163)
+  int first = 0;             // Wolfe: iteration 0 takes alpha0 without a search
+  int host_fold = 0;         // use fold/foldf below instead of SC_FOLD/SC_FOLDF
+  double fold = 0.0;
+  float foldf = 0.0f;
+  double c1 = 0.0, c2 = 0.0, tol = 0.0;
+  float alphaf = 1.0f;       // Armijo trial step
+};
+void ls_ctl(hipStream_t s, const LsCtlArgs &a);
 
 struct HistView {
   int m = 0, slots = 0;
@@ -137,6 +169,7 @@ struct HistView {
   double *rho = nullptr, *SS = nullptr, *SY = nullptr, *YY = nullptr, *gS = nullptr, *gY = nullptr;
   double *coef = nullptr; // [2*slots + 1]: cs (logical), cy (logical), cg
   double *scal = nullptr; // SC_N
+  const int *abort = nullptr; // speculative execution flag (nullable)
 };
 
 struct GramArgs {

@@ -145,6 +145,7 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
     d.epi = EPI_FWD;
     d.bias = P + L.off + size_t(L.in) * L.out;
     d.act = L.act;
+    d.abort = ctx_->abort;
     ProfScope ps(ctx_, PK_FWD, int(l));
     gemm(s, d);
     in = A_[l].get();
@@ -167,10 +168,10 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     {
       ProfScope ps(ctx_, PK_LOSS);
       head_fused(s, A_[nl - 2].get(), Lo.in, P + Lo.off, Lo.out, Y, idx, B, Lo.act, layers_[nl - 2].act, inv_scale,
-                 D_[nl - 2].get(), head_slab_.get(), loss_part_.get());
+                 D_[nl - 2].get(), head_slab_.get(), loss_part_.get(), ctx_->abort);
     }
     ProfScope ps(ctx_, PK_SLAB, nl - 1);
-    reduce_slabs(s, head_slab_.get(), nloss, seg, seg, G + Lo.off);
+    reduce_slabs(s, head_slab_.get(), nloss, seg, seg, G + Lo.off, ctx_->abort);
     lstart = nl - 2;
   } else {
     nloss = loss_partials_wg(std::max(1LL, B), Lo.out);
@@ -200,6 +201,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     d.ldc = L.out;
     d.splits = L.splits;
     d.k_chunk = L.k_chunk;
+    d.abort = ctx_->abort;
     const long long seg = (long long)(L.in + 1) * L.out;
     if (L.splits > 1) {
       d.C = slab_.get();
@@ -209,7 +211,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
         gemm(s, d);
       }
       ProfScope ps(ctx_, PK_SLAB, l);
-      reduce_slabs(s, slab_.get(), L.splits, seg, seg, G + L.off);
+      reduce_slabs(s, slab_.get(), L.splits, seg, seg, G + L.off, ctx_->abort);
     } else {
       d.C = G + L.off;
       ProfScope ps(ctx_, PK_DW, l);
@@ -234,6 +236,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
       x.aux = A_[l - 1].get();
       x.ldaux = L.in;
       x.aux_act = P0.act;
+      x.abort = ctx_->abort;
       ProfScope ps(ctx_, PK_DX, l);
       gemm(s, x);
     }
@@ -242,7 +245,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
   if (ctx_->nranks > 1) {
     {
       ProfScope ps(ctx_, PK_FINAL, 0);
-      sse_pack(s, loss_part_.get(), nloss, G + nparams_);
+      sse_pack(s, loss_part_.get(), nloss, G + nparams_, ctx_->abort);
     }
     ProfScope ps(ctx_, PK_ALLREDUCE);
     ctx_->allreduce(G, nparams_ + 2); // one RCCL all-reduce of [grad | sse_hi | sse_lo]
@@ -251,8 +254,8 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
   {
     ProfScope ps(ctx_, PK_FINAL, 1);
     const int nd = dots_partials_wg(nparams_);
-    finalize_grad_dots(s, nparams_, G, P, lambda, pdir, dots_part_.get());
-    eval_tail(s, dots_part_.get(), nd, loss_part_.get(), nloss, hilo, inv_scale, lambda, scal);
+    finalize_grad_dots(s, nparams_, G, P, lambda, pdir, dots_part_.get(), ctx_->abort);
+    eval_tail(s, dots_part_.get(), nd, loss_part_.get(), nloss, hilo, inv_scale, lambda, scal, ctx_->abort);
   }
   ++evals_;
 }
@@ -307,6 +310,7 @@ void History::reset() { hist_reset(ctx_->stream, v_); }
 void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
   GramArgs g = g0;
   g.h = v_;
+  g.h.abort = ctx_->abort;
   hipStream_t s = ctx_->stream;
   {
     ProfScope ps(ctx_, PK_GRAM);
@@ -314,6 +318,7 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
   }
   CoefArgs c;
   c.h = v_;
+  c.h.abort = ctx_->abort;
   c.partials = part_.get();
   c.nwg = gram_nwg(v_.n);
   c.has_pair = g.has_pair;
@@ -331,6 +336,7 @@ void History::combine(const float *g, float *dir, const float *x_in, float *x_ou
                       bool alpha_from_state, double alpha) {
   CombineArgs a;
   a.h = v_;
+  a.h.abort = ctx_->abort;
   a.g = g;
   a.dir = dir;
   a.x_in = x_in;

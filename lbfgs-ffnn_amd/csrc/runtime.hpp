@@ -17,6 +17,8 @@ enum ProfKind : int { PK_FWD = 0, PK_DW = 1, PK_DX = 2, PK_LOSS = 3, PK_SLAB = 4
                       PK_COEF = 7, PK_COMBINE = 8, PK_AXPY = 9, PK_ALLREDUCE = 10 };
 struct Profiler {
   bool on = false;
+  int only = -1; // section filter (-1: all)
+  bool want(int id) const { return on && (only < 0 || only == id); }
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   struct Rec { int id; size_t a, b; };
@@ -35,6 +37,7 @@ struct Ctx {
   bool own_stream = false;
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
+  const int *abort = nullptr; // set by a solver while it runs speculatively (see LbfgsSolver)
   // scratch for the BLAS-1 ABI helpers
   DevBuf<double> part, red;
   PinnedBuf<double> host;
@@ -55,11 +58,12 @@ struct ProfScope {
   Ctx *c;
   int id;
   size_t a = 0;
-  ProfScope(Ctx *ctx, int kind, int layer = 0) : c(ctx), id(kind * 16 + layer) {
-    if (c->prof.on) a = c->prof.mark(c->stream);
+  bool on;
+  ProfScope(Ctx *ctx, int kind, int layer = 0) : c(ctx), id(kind * 16 + layer), on(ctx->prof.want(id)) {
+    if (on) a = c->prof.mark(c->stream);
   }
   ~ProfScope() {
-    if (c->prof.on) c->prof.recs.push_back({id, a, c->prof.mark(c->stream)});
+    if (on) c->prof.recs.push_back({id, a, c->prof.mark(c->stream)});
   }
 };
 
@@ -81,6 +85,7 @@ public:
   void loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
                  double inv_scale, double lambda, const float *pdir, double *scal);
   long long evals() const { return evals_; }
+  void discard_evals(long long k) { evals_ -= k; } // speculative evaluations that were aborted
 
 private:
   void ensure(long long B);

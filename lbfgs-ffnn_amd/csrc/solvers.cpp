@@ -3,8 +3,13 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <limits>
 #include <numeric>
+
+// Host-side acceptance tests must round like ls_ctl_kernel (and the reference's host code).
+#pragma clang fp contract(off)
 
 namespace lbf {
 
@@ -57,6 +62,20 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
   gp_ = gbuf_[1].get();
   gt_ = gbuf_[2].get();
   hs_.ensure(SC_N);
+  // Speculation depth: iterations enqueued ahead of the host's line-search decision
+  // (LBF_SPEC_DEPTH, default 3; 0 = host-driven). Host callbacks synchronise anyway.
+  depth_ = 3;
+  if (const char *e = std::getenv("LBF_SPEC_DEPTH")) depth_ = std::max(0, std::min(16, std::atoi(e)));
+  if (!obj_->async()) depth_ = 0;
+  if (depth_ > 0) {
+    abort_.resize(1);
+    LBF_HIP(hipMemsetAsync(abort_.get(), 0, sizeof(int), ctx_->stream));
+    LBF_HIP(hipHostMalloc(reinterpret_cast<void **>(&spec_rec_), kSpecRing * sizeof(SpecRecord),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(spec_rec_, 0xff, kSpecRing * sizeof(SpecRecord));
+    spec_ev_.resize(kSpecRing);
+    for (auto &e : spec_ev_) LBF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   LBF_HIP(hipMemcpyAsync(x_, d_params, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, ctx_->stream));
   // initial evaluation (lbfgs.hpp:44 / lbfgs.cuh:147)
   eval(x_, g_, nullptr);
@@ -65,6 +84,11 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
   lossf_ = float(loss_);
   gg_ = hs_[SC_TGG];
   t0_ = std::chrono::steady_clock::now();
+}
+
+LbfgsSolver::~LbfgsSolver() {
+  for (auto e : spec_ev_) (void)hipEventDestroy(e);
+  if (spec_rec_) (void)hipHostFree(spec_rec_);
 }
 
 void LbfgsSolver::eval(const float *x, float *g, const float *pdir) { obj_->eval(x, g, pdir, hist_.scal()); }
@@ -93,12 +117,74 @@ void LbfgsSolver::record(lbf_record *rec, double loss, double gnorm, double alph
   rec->size = std::max(rec->size, i + 1);
 }
 
+// The accepted flag of a pair is only known when the next iteration's history step has run.
+void LbfgsSolver::mark_prev_accepted(lbf_record *rec, double flag) {
+  if (rec && rec->accepted && rec_idx_ > 0 && rec_idx_ - 1 < rec->cap) rec->accepted[rec_idx_ - 1] = int(flag);
+}
+
+bool LbfgsSolver::entry_converged() const {
+  if (prm_.line_search == LBF_LS_ARMIJO) return float(std::sqrt(gg_)) < float(prm_.tol); // lbfgs.cuh:143
+  return std::sqrt(gg_) < prm_.tol;                                                     // lbfgs.hpp:42
+}
+
 int LbfgsSolver::iterate(int iters, lbf_record *rec) {
   ctx_->set_device();
   rec_idx_ = rec ? rec->size : 0;
-  const int done = prm_.line_search == LBF_LS_ARMIJO ? iterate_armijo(iters, rec) : iterate_wolfe(iters, rec);
+  int done;
+  if (depth_ > 0)
+    done = iterate_spec(iters, rec);
+  else
+    done = prm_.line_search == LBF_LS_ARMIJO ? iterate_armijo(iters, rec) : iterate_wolfe(iters, rec);
   writeback();
   return done;
+}
+
+// x <- trial, xp <- old x, xt <- free (same rotation for g)
+void LbfgsSolver::accept_roles() {
+  std::swap(xp_, x_);
+  std::swap(x_, xt_);
+  std::swap(gp_, g_);
+  std::swap(g_, gt_);
+  pending_pair_ = prm_.m > 0;
+  ++iter_;
+}
+
+void LbfgsSolver::restore(const Roles &r) {
+  x_ = r.x;
+  xp_ = r.xp;
+  xt_ = r.xt;
+  g_ = r.g;
+  gp_ = r.gp;
+  gt_ = r.gt;
+  iter_ = r.iter;
+  pending_pair_ = r.pair;
+  pending_reset_ = r.reset;
+}
+
+float LbfgsSolver::begin_iteration() {
+  const bool armijo = prm_.line_search == LBF_LS_ARMIJO;
+  GramArgs ga;
+  ga.policy = armijo ? POL_CUDA : POL_CPU;
+  ga.has_g = 1;
+  ga.ga = g_;
+  ga.reset = (armijo && pending_reset_) ? 1 : 0;
+  if (pending_pair_) {
+    ga.has_pair = 1;
+    ga.sa = x_;
+    ga.sb = xp_;
+    ga.ya = g_;
+    ga.yb = gp_;
+  }
+  hist_.update(ga, 1, iter_, -1.0);
+  float alpha = 1.0f;
+  if (armijo) {
+    if (iter_ == 0) alpha = std::min(1.0f, 1.0f / float(std::sqrt(gg_))); // lbfgs.cuh:149
+    hist_.combine(g_, p_.get(), x_, xt_, nullptr, false, double(alpha));
+  } else {
+    hist_.combine(g_, p_.get(), x_, xt_, nullptr, true, 0.0); // xt = x + alpha0 p
+  }
+  eval(xt_, gt_, p_.get());
+  return alpha;
 }
 
 // CPU semantics: LBFGS::solve (lbfgs.hpp:38-100) + FullBatchMinimizer::line_search
@@ -106,154 +192,221 @@ int LbfgsSolver::iterate(int iters, lbf_record *rec) {
 // fused evaluation: line_search's f(x), Gradient(x) are the previous accepted trial, the trial's
 // Gradient(x+ap) comes with its f, the post-search Gradient(x_new) and the recorder's f(x) are the
 // accepted trial's. Only an exhausted search (returns an alpha it never evaluated) costs one more.
-int LbfgsSolver::iterate_wolfe(int iters, lbf_record *rec) {
+void LbfgsSolver::finish_wolfe(lbf_record *rec) {
   const double inf = std::numeric_limits<double>::infinity();
+  double alpha = hs_[SC_ALPHA0];
+  int trials = 0;
+  if (iter_ > 0) {
+    const double f_old = loss_, gfo = hs_[SC_GTP];
+    double amin = 0.0, amax = inf;
+    alpha = 1.0;
+    bool evaluated = true;
+    for (int i = 0; i < prm_.max_line_iters; ++i) {
+      if (!evaluated) {
+        {
+          ProfScope ps(ctx_, PK_AXPY);
+          axpy_to(ctx_->stream, n_, x_, float(alpha), p_.get(), xt_);
+        }
+        eval(xt_, gt_, p_.get());
+        read_status();
+        evaluated = true;
+      }
+      ++trials;
+      const double fn = hs_[SC_LOSS];
+      if (fn > f_old + prm_.c1 * alpha * gfo) {
+        amax = alpha;
+        alpha = prm_.rho * (amin + amax);
+        evaluated = false;
+        continue;
+      }
+      const double gnp = hs_[SC_TGP];
+      if (gnp < prm_.c2 * gfo) {
+        amin = alpha;
+        alpha = (amax == inf) ? alpha * 2 : prm_.rho * (amin + amax);
+        evaluated = false;
+        continue;
+      }
+      break;
+    }
+    if (!evaluated) { // exhausted: the returned alpha was never evaluated (lbfgs.hpp:67-70)
+      axpy_to(ctx_->stream, n_, x_, float(alpha), p_.get(), xt_);
+      eval(xt_, gt_, p_.get());
+      read_status();
+    }
+  }
+  accept_roles();
+  loss_ = hs_[SC_LOSS];
+  gg_ = hs_[SC_TGG];
+  record(rec, loss_, std::sqrt(gg_), alpha, trials, -1);
+}
+
+int LbfgsSolver::iterate_wolfe(int iters, lbf_record *rec) {
   int k = 0;
   for (; k < iters; ++k) {
-    if (std::sqrt(gg_) < prm_.tol) {
+    if (entry_converged()) {
       converged_ = true;
       break;
     }
-    GramArgs ga;
-    ga.policy = POL_CPU;
-    ga.has_g = 1;
-    ga.ga = g_;
-    if (pending_pair_) {
-      ga.has_pair = 1;
-      ga.sa = x_;
-      ga.sb = xp_;
-      ga.ya = g_;
-      ga.yb = gp_;
-    }
-    hist_.update(ga, 1, iter_, -1.0);
-    hist_.combine(g_, p_.get(), x_, xt_, nullptr, true, 0.0); // xt = x + alpha0 p
-    eval(xt_, gt_, p_.get());
+    const bool had_pair = pending_pair_;
+    begin_iteration();
     read_status();
-    if (pending_pair_ && rec && rec->accepted && rec_idx_ > 0 && rec_idx_ - 1 < rec->cap)
-      rec->accepted[rec_idx_ - 1] = int(hs_[SC_ACCEPT]);
-    double alpha = hs_[SC_ALPHA0];
-    int trials = 0;
-    if (iter_ > 0) {
-      const double f_old = loss_, gfo = hs_[SC_GTP];
-      double amin = 0.0, amax = inf;
-      alpha = 1.0;
-      bool evaluated = true;
-      for (int i = 0; i < prm_.max_line_iters; ++i) {
-        if (!evaluated) {
-          {
-            ProfScope ps(ctx_, PK_AXPY);
-            axpy_to(ctx_->stream, n_, x_, float(alpha), p_.get(), xt_);
-          }
-          eval(xt_, gt_, p_.get());
-          read_status();
-          evaluated = true;
-        }
-        ++trials;
-        const double fn = hs_[SC_LOSS];
-        if (fn > f_old + prm_.c1 * alpha * gfo) {
-          amax = alpha;
-          alpha = prm_.rho * (amin + amax);
-          evaluated = false;
-          continue;
-        }
-        const double gnp = hs_[SC_TGP];
-        if (gnp < prm_.c2 * gfo) {
-          amin = alpha;
-          alpha = (amax == inf) ? alpha * 2 : prm_.rho * (amin + amax);
-          evaluated = false;
-          continue;
-        }
-        break;
-      }
-      if (!evaluated) { // exhausted: the returned alpha was never evaluated (lbfgs.hpp:67-70)
-        axpy_to(ctx_->stream, n_, x_, float(alpha), p_.get(), xt_);
-        eval(xt_, gt_, p_.get());
-        read_status();
-      }
-    }
-    std::swap(xp_, x_);
-    std::swap(x_, xt_); // x <- trial, xp <- old x, xt <- free
-    std::swap(gp_, g_);
-    std::swap(g_, gt_);
-    loss_ = hs_[SC_LOSS];
-    gg_ = hs_[SC_TGG];
-    pending_pair_ = prm_.m > 0;
-    record(rec, loss_, std::sqrt(gg_), alpha, trials, -1);
-    ++iter_;
+    if (had_pair) mark_prev_accepted(rec, hs_[SC_ACCEPT]);
+    finish_wolfe(rec);
   }
   return k;
 }
 
 // CUDA semantics: CudaLBFGS::solve (lbfgs.cuh:39-194), host scalars in fp32 like the reference.
+void LbfgsSolver::finish_armijo(float alpha, lbf_record *rec) {
+  const float c1 = float(prm_.c1), rho = float(prm_.rho);
+  const float gdp = float(hs_[SC_GTP]);
+  bool ok = false;
+  int trials = 0;
+  float lnew = 0.f, a_eval = alpha;
+  for (int ls = 0; ls < prm_.max_line_iters; ++ls) {
+    if (ls > 0) {
+      axpy_to(ctx_->stream, n_, x_, alpha, p_.get(), xt_);
+      eval(xt_, gt_, p_.get());
+      read_status();
+    }
+    ++trials;
+    a_eval = alpha;
+    lnew = float(hs_[SC_LOSS]);
+    if (lnew <= lossf_ + c1 * alpha * gdp) {
+      ok = true;
+      break;
+    }
+    const float den = 2.0f * (lnew - lossf_ - gdp * alpha);
+    bool fb = true;
+    if (std::fabs(den) > 1e-20f) {
+      const float na = -(gdp * alpha * alpha) / den;
+      if (na >= 0.1f * alpha && na <= 0.9f * alpha) {
+        alpha = na;
+        fb = false;
+      }
+    }
+    if (fb) alpha *= rho;
+  }
+  accept_roles();
+  pending_reset_ = !ok; // lbfgs.cuh:147
+  lossf_ = lnew;
+  loss_ = hs_[SC_LOSS];
+  gg_ = hs_[SC_TGG];
+  record(rec, double(lnew), double(float(std::sqrt(gg_))), double(a_eval), trials, -1);
+}
+
 int LbfgsSolver::iterate_armijo(int iters, lbf_record *rec) {
   int k = 0;
-  const float c1 = float(prm_.c1), rho = float(prm_.rho);
   for (; k < iters; ++k) {
-    const float gnorm = float(std::sqrt(gg_));
-    if (gnorm < float(prm_.tol)) {
+    if (entry_converged()) {
       converged_ = true;
       break;
     }
-    GramArgs ga;
-    ga.policy = POL_CUDA;
-    ga.has_g = 1;
-    ga.ga = g_;
-    ga.reset = pending_reset_ ? 1 : 0;
-    if (pending_pair_) {
-      ga.has_pair = 1;
-      ga.sa = x_;
-      ga.sb = xp_;
-      ga.ya = g_;
-      ga.yb = gp_;
-    }
-    hist_.update(ga, 1, iter_, -1.0);
-    float alpha = (iter_ == 0) ? std::min(1.0f, 1.0f / gnorm) : 1.0f;
-    hist_.combine(g_, p_.get(), x_, xt_, nullptr, false, double(alpha));
-    eval(xt_, gt_, p_.get());
+    const bool had_pair = pending_pair_;
+    const float alpha = begin_iteration();
     read_status();
-    if (pending_pair_ && rec && rec->accepted && rec_idx_ > 0 && rec_idx_ - 1 < rec->cap)
-      rec->accepted[rec_idx_ - 1] = int(hs_[SC_ACCEPT]);
-    const float gdp = float(hs_[SC_GTP]);
-    bool ok = false;
-    int trials = 0;
-    float lnew = 0.f, a_eval = alpha;
-    for (int ls = 0; ls < prm_.max_line_iters; ++ls) {
-      if (ls > 0) {
-        axpy_to(ctx_->stream, n_, x_, alpha, p_.get(), xt_);
-        eval(xt_, gt_, p_.get());
-        read_status();
-      }
-      ++trials;
-      a_eval = alpha;
-      lnew = float(hs_[SC_LOSS]);
-      if (lnew <= lossf_ + c1 * alpha * gdp) {
-        ok = true;
-        break;
-      }
-      const float den = 2.0f * (lnew - lossf_ - gdp * alpha);
-      bool fb = true;
-      if (std::fabs(den) > 1e-20f) {
-        const float na = -(gdp * alpha * alpha) / den;
-        if (na >= 0.1f * alpha && na <= 0.9f * alpha) {
-          alpha = na;
-          fb = false;
-        }
-      }
-      if (fb) alpha *= rho;
-    }
-    pending_reset_ = !ok; // lbfgs.cuh:147
-    std::swap(xp_, x_);
-    std::swap(x_, xt_);
-    std::swap(gp_, g_);
-    std::swap(g_, gt_);
-    lossf_ = lnew;
-    loss_ = hs_[SC_LOSS];
-    gg_ = hs_[SC_TGG];
-    pending_pair_ = prm_.m > 0;
-    record(rec, double(lnew), double(float(std::sqrt(gg_))), double(a_eval), trials, -1);
-    ++iter_;
+    if (had_pair) mark_prev_accepted(rec, hs_[SC_ACCEPT]);
+    finish_armijo(alpha, rec);
   }
   return k;
+}
+
+// Waits for everything queued, clears the abort flag and forgets the aborted iterations.
+void LbfgsSolver::drain(std::deque<Flight> &q, size_t prof_end) {
+  LBF_HIP(hipStreamSynchronize(ctx_->stream));
+  LBF_HIP(hipMemsetAsync(abort_.get(), 0, sizeof(int), ctx_->stream));
+  obj_->discard_evals((long long)q.size());
+  if (ctx_->prof.on && ctx_->prof.recs.size() > prof_end) ctx_->prof.recs.resize(prof_end);
+  q.clear();
+}
+
+// Speculative pipeline. Almost every accepted step is the first trial (alpha = 1), so the host
+// enqueues up to depth_ iterations assuming it will be, and a one-thread ls_ctl kernel after each first
+// trial decides on the device with the host's own test. A rejected (or converged) trial raises the
+// abort flag: every launch queued behind it exits at entry, the host waits, restores the buffer roles
+// of that iteration (the history, Gram state and status block are exactly as that trial left them)
+// and finishes it host-driven, then speculates again. Results are identical to the host-driven loop.
+int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
+  const bool armijo = prm_.line_search == LBF_LS_ARMIJO;
+  std::deque<Flight> q;
+  int done = 0, issued = 0;
+  bool host_fold = true;
+  ctx_->abort = abort_.get();
+  struct Clear {
+    Ctx *c;
+    ~Clear() { c->abort = nullptr; }
+  } clear{ctx_};
+  while (done < iters) {
+    if (q.empty() && entry_converged()) {
+      converged_ = true;
+      break;
+    }
+    while (issued < iters && int(q.size()) < depth_) {
+      Flight f;
+      f.roles = roles();
+      f.alpha = begin_iteration();
+      f.seq = seq_++;
+      LsCtlArgs a;
+      a.scal = hist_.scal();
+      a.abort = abort_.get();
+      a.rec = spec_rec_ + f.seq % kSpecRing;
+      a.seq = f.seq;
+      a.armijo = armijo ? 1 : 0;
+      a.first = iter_ == 0 ? 1 : 0;
+      a.host_fold = host_fold ? 1 : 0;
+      a.fold = loss_;
+      a.foldf = lossf_;
+      a.c1 = prm_.c1;
+      a.c2 = prm_.c2;
+      a.tol = prm_.tol;
+      a.alphaf = f.alpha;
+      ls_ctl(ctx_->stream, a);
+      LBF_HIP(hipEventRecord(spec_ev_[f.seq % kSpecRing], ctx_->stream));
+      f.prof_end = ctx_->prof.recs.size();
+      q.push_back(f);
+      host_fold = false;
+      accept_roles(); // assume the first trial is taken
+      pending_reset_ = false;
+      ++issued;
+    }
+    const Flight f = q.front();
+    q.pop_front();
+    LBF_HIP(hipEventSynchronize(spec_ev_[f.seq % kSpecRing]));
+    SpecRecord r;
+    std::memcpy(&r, spec_rec_ + f.seq % kSpecRing, sizeof(r)); // complete: the event has fired
+    if (r.seq != f.seq) throw Error(2, "speculative line search: record out of sequence");
+    if (f.roles.pair) mark_prev_accepted(rec, r.accept_prev);
+    if (r.status == SPEC_REJECT) {
+      drain(q, f.prof_end);
+      restore(f.roles);
+      read_status();
+      if (armijo)
+        finish_armijo(f.alpha, rec);
+      else
+        finish_wolfe(rec);
+      ++done;
+      issued = done;
+      host_fold = true;
+      continue;
+    }
+    loss_ = r.loss;
+    gg_ = r.tgg;
+    if (armijo) {
+      lossf_ = float(r.loss);
+      record(rec, double(lossf_), double(float(std::sqrt(gg_))), double(f.alpha), 1, -1);
+    } else {
+      record(rec, loss_, std::sqrt(gg_), f.roles.iter == 0 ? r.alpha0 : 1.0, f.roles.iter == 0 ? 0 : 1, -1);
+    }
+    ++done;
+    if (r.status == SPEC_CONVERGED) {
+      // the iterations queued behind were aborted: return to the roles right after this step
+      if (!q.empty()) restore(q.front().roles);
+      drain(q, f.prof_end);
+      issued = done;
+      host_fold = true;
+    }
+  }
+  return done;
 }
 
 void LbfgsSolver::info(lbf_solve_info *out) const {

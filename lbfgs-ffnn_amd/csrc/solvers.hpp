@@ -5,6 +5,7 @@
 #include "runtime.hpp"
 
 #include <chrono>
+#include <deque>
 #include <random>
 
 namespace lbf {
@@ -18,6 +19,9 @@ struct Objective {
   virtual long long n() const = 0;
   virtual void eval(const float *x, float *g, const float *pdir, double *scal) = 0;
   virtual long long evals() const = 0;
+  // Asynchronous objectives can be enqueued ahead of the host's line-search decisions.
+  virtual bool async() const { return false; }
+  virtual void discard_evals(long long) {}
 };
 
 // The MLP's fused loss+grad over the rank's shard (mean over n_global samples).
@@ -33,6 +37,8 @@ struct MlpObjective : Objective {
     net->loss_grad(x, g, X, Y, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal);
   }
   long long evals() const override { return net->evals(); }
+  bool async() const override { return true; }
+  void discard_evals(long long k) override { net->discard_evals(k); }
 };
 
 // A user callback with the reference's LossGradFun contract: returns the loss, writes the gradient
@@ -61,6 +67,7 @@ struct CallbackObjective : Objective {
 class LbfgsSolver {
 public:
   LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_params);
+  ~LbfgsSolver();
   // Runs up to `iters` iterations. Returns the number run (fewer on convergence).
   int iterate(int iters, lbf_record *rec);
   void info(lbf_solve_info *out) const;
@@ -72,7 +79,40 @@ private:
   void writeback();
   int iterate_wolfe(int iters, lbf_record *rec);
   int iterate_armijo(int iters, lbf_record *rec);
+  int iterate_spec(int iters, lbf_record *rec);
+  bool entry_converged() const;
+  // First trial of an iteration (history update, direction, x + alpha p, evaluation), enqueued only.
+  // Returns the Armijo trial step (Wolfe takes alpha0 from the device status block).
+  float begin_iteration();
+  // Rest of the iteration once hs_ holds the first trial's status: further trials, role rotation,
+  // record.
+  void finish_wolfe(lbf_record *rec);
+  void finish_armijo(float alpha, lbf_record *rec);
+  void accept_roles();
+  void mark_prev_accepted(lbf_record *rec, double flag);
   void record(lbf_record *rec, double loss, double gnorm, double alpha, int trials, int accepted);
+
+  // speculative pipeline state
+  struct Roles {
+    float *x, *xp, *xt, *g, *gp, *gt;
+    int iter;
+    bool pair, reset;
+  };
+  Roles roles() const { return {x_, xp_, xt_, g_, gp_, gt_, iter_, pending_pair_, pending_reset_}; }
+  void restore(const Roles &r);
+  struct Flight {
+    Roles roles;
+    float alpha;
+    int seq;
+    size_t prof_end;
+  };
+  void drain(std::deque<Flight> &q, size_t prof_end);
+  static constexpr int kSpecRing = 32;
+  int depth_ = 0;
+  int seq_ = 0;
+  DevBuf<int> abort_;
+  SpecRecord *spec_rec_ = nullptr;
+  std::vector<hipEvent_t> spec_ev_;
 
   Objective *obj_;
   Ctx *ctx_;

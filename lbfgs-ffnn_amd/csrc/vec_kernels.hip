@@ -118,7 +118,8 @@ void loss_diff(hipStream_t s, const float *Aout, long long lda, const float *Y, 
 // a fixed order. CW = 64 for few splits (coalesced 256-B rows), 16 when splits are many (more
 // parallelism per column for the tall-and-thin slabs of small layers).
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float *slab, int splits, long long stride,
-                                                           long long count, int cw, float *grad) {
+                                                           long long count, int cw, float *grad, const int *abort) {
+  if (abort && *abort) return;
   __shared__ double part[256];
   const int t = threadIdx.x;
   const int nst = 256 / cw;
@@ -136,10 +137,11 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float *slab, in
   }
 }
 
-void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride, long long count, float *grad) {
+void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride, long long count, float *grad,
+                  const int *abort) {
   const int cw = splits > 64 ? 16 : 64;
   hipLaunchKernelGGL(reduce_slabs_kernel, dim3(unsigned(cdiv(count, cw))), dim3(256), 0, s, slab, splits, stride,
-                     count, cw, grad);
+                     count, cw, grad, abort);
   LBF_KERNEL_CHECK();
 }
 
@@ -152,7 +154,8 @@ int dots_partials_wg(long long n) {
 }
 
 __global__ __launch_bounds__(256) void finalize_kernel(long long n, float *g, const float *w, double lambda,
-                                                       const float *p, double *partials) {
+                                                       const float *p, double *partials, const int *abort) {
+  if (abort && *abort) return;
   __shared__ double scratch[48];
   double acc[3] = {0.0, 0.0, 0.0};
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -177,8 +180,9 @@ __global__ __launch_bounds__(256) void finalize_kernel(long long n, float *g, co
 }
 
 void finalize_grad_dots(hipStream_t s, long long n, float *g, const float *w, double lambda, const float *p,
-                        double *partials) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(dots_partials_wg(n)), dim3(256), 0, s, n, g, w, lambda, p, partials);
+                        double *partials, const int *abort) {
+  hipLaunchKernelGGL(finalize_kernel, dim3(dots_partials_wg(n)), dim3(256), 0, s, n, g, w, lambda, p, partials,
+                     abort);
   LBF_KERNEL_CHECK();
 }
 
@@ -314,6 +318,7 @@ __device__ __forceinline__ int hist_write_slot(const int *ist, int m, int policy
 }
 
 __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, long long chunk, double *partials) {
+  if (a.h.abort && *a.h.abort) return;
   extern __shared__ __attribute__((aligned(16))) float sh[];
   __shared__ double scratch[6 * 16];
   float *ls = sh, *ly = sh + chunk, *lg = sh + 2 * chunk;
@@ -432,6 +437,7 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
 static constexpr int COEF_MAXK = 128;
 
 __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
+  if (a.h.abort && *a.h.abort) return;
   extern __shared__ double sy[]; // [k][k] live s_i . y_j after the push (logical order)
   __shared__ double dots[6 * COEF_MAXK + 6];
   __shared__ double gS_l[COEF_MAXK], gY_l[COEF_MAXK], rho_l[COEF_MAXK], alpha_l[COEF_MAXK], c_l[COEF_MAXK];
@@ -652,6 +658,7 @@ void hist_coef(hipStream_t s, const CoefArgs &a) {
 // fused with the trial point x_out = x_in + alpha*dir (and an optional second copy).
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
+  if (a.h.abort && *a.h.abort) return;
   __shared__ double cs[COEF_MAXK], cy[COEF_MAXK];
   __shared__ int L[COEF_MAXK];
   const HistView &h = a.h;
@@ -727,7 +734,8 @@ void hist_reset(hipStream_t s, const HistView &h) {
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void eval_tail_kernel(const double *dots_part, int nd, const double *sse_part,
                                                         int nsse, const float *hilo, double inv_scale,
-                                                        double lambda, double *scal) {
+                                                        double lambda, double *scal, const int *abort) {
+  if (abort && *abort) return;
   __shared__ double v[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double s = 0.0;
@@ -752,15 +760,17 @@ __global__ __launch_bounds__(256) void eval_tail_kernel(const double *dots_part,
 }
 
 void eval_tail(hipStream_t s, const double *dots_part, int nd, const double *sse_part, int nsse, const float *hilo,
-               double inv_scale, double lambda, double *scal) {
+               double inv_scale, double lambda, double *scal, const int *abort) {
   hipLaunchKernelGGL(eval_tail_kernel, dim3(1), dim3(256), 0, s, dots_part, nd, sse_part, nsse, hilo, inv_scale,
-                     lambda, scal);
+                     lambda, scal, abort);
   LBF_KERNEL_CHECK();
 }
 
 // Data-parallel: reduce this rank's SSE partials and store them as an fp32 (hi, lo) pair behind the
 // gradient, so one all-reduce of [grad | hi | lo] carries the loss with ~fp64 accuracy.
-__global__ __launch_bounds__(64) void sse_pack_kernel(const double *sse_part, int nsse, float *hilo) {
+__global__ __launch_bounds__(64) void sse_pack_kernel(const double *sse_part, int nsse, float *hilo,
+                                                      const int *abort) {
+  if (abort && *abort) return;
   double s = 0.0;
   for (int r = threadIdx.x; r < nsse; r += 64) s += sse_part[r];
   s = wave_sum(s);
@@ -771,8 +781,46 @@ __global__ __launch_bounds__(64) void sse_pack_kernel(const double *sse_part, in
   }
 }
 
-void sse_pack(hipStream_t s, const double *sse_part, int nsse, float *hilo) {
-  hipLaunchKernelGGL(sse_pack_kernel, dim3(1), dim3(64), 0, s, sse_part, nsse, hilo);
+void sse_pack(hipStream_t s, const double *sse_part, int nsse, float *hilo, const int *abort) {
+  hipLaunchKernelGGL(sse_pack_kernel, dim3(1), dim3(64), 0, s, sse_part, nsse, hilo, abort);
+  LBF_KERNEL_CHECK();
+}
+
+// Acceptance test of the first line-search trial, evaluated exactly as the host would (no FMA
+// contraction, same precision): Wolfe in fp64 (full_batch_minimizer.hpp:136-152), Armijo in fp32
+// (lbfgs.cuh:159-163). Convergence uses the next iteration's entry test (lbfgs.hpp:42, lbfgs.cuh:143).
+__global__ __launch_bounds__(64) void ls_ctl_kernel(const LsCtlArgs a) {
+  if (threadIdx.x != 0 || *a.abort) return;
+  double *sc = a.scal;
+  const double fn = sc[SC_LOSS], gfo = sc[SC_GTP], gnp = sc[SC_TGP], tgg = sc[SC_TGG];
+  bool ok, conv;
+  if (!a.armijo) {
+    const double fold = a.host_fold ? a.fold : sc[SC_FOLD];
+    ok = a.first || (!(fn > __dadd_rn(fold, __dmul_rn(__dmul_rn(a.c1, 1.0), gfo))) && !(gnp < __dmul_rn(a.c2, gfo)));
+    conv = sqrt(tgg) < a.tol;
+    if (ok) sc[SC_FOLD] = fn;
+  } else {
+    const float foldf = a.host_fold ? a.foldf : float(sc[SC_FOLDF]);
+    const float lnew = float(fn), gdp = float(gfo);
+    ok = lnew <= __fadd_rn(foldf, __fmul_rn(__fmul_rn(float(a.c1), a.alphaf), gdp));
+    conv = float(sqrt(tgg)) < float(a.tol);
+    if (ok) sc[SC_FOLDF] = double(lnew);
+  }
+  const int status = !ok ? SPEC_REJECT : (conv ? SPEC_CONVERGED : SPEC_ACCEPT);
+  if (status != SPEC_ACCEPT) *a.abort = 1;
+  SpecRecord *r = a.rec;
+  r->loss = fn;
+  r->tgg = tgg;
+  r->alpha0 = sc[SC_ALPHA0];
+  r->accept_prev = sc[SC_ACCEPT];
+  r->status = status;
+  __threadfence_system();
+  r->seq = a.seq;
+  __threadfence_system();
+}
+
+void ls_ctl(hipStream_t s, const LsCtlArgs &a) {
+  hipLaunchKernelGGL(ls_ctl_kernel, dim3(1), dim3(64), 0, s, a);
   LBF_KERNEL_CHECK();
 }
 

@@ -80,6 +80,14 @@ class Context:
     def prof_enable(self, on: bool = True):
         check(lib().lbf_prof_enable(self.h, int(on)), "lbf_prof_enable")
 
+    def prof_select(self, section=None):
+        """Time only `section` ("kind[layer]"), or every section when None."""
+        sid = -1
+        if section is not None:
+            kind, layer = section.split("[")
+            sid = self.PROF_KINDS.index(kind) * 16 + int(layer.rstrip("]"))
+        check(lib().lbf_prof_select(self.h, sid), "lbf_prof_select")
+
     def prof_read(self):
         """{section name: (total ms, launches)}; section = kind[layer]."""
         n = C.c_int(0)

@@ -243,3 +243,40 @@ def test_lbfgs_full_size_decreases(ctx, pkg):
     assert len(hist["loss"]) == 10
     assert np.all(np.diff(hist["loss"]) <= 0)
     assert hist["loss"][-1] < 0.5 * hist["loss"][0]
+
+
+def _spec_run(pkg, ctx, monkeypatch, depth, line_search, tol, iters, chunks=1):
+    monkeypatch.setenv("LBF_SPEC_DEPTH", str(depth))
+    dims, acts = [784, 32, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(256)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(7, "cuda" if line_search == "armijo" else "cpu")
+    run = pkg.LbfgsRun(net, P, dev(Xh), dev(Yh), line_search=line_search, m=5, max_iters=iters, tol=tol)
+    for c in range(chunks):
+        run.iterate(iters // chunks)
+    info = run.info
+    h = run.hist.as_dict()
+    run.close()
+    return h, (info.iterations, info.n_evals, info.final_loss, info.final_grad_norm), host(P)
+
+
+@pytest.mark.parametrize("line_search", ["wolfe", "armijo"])
+def test_speculative_line_search_is_exact(ctx, pkg, monkeypatch, line_search):
+    """The speculative pipeline (ls_ctl + abort flag, solvers.cpp iterate_spec) reproduces the host-driven
+    loop bit for bit: records, evaluation count, final parameters — across rejections of the first trial,
+    convergence inside the speculation window, and solves split into several iterate() calls."""
+    ref, ref_info, ref_P = _spec_run(pkg, ctx, monkeypatch, 0, line_search, 0.0, 40)
+    assert np.any(ref["ls_trials"][1:] > 1), "problem must exercise rejected first trials"
+    for depth, chunks in [(1, 1), (3, 1), (8, 1), (3, 4)]:
+        h, info, P = _spec_run(pkg, ctx, monkeypatch, depth, line_search, 0.0, 40, chunks)
+        for k in ("loss", "grad_norm", "alpha", "ls_trials", "accepted"):
+            assert np.array_equal(h[k], ref[k]), (depth, chunks, k)
+        assert info == ref_info, (depth, info, ref_info)
+        assert np.array_equal(P, ref_P)
+    # convergence in the middle of a speculation window
+    tol = float(ref["grad_norm"][12]) * (1 + 1e-6)
+    ref_c, ref_ci, ref_cP = _spec_run(pkg, ctx, monkeypatch, 0, line_search, tol, 40)
+    assert len(ref_c["loss"]) < 40
+    h, info, P = _spec_run(pkg, ctx, monkeypatch, 4, line_search, tol, 40)
+    assert info == ref_ci
+    assert np.array_equal(h["loss"], ref_c["loss"]) and np.array_equal(P, ref_cP)
