@@ -30,6 +30,7 @@ METRIC = "L-BFGS iters/sec + grad-eval GFLOP/s, 784-128-10 MLP full-batch"
 REF_GPU_ITERS_PER_S = 139.1      # L-BFGS m=10, 784-128-10, N=60000 (sm_86, fp32 cuBLAS)
 FP32_MFMA_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix peak (dense)
 HBM_PEAK_GBS = 8000.0
+PROF_EVERY = 8                   # time every 8th launch of the dominant kernel inside the timed region
 
 
 def parse():
@@ -112,6 +113,7 @@ def main():
     evals0 = run.info.n_evals
     it0 = run.hist.size
     ctx.prof_select(dominant)
+    ctx.prof_sample(PROF_EVERY)
     ctx.prof_enable(True)
 
     def barrier():
@@ -134,6 +136,7 @@ def main():
     prof = ctx.prof_read()
     ctx.prof_enable(False)
     ctx.prof_select(None)
+    ctx.prof_sample(1)
     evals = run.info.n_evals - evals0
     iters_done = run.hist.size - it0
 
@@ -155,6 +158,7 @@ def main():
         roof["frac"] = round(roof["achieved"] / roof["peak"], 4) if roof["achieved"] else None
         roof["kernel"] = name
         roof["avg_launch_us"] = round(avg_s * 1e6, 2)
+        roof["timed_launches"] = cnt
         roof["traffic"] = None
         if os.path.exists(a.pmc_json):
             try:

@@ -172,6 +172,9 @@ int lbf_prof_enable(lbf_ctx *ctx, int on);
 /* Restrict timing to one section id (-1: all). Two events per launch of that section only, so the
  * timed region of a benchmark is not serialised by event packets around every kernel. */
 int lbf_prof_select(lbf_ctx *ctx, int section_id);
+/* Time only every `every`-th launch of the selected sections (1 = all): live timing inside a timed
+ * region at 1/every of the event cost (an event record idles the GPU for ~5 us). */
+int lbf_prof_sample(lbf_ctx *ctx, int every);
 int lbf_prof_read(lbf_ctx *ctx, int cap, int *ids, double *ms, long long *counts, int *n_out);
 
 /* ---- device memory, so C/C++ consumers need no HIP headers (the reference's DeviceBuffer,

@@ -14,7 +14,7 @@ from typing import Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "build", "liblbfgs_amd.so")
+LIB_PATH = os.environ.get("LBF_LIB_PATH") or os.path.join(_HERE, "build", "liblbfgs_amd.so")
 
 LS_WOLFE, LS_ARMIJO = 0, 1
 INIT_CPU, INIT_CUDA = 0, 1
@@ -101,6 +101,7 @@ def lib():
                                        C.POINTER(SolveInfo)]),
         "lbf_prof_enable": (C.c_int, [_vp, C.c_int]),
         "lbf_prof_select": (C.c_int, [_vp, C.c_int]),
+        "lbf_prof_sample": (C.c_int, [_vp, C.c_int]),
         "lbf_prof_read": (C.c_int, [_vp, C.c_int, _ip, _dp, C.POINTER(C.c_longlong), _ip]),
         "lbf_synth_mnist": (C.c_int, [C.c_longlong, C.c_int, C.c_int, C.c_uint, _vp, _vp]),
         "lbf_sample_indices": (C.c_int, [C.c_longlong, C.c_int, C.c_uint, C.c_int, _vp]),
@@ -117,7 +118,7 @@ EXPORTS = ("lbf_last_error lbf_version lbf_ctx_create lbf_ctx_destroy lbf_ctx_sy
            "lbf_comm_unique_id lbf_comm_init lbf_comm_rank lbf_allreduce_sum lbf_mlp_create lbf_mlp_destroy "
            "lbf_mlp_param_count lbf_mlp_init_params lbf_init_params_host lbf_mlp_forward lbf_mlp_loss_grad lbf_two_loop lbf_dot "
            "lbf_nrm2 lbf_axpy lbf_scal lbf_lbfgs_default_params lbf_slbfgs_default_params lbf_lbfgs_solve "
-           "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_prof_enable lbf_prof_select lbf_prof_read lbf_synth_mnist "
+           "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_prof_enable lbf_prof_select lbf_prof_sample lbf_prof_read lbf_synth_mnist "
            "lbf_sample_indices").split()
 
 

@@ -455,6 +455,14 @@ int lbf_prof_select(lbf_ctx *ctx, int section_id) {
   });
 }
 
+int lbf_prof_sample(lbf_ctx *ctx, int every) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && every >= 1, "ctx / every >= 1");
+    ctx->c.prof.every = every;
+    ctx->c.prof.seen = 0;
+  });
+}
+
 int lbf_prof_read(lbf_ctx *ctx, int cap, int *ids, double *ms, long long *counts, int *n_out) {
   return guard([&] {
     LBF_REQUIRE(ctx && n_out, "null argument");

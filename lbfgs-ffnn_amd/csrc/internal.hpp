@@ -87,4 +87,18 @@ private:
 
 inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
 
+// Phase timestamps for kernel tuning (debug build only: make ktrace). KT(slot) stores the 100 MHz
+// wall clock from thread 0 of block 0; lbf_dbg_ktrace() copies the slots to the host.
+#ifdef LBF_KTRACE
+extern __device__ unsigned long long lbf_kt_buf[256];
+#define KT(slot)                                                                                        \
+  do {                                                                                                  \
+    if (blockIdx.x == 0 && threadIdx.x == 0) lbf_kt_buf[slot] = wall_clock64();                         \
+  } while (0)
+#else
+#define KT(slot)                                                                                        \
+  do {                                                                                                  \
+  } while (0)
+#endif
+
 } // namespace lbf

@@ -76,6 +76,46 @@ void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride
 
 // g += lambda*w (if lambda != 0); per-WG partials of (g.g, g.p, w.w) -> partials[wg*3 + {0,1,2}]
 int dots_partials_wg(long long n);
+// Two launches for the whole evaluation tail: every layer's [dW ; db] segment is reduced from its
+// split-K / head partial slabs (fixed order, fp64), or taken as written (splits == 0). Column groups
+// with many slabs are split over several blocks by split range and combined in range order by the
+// second launch (one block). With `dots` (single rank) they also apply g += lambda*w and write
+// per-group (g.g, g.p, w.w) partials, which the second launch reduces with the SSE partials into the
+// status block like eval_tail. No grid-wide ticket: an agent-scope fence right after the GEMM's slab
+// writes costs tens of microseconds (dirty-L2 write-back on every XCD).
+constexpr int RA_MAXSEG = 17;
+struct RedSeg {
+  const float *slab = nullptr;
+  long long stride = 0, count = 0, goff = 0;
+  int splits = 0;
+  int parts = 1; // blocks per 64-column group, each over a contiguous range of splits
+  int wg0 = 0;   // first block of the segment (reduce launch)
+  int cg0 = 0;   // first column group of the segment (global numbering)
+  int fin0 = -1; // parts > 1: first block of the segment in the finishing launch
+};
+struct RedAllArgs {
+  RedSeg seg[RA_MAXSEG];
+  int nseg = 0, nwg = 0;
+  float *G = nullptr;
+  const float *w = nullptr, *p = nullptr;
+  double lambda = 0.0;
+  int dots = 0;
+  double *partials = nullptr;   // [ncg][3] dot partials
+  double *colpart = nullptr;    // [ncg][RA_MAXPART][64] split-range partials
+  int ncg = 0;
+  int nfin = 0;                 // column groups with parts > 1
+  const double *sse_part = nullptr;
+  int nsse = 0;
+  double inv_scale = 1.0;
+  double *scal = nullptr;
+  const int *abort = nullptr;
+};
+constexpr int RA_COLS = 64;
+constexpr int RA_MAXPART = 32;
+constexpr int RA_SPLITS_PER_PART = 64; // 4 stripes x 16 loads per thread
+constexpr int RA_MAXFIN = 128;         // column groups the one-block finishing launch combines
+void reduce_all(hipStream_t s, const RedAllArgs &a);
+
 void finalize_grad_dots(hipStream_t s, long long n, float *g, const float *w, double lambda, const float *p,
                         double *partials, const int *abort = nullptr);
 // generic: per-WG partials of x.y -> partials[wg]
@@ -198,6 +238,7 @@ struct CoefArgs {
   int has_pair = 0, has_g = 0, reset = 0, policy = POL_CPU;
   int want_dir = 1;
   int iter = 1;
+  int stage = 0; // LDS doubles for staging partial rows (set by hist_coef)
   double dsign = -1.0;
 };
 void hist_coef(hipStream_t s, const CoefArgs &a);

@@ -92,7 +92,8 @@ void Mlp::plan(long long B) {
     splits = std::max(1LL, cdiv(B, kc));
     L.splits = int(splits);
     L.k_chunk = int(kc);
-    if (splits > 1) slab = std::max(slab, size_t(splits) * size_t(M) * L.out);
+    L.slab_off = slab;
+    if (splits > 1) slab += size_t(splits) * size_t(M) * L.out; // every layer keeps its own slabs until reduce_all
   }
   slab_.ensure(slab);
   planned_ = B;
@@ -118,7 +119,10 @@ void Mlp::ensure(long long B) {
     head_slab_.ensure(hw * size_t(Lo.in + 1) * Lo.out);
   }
   loss_part_.ensure(nloss);
-  dots_part_.ensure(size_t(dots_partials_wg(nparams_)) * 3);
+  long long ncg = 0;
+  for (auto &L : layers_) ncg += cdiv((long long)(L.in + 1) * L.out, RA_COLS);
+  dots_part_.ensure(size_t(std::max<long long>(dots_partials_wg(nparams_), ncg)) * 3);
+  colpart_.ensure(size_t(ncg) * RA_MAXPART * RA_COLS);
   sse_.ensure(1);
 }
 
@@ -164,14 +168,11 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
   if (fused) {
     // last layer: forward + loss + dZ + delta + [dW ; db] partials in one kernel (head.hip)
     nloss = head_nwg(B, Lo.in);
-    const long long seg = (long long)(Lo.in + 1) * Lo.out;
     {
       ProfScope ps(ctx_, PK_LOSS);
       head_fused(s, A_[nl - 2].get(), Lo.in, P + Lo.off, Lo.out, Y, idx, B, Lo.act, layers_[nl - 2].act, inv_scale,
                  D_[nl - 2].get(), head_slab_.get(), loss_part_.get(), ctx_->abort);
     }
-    ProfScope ps(ctx_, PK_SLAB, nl - 1);
-    reduce_slabs(s, head_slab_.get(), nloss, seg, seg, G + Lo.off, ctx_->abort);
     lstart = nl - 2;
   } else {
     nloss = loss_partials_wg(std::max(1LL, B), Lo.out);
@@ -204,14 +205,10 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     d.abort = ctx_->abort;
     const long long seg = (long long)(L.in + 1) * L.out;
     if (L.splits > 1) {
-      d.C = slab_.get();
+      d.C = slab_.get() + L.slab_off;
       d.slab_stride = seg;
-      {
-        ProfScope ps(ctx_, PK_DW, l);
-        gemm(s, d);
-      }
-      ProfScope ps(ctx_, PK_SLAB, l);
-      reduce_slabs(s, slab_.get(), L.splits, seg, seg, G + L.off, ctx_->abort);
+      ProfScope ps(ctx_, PK_DW, l);
+      gemm(s, d);
     } else {
       d.C = G + L.off;
       ProfScope ps(ctx_, PK_DW, l);
@@ -240,6 +237,55 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
       ProfScope ps(ctx_, PK_DX, l);
       gemm(s, x);
     }
+  }
+  // every layer's partial slabs -> gradient (+ dots and the status block on a single rank)
+  RedAllArgs ra;
+  ra.G = G;
+  ra.w = P;
+  ra.p = pdir;
+  ra.lambda = lambda;
+  ra.dots = ctx_->nranks > 1 ? 0 : 1;
+  ra.partials = dots_part_.get();
+  ra.colpart = colpart_.get();
+  ra.sse_part = loss_part_.get();
+  ra.nsse = nloss;
+  ra.inv_scale = inv_scale;
+  ra.scal = scal;
+  ra.abort = ctx_->abort;
+  for (int l = 0; l < nl; ++l) {
+    const Layer &L = layers_[l];
+    RedSeg &g = ra.seg[l];
+    g.count = (long long)(L.in + 1) * L.out;
+    g.goff = (long long)L.off;
+    g.stride = g.count;
+    if (fused && l == nl - 1) {
+      g.slab = head_slab_.get();
+      g.splits = nloss;
+    } else if (L.splits > 1) {
+      g.slab = slab_.get() + L.slab_off;
+      g.splits = L.splits;
+    }
+    const int ncols = int(cdiv(g.count, RA_COLS));
+    // many slabs over few columns (the head's): split ranges over blocks, finished by one block
+    if (g.splits > 2 * RA_SPLITS_PER_PART && ra.nfin + ncols <= RA_MAXFIN)
+      g.parts = int(std::min<long long>(RA_MAXPART, cdiv(g.splits, RA_SPLITS_PER_PART)));
+    g.wg0 = ra.nwg;
+    g.cg0 = ra.ncg;
+    if (g.parts > 1) {
+      g.fin0 = ra.nfin;
+      ra.nfin += ncols;
+    }
+    ra.nwg += ncols * g.parts;
+    ra.ncg += ncols;
+  }
+  ra.nseg = nl;
+  {
+    ProfScope ps(ctx_, PK_SLAB, 0);
+    reduce_all(s, ra);
+  }
+  if (ra.dots) {
+    ++evals_;
+    return;
   }
   const float *hilo = nullptr;
   if (ctx_->nranks > 1) {

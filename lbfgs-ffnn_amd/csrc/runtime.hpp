@@ -18,7 +18,12 @@ enum ProfKind : int { PK_FWD = 0, PK_DW = 1, PK_DX = 2, PK_LOSS = 3, PK_SLAB = 4
 struct Profiler {
   bool on = false;
   int only = -1; // section filter (-1: all)
-  bool want(int id) const { return on && (only < 0 || only == id); }
+  int every = 1;  // sample every k-th launch of a wanted section
+  long long seen = 0;
+  bool want(int id) {
+    if (!on || (only >= 0 && only != id)) return false;
+    return every <= 1 || (seen++ % every) == 0;
+  }
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   struct Rec { int id; size_t a, b; };
@@ -51,6 +56,7 @@ struct Layer {
   size_t off;      // flat offset of the [(in+1) x out] segment
   int splits = 1;  // split-K factor of the dW GEMM at the planned batch
   int k_chunk = 0;
+  size_t slab_off = 0; // this layer's partial slabs inside the shared slab buffer
 };
 
 // RAII section: records an event pair around the enclosed launches when profiling is on.
@@ -96,7 +102,7 @@ private:
   std::vector<DevBuf<float>> A_, D_;
   DevBuf<float> slab_, head_slab_;
   bool use_head_ = true; // fused output layer when the shape allows (LBF_NO_HEAD=1 disables)
-  DevBuf<double> loss_part_, dots_part_, sse_;
+  DevBuf<double> loss_part_, dots_part_, sse_, colpart_;
   long long evals_ = 0;
   void plan(long long B);
 };

@@ -73,8 +73,6 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
     LBF_HIP(hipHostMalloc(reinterpret_cast<void **>(&spec_rec_), kSpecRing * sizeof(SpecRecord),
                           hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(spec_rec_, 0xff, kSpecRing * sizeof(SpecRecord));
-    spec_ev_.resize(kSpecRing);
-    for (auto &e : spec_ev_) LBF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   LBF_HIP(hipMemcpyAsync(x_, d_params, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, ctx_->stream));
   // initial evaluation (lbfgs.hpp:44 / lbfgs.cuh:147)
@@ -87,7 +85,6 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
 }
 
 LbfgsSolver::~LbfgsSolver() {
-  for (auto e : spec_ev_) (void)hipEventDestroy(e);
   if (spec_rec_) (void)hipHostFree(spec_rec_);
 }
 
@@ -311,6 +308,33 @@ int LbfgsSolver::iterate_armijo(int iters, lbf_record *rec) {
   return k;
 }
 
+// Spins on the host-mapped record of speculative iteration `seq` (no event: an event record costs
+// ~5 us of idle GPU per iteration). Every ~1 ms of spinning, the stream is queried so a failed launch
+// or an already-drained queue surfaces instead of spinning forever.
+void LbfgsSolver::wait_record(int seq, SpecRecord *out) {
+  volatile SpecRecord *r = spec_rec_ + seq % kSpecRing;
+  auto t0 = std::chrono::steady_clock::now();
+  for (long long spin = 0;; ++spin) {
+    if (__atomic_load_n(&spec_rec_[seq % kSpecRing].seq, __ATOMIC_ACQUIRE) == seq) break;
+    if ((spin & 1023) == 1023) {
+      const hipError_t q = hipStreamQuery(ctx_->stream);
+      if (q == hipSuccess) { // queue drained: the record must be there now
+        if (__atomic_load_n(&spec_rec_[seq % kSpecRing].seq, __ATOMIC_ACQUIRE) == seq) break;
+        throw Error(2, "speculative line search: record missing after the stream drained");
+      }
+      if (q != hipErrorNotReady) LBF_HIP(q);
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+        throw Error(2, "speculative line search: timed out waiting for the device");
+    }
+  }
+  out->loss = r->loss;
+  out->tgg = r->tgg;
+  out->alpha0 = r->alpha0;
+  out->accept_prev = r->accept_prev;
+  out->status = r->status;
+  out->seq = r->seq;
+}
+
 // Waits for everything queued, clears the abort flag and forgets the aborted iterations.
 void LbfgsSolver::drain(std::deque<Flight> &q, size_t prof_end) {
   LBF_HIP(hipStreamSynchronize(ctx_->stream));
@@ -361,7 +385,6 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
       a.tol = prm_.tol;
       a.alphaf = f.alpha;
       ls_ctl(ctx_->stream, a);
-      LBF_HIP(hipEventRecord(spec_ev_[f.seq % kSpecRing], ctx_->stream));
       f.prof_end = ctx_->prof.recs.size();
       q.push_back(f);
       host_fold = false;
@@ -371,9 +394,8 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
     }
     const Flight f = q.front();
     q.pop_front();
-    LBF_HIP(hipEventSynchronize(spec_ev_[f.seq % kSpecRing]));
     SpecRecord r;
-    std::memcpy(&r, spec_rec_ + f.seq % kSpecRing, sizeof(r)); // complete: the event has fired
+    wait_record(f.seq, &r);
     if (r.seq != f.seq) throw Error(2, "speculative line search: record out of sequence");
     if (f.roles.pair) mark_prev_accepted(rec, r.accept_prev);
     if (r.status == SPEC_REJECT) {

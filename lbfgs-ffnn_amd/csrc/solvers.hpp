@@ -107,12 +107,12 @@ private:
     size_t prof_end;
   };
   void drain(std::deque<Flight> &q, size_t prof_end);
+  void wait_record(int seq, SpecRecord *out);
   static constexpr int kSpecRing = 32;
   int depth_ = 0;
   int seq_ = 0;
   DevBuf<int> abort_;
   SpecRecord *spec_rec_ = nullptr;
-  std::vector<hipEvent_t> spec_ev_;
 
   Objective *obj_;
   Ctx *ctx_;

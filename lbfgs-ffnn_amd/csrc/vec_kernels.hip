@@ -10,7 +10,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 namespace lbf {
+
+#ifdef LBF_KTRACE
+__device__ unsigned long long lbf_kt_buf[256];
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -143,6 +149,152 @@ void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride
   hipLaunchKernelGGL(reduce_slabs_kernel, dim3(unsigned(cdiv(count, cw))), dim3(256), 0, s, slab, splits, stride,
                      count, cw, grad, abort);
   LBF_KERNEL_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------------
+// reduce_all: block = 64 columns x 4 split stripes (each stripe row a 256-B coalesced read).
+// ---------------------------------------------------------------------------------------------
+// Final value of one gradient column (+ its dot contributions). Lanes of wave 0 only.
+__device__ __forceinline__ void ra_column(const RedAllArgs &a, const RedSeg &S, int cg, long long col, bool live,
+                                          double colsum) {
+  const int lane = threadIdx.x & 63;
+  double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+  if (live) {
+    const long long e = S.goff + col;
+    float gv = S.splits > 0 ? float(colsum) : a.G[e];
+    if (a.dots) {
+      const float wv = a.w ? a.w[e] : 0.0f;
+      if (a.lambda != 0.0) gv = gv + float(a.lambda) * wv; // finalize_kernel's update
+      d0 = double(gv) * double(gv);
+      if (a.p) d1 = double(gv) * double(a.p[e]);
+      d2 = double(wv) * double(wv);
+    }
+    if (S.splits > 0 || (a.dots && a.lambda != 0.0)) a.G[e] = gv;
+  }
+  if (a.dots) {
+    d0 = wave_sum(d0);
+    d1 = wave_sum(d1);
+    d2 = wave_sum(d2);
+    if (lane == 0) {
+      a.partials[cg * 3 + 0] = d0;
+      a.partials[cg * 3 + 1] = d1;
+      a.partials[cg * 3 + 2] = d2;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void reduce_all_kernel(const RedAllArgs a) {
+  if (a.abort && *a.abort) return;
+  __shared__ double part[4][RA_COLS];
+  const int t = threadIdx.x, lane = t & 63, stripe = t >> 6;
+  const int b = blockIdx.x;
+  int si = 0;
+  while (si + 1 < a.nseg && a.seg[si + 1].wg0 <= b) ++si;
+  const RedSeg S = a.seg[si];
+  const int local = b - S.wg0;
+  const int cgl = local / S.parts, pi = local - cgl * S.parts;
+  const int cg = S.cg0 + cgl;
+  const long long col = (long long)cgl * RA_COLS + lane;
+  const bool live = col < S.count;
+  // this block's contiguous range of splits
+  const int k0 = int((long long)S.splits * pi / S.parts), k1 = int((long long)S.splits * (pi + 1) / S.parts);
+  double acc = 0.0;
+  if (live && S.splits > 0) {
+    const float *src = S.slab + col;
+    int k = k0 + stripe;
+    for (; k + 12 < k1; k += 16) { // four independent loads in flight, summed in split order
+      const float x0 = src[(long long)k * S.stride], x1 = src[(long long)(k + 4) * S.stride];
+      const float x2 = src[(long long)(k + 8) * S.stride], x3 = src[(long long)(k + 12) * S.stride];
+      acc += double(x0);
+      acc += double(x1);
+      acc += double(x2);
+      acc += double(x3);
+    }
+    for (; k < k1; k += 4) acc += double(src[(long long)k * S.stride]);
+  }
+  part[stripe][lane] = acc;
+  __syncthreads();
+  if (stripe != 0) return;
+  const double colsum = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  if (S.parts > 1)
+    a.colpart[((long long)cg * RA_MAXPART + pi) * RA_COLS + lane] = colsum;
+  else
+    ra_column(a, S, cg, col, live, colsum);
+}
+
+// One block: combine the split-range partials of the multi-range column groups, then (single rank)
+// the eval_tail reduction. Everything it reads was written by earlier launches (stream order), so it
+// needs no fence.
+constexpr int RF_THREADS = 1024;
+__global__ __launch_bounds__(RF_THREADS) void reduce_fin_kernel(const RedAllArgs a) {
+  if (a.abort && *a.abort) return;
+  KT(32);
+  __shared__ double v[4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  for (int b = wave; b < a.nfin; b += RF_THREADS / 64) {
+    int si = 0;
+    while (!(a.seg[si].fin0 >= 0 && b >= a.seg[si].fin0 &&
+             b < a.seg[si].fin0 + int((a.seg[si].count + RA_COLS - 1) / RA_COLS)))
+      ++si;
+    const RedSeg S = a.seg[si];
+    const int cgl = b - S.fin0, cg = S.cg0 + cgl;
+    const long long col = (long long)cgl * RA_COLS + lane;
+    double pv[RA_MAXPART];
+#pragma unroll
+    for (int q = 0; q < RA_MAXPART; ++q)
+      pv[q] = q < S.parts ? a.colpart[((long long)cg * RA_MAXPART + q) * RA_COLS + lane] : 0.0;
+    double colsum = 0.0;
+#pragma unroll
+    for (int q = 0; q < RA_MAXPART; ++q)
+      if (q < S.parts) colsum += pv[q];
+    ra_column(a, S, cg, col, col < S.count, colsum);
+  }
+  KT(33);
+  if (!a.dots) return;
+  __syncthreads(); // this block's partials are visible to the whole block
+  KT(34);
+  // every thread a fixed set of rows, then a fixed-order tree: deterministic, one round of loads
+  __shared__ double ws[RF_THREADS / 64][4];
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int r = t; r < a.ncg; r += RF_THREADS) {
+    acc[0] += a.partials[r * 3 + 0];
+    acc[1] += a.partials[r * 3 + 1];
+    acc[2] += a.partials[r * 3 + 2];
+  }
+  for (int r = t; r < a.nsse; r += RF_THREADS) acc[3] += a.sse_part[r];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double w = wave_sum(acc[i]);
+    if (lane == 0) ws[wave][i] = w;
+  }
+  __syncthreads();
+  if (t < 4) {
+    double x = 0.0;
+    for (int w = 0; w < RF_THREADS / 64; ++w) x += ws[w][t];
+    v[t] = x;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double *sc = a.scal;
+    sc[SC_TGG] = v[0];
+    sc[SC_TGP] = v[1];
+    sc[SC_WW] = v[2];
+    sc[SC_SSE] = v[3];
+    double loss = 0.5 * v[3] * a.inv_scale;
+    if (a.lambda != 0.0) loss += 0.5 * a.lambda * v[2];
+    sc[SC_LOSS] = loss;
+  }
+  KT(35);
+}
+
+void reduce_all(hipStream_t s, const RedAllArgs &a) {
+  if (a.nwg <= 0) return;
+  hipLaunchKernelGGL(reduce_all_kernel, dim3(unsigned(a.nwg)), dim3(256), 0, s, a);
+  LBF_KERNEL_CHECK();
+  if (a.nfin > 0 || a.dots) {
+    hipLaunchKernelGGL(reduce_fin_kernel, dim3(1), dim3(RF_THREADS), 0, s, a);
+    LBF_KERNEL_CHECK();
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -319,6 +471,7 @@ __device__ __forceinline__ int hist_write_slot(const int *ist, int m, int policy
 
 __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, long long chunk, double *partials) {
   if (a.h.abort && *a.h.abort) return;
+  KT(16);
   extern __shared__ __attribute__((aligned(16))) float sh[];
   __shared__ double scratch[6 * 16];
   float *ls = sh, *ly = sh + chunk, *lg = sh + 2 * chunk;
@@ -361,7 +514,9 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
     self[4] += g * y;
     self[5] += g * g;
   }
+  KT(17);
   block_sum<6>(self, scratch); // includes __syncthreads: LDS vectors complete after this
+  KT(18);
   double *out = partials + (long long)blockIdx.x * ncols;
   if (threadIdx.x == 0)
     for (int j = 0; j < 6; ++j) out[6 * h.m + j] = self[j];
@@ -380,25 +535,38 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
     }
     const float *V = (v < count ? h.S : h.Y) + (long long)slot * h.ld + e0;
     double ds = 0.0, dy = 0.0, dg = 0.0;
-    int i = lane * 4;
-    for (; i + 3 < len; i += 256) {
-      const f32x4 x = *reinterpret_cast<const f32x4 *>(V + i);
-      const f32x4 s4 = *reinterpret_cast<const f32x4 *>(ls + i);
-      const f32x4 y4 = *reinterpret_cast<const f32x4 *>(ly + i);
-      const f32x4 g4 = *reinterpret_cast<const f32x4 *>(lg + i);
+    const int full = len & ~3; // elements in whole 16-B quads
+    for (int i0 = lane * 4; i0 < full; i0 += 256 * 4) { // four independent 16-B loads in flight per lane
+      f32x4 xs[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const double xv = x[j];
-        ds += xv * double(s4[j]);
-        dy += xv * double(y4[j]);
-        dg += xv * double(g4[j]);
+      for (int u = 0; u < 4; ++u) {
+        const int iu = i0 + 256 * u;
+        xs[u] = iu < full ? *reinterpret_cast<const f32x4 *>(V + iu) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int iu = i0 + 256 * u;
+        if (iu < full) {
+          const f32x4 s4 = *reinterpret_cast<const f32x4 *>(ls + iu);
+          const f32x4 y4 = *reinterpret_cast<const f32x4 *>(ly + iu);
+          const f32x4 g4 = *reinterpret_cast<const f32x4 *>(lg + iu);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const double xv = xs[u][j];
+            ds += xv * double(s4[j]);
+            dy += xv * double(y4[j]);
+            dg += xv * double(g4[j]);
+          }
+        }
       }
     }
-    for (int j = i; j < len && j < i + 4; ++j) {
-      const double xv = V[j];
-      ds += xv * double(ls[j]);
-      dy += xv * double(ly[j]);
-      dg += xv * double(lg[j]);
+    if (full < len && lane == ((full >> 2) & 63)) { // the partial quad, on the lane whose stride reaches it
+      for (int j = full; j < len; ++j) {
+        const double xv = V[j];
+        ds += xv * double(ls[j]);
+        dy += xv * double(ly[j]);
+        dg += xv * double(lg[j]);
+      }
     }
     ds = wave_sum(ds);
     dy = wave_sum(dy);
@@ -410,6 +578,7 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
       out[6 * li + c + 4] = dg;
     }
   }
+  KT(19);
 }
 
 void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
@@ -435,9 +604,12 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
 // travels by __shfl.
 // ---------------------------------------------------------------------------------------------
 static constexpr int COEF_MAXK = 128;
+static constexpr int HIST_STAGE_DOUBLES = 4096;   // up to 32 KB of partial rows staged per round
+static constexpr int HIST_STATIC_LDS = 16 * 1024; // bound on the kernel's static LDS
 
 __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
   if (a.h.abort && *a.h.abort) return;
+  KT(0);
   extern __shared__ double sy[]; // [k][k] live s_i . y_j after the push (logical order)
   __shared__ double dots[6 * COEF_MAXK + 6];
   __shared__ double gS_l[COEF_MAXK], gY_l[COEF_MAXK], rho_l[COEF_MAXK], alpha_l[COEF_MAXK], c_l[COEF_MAXK];
@@ -452,23 +624,57 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
   }
   for (int i = t; i < S_; i += 256) inv0[i] = -1;
   __syncthreads();
+  KT(1);
   const int count0 = s_count0, w = s_w;
   for (int i = t; i < count0; i += 256) {
     const int j = h.ist[IST_ORDER + i];
     L0[i] = j;
     inv0[j] = i;
   }
-  // ---- A: reduce the columns in use (one wave per column, fixed order) ----
+  // ---- A: reduce the columns in use. Tiles of partial rows are staged into LDS with every load in
+  // flight at once (one global round trip per tile), then thread q sums column q in row order. ----
   const int ncols = 6 * h.m + 6;
   const int nneed = 6 * count0 + 6;
-  for (int q = wave; q < nneed; q += 4) {
-    const int col = q < 6 * count0 ? q : 6 * h.m + (q - 6 * count0);
-    double s = 0.0;
-    for (int r = lane; r < a.nwg; r += 64) s += a.partials[(long long)r * ncols + col];
-    s = wave_sum(s);
-    if (lane == 0) dots[col] = s;
+  double *stage = sy + size_t(h.m) * h.m; // dynamic LDS after the k x k block
+  const int rt = max(1, min(a.nwg, a.stage / nneed));
+  double colacc[(6 * COEF_MAXK + 6 + 255) / 256];
+#pragma unroll
+  for (int i = 0; i < (6 * COEF_MAXK + 6 + 255) / 256; ++i) colacc[i] = 0.0;
+  for (int r0 = 0; r0 < a.nwg; r0 += rt) {
+    const int rows = min(rt, a.nwg - r0);
+    const int tot = rows * nneed;
+    for (int e0 = t; e0 < tot; e0 += 256 * 8) { // 8 independent loads in flight per thread
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + 256 * u;
+        v[u] = 0.0;
+        if (e < tot) {
+          const int r = e / nneed, q = e - r * nneed;
+          const int col = q < 6 * count0 ? q : 6 * h.m + (q - 6 * count0);
+          v[u] = a.partials[(long long)(r0 + r) * ncols + col];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0 + 256 * u < tot) stage[e0 + 256 * u] = v[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < (6 * COEF_MAXK + 6 + 255) / 256; ++i) {
+      const int q = t + 256 * i;
+      if (q < nneed)
+        for (int r = 0; r < rows; ++r) colacc[i] += stage[r * nneed + q];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < (6 * COEF_MAXK + 6 + 255) / 256; ++i) {
+    const int q = t + 256 * i;
+    if (q < nneed) dots[q < 6 * count0 ? q : 6 * h.m + (q - 6 * count0)] = colacc[i];
   }
   __syncthreads();
+  KT(2);
   const double *self = dots + 6 * h.m;
   // ---- B: Gram rows of the new pair and the g-dots -> global (consumed by later steps) ----
   if (wave == 0) {
@@ -538,6 +744,7 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
     s_k = count;
   }
   __syncthreads();
+  KT(3);
   if (a.want_dir <= 0) return;
 
   // ---- C1: stage the live quantities ----
@@ -558,9 +765,25 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
     }
     return h.YY[p * S_ + q];
   };
-  for (int e = t; e < k * k; e += 256) {
-    const int i = e / k, j = e - i * k;
-    sy[e] = SYv(L[i], L[j]);
+  double *yyl = stage; // the staging area is free again: live YY block (k x k)
+  for (int e0 = t; e0 < k * k; e0 += 256 * 4) {
+    double a4[4], b4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + 256 * u;
+      a4[u] = b4[u] = 0.0;
+      if (e < k * k) {
+        const int i = e / k, j = e - i * k;
+        a4[u] = SYv(L[i], L[j]);
+        b4[u] = YYv(L[i], L[j]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (e0 + 256 * u < k * k) {
+        sy[e0 + 256 * u] = a4[u];
+        yyl[e0 + 256 * u] = b4[u];
+      }
   }
   for (int i = t; i < k; i += 256) {
     const int j = L[i];
@@ -575,13 +798,14 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
     rho_l[i] = fresh ? s_rhow : h.rho[j];
   }
   __syncthreads();
+  KT(4);
   if (wave != 0) return;
 
   // ---- C2: the recurrences (wave 0) ----
   const double gg = a.has_g ? self[5] : h.scal[SC_GG];
   double gamma = 1.0;
   if (k > 0) {
-    const double ys = sy[(k - 1) * k + (k - 1)], yy = YYv(L[k - 1], L[k - 1]);
+    const double ys = sy[(k - 1) * k + (k - 1)], yy = yyl[(k - 1) * k + (k - 1)];
     if (a.policy == POL_CPU) {
       gamma = ys / yy; // lbfgs.hpp:127-128, no guard
     } else if (a.policy == POL_CUDA) {
@@ -599,17 +823,19 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
     if (lane < i) r0v -= ai * sy[lane * k + i];
     if (lane + 64 < i) r1v -= ai * sy[(lane + 64) * k + i];
   }
+  KT(5);
   double t0v = 0.0, t1v = 0.0;
   if (lane < k) {
     double acc = gY_l[lane];
-    for (int j = 0; j < k; ++j) acc -= alpha_l[j] * YYv(L[lane], L[j]);
+    for (int j = 0; j < k; ++j) acc -= alpha_l[j] * yyl[lane * k + j];
     t0v = gamma * acc;
   }
   if (lane + 64 < k) {
     double acc = gY_l[lane + 64];
-    for (int j = 0; j < k; ++j) acc -= alpha_l[j] * YYv(L[lane + 64], L[j]);
+    for (int j = 0; j < k; ++j) acc -= alpha_l[j] * yyl[(lane + 64) * k + j];
     t1v = gamma * acc;
   }
+  KT(6);
   for (int i = 0; i < k; ++i) {
     const double cand = rho_l[i] * ((i >> 6) == 0 ? t0v : t1v);
     const double ci = alpha_l[i] - __shfl(cand, i & 63, 64);
@@ -617,6 +843,7 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
     if (lane > i && lane < k) t0v += ci * sy[i * k + lane];
     if (lane + 64 > i && lane + 64 < k) t1v += ci * sy[i * k + lane + 64];
   }
+  KT(7);
   const double ds = a.dsign;
   double part = 0.0;
   for (int i = lane; i < k; i += 64) part += c_l[i] * gS_l[i] - gamma * alpha_l[i] * gY_l[i];
@@ -639,6 +866,7 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
     h.scal[SC_GAMMA] = gamma;
     h.scal[SC_ALPHA0] = (a.iter == 0) ? fmin(1.0, 1.0 / sqrt(gg)) : 1.0;
   }
+  KT(8);
 }
 
 void hist_coef(hipStream_t s, const CoefArgs &a) {
@@ -646,11 +874,16 @@ void hist_coef(hipStream_t s, const CoefArgs &a) {
   static bool attr_set = false;
   if (!attr_set) {
     LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(hist_step_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, COEF_MAXK * COEF_MAXK * 8));
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024 - HIST_STATIC_LDS));
     attr_set = true;
   }
-  const size_t shmem = size_t(a.h.m) * a.h.m * sizeof(double);
-  hipLaunchKernelGGL(hist_step_kernel, dim3(1), dim3(256), shmem, s, a);
+  CoefArgs c = a;
+  const long long room = (160 * 1024 - HIST_STATIC_LDS) / 8 - (long long)a.h.m * a.h.m;
+  c.stage = int(std::min<long long>(HIST_STAGE_DOUBLES, room));
+  LBF_REQUIRE(c.stage >= 6 * a.h.m + 6, "hist_step: LDS staging too small");
+  const size_t shmem = (size_t(a.h.m) * a.h.m + size_t(c.stage)) * sizeof(double);
+  hipLaunchKernelGGL(hist_step_kernel, dim3(1), dim3(256), shmem, s, c);
   LBF_KERNEL_CHECK();
 }
 // ---------------------------------------------------------------------------------------------
@@ -808,15 +1041,19 @@ __global__ __launch_bounds__(64) void ls_ctl_kernel(const LsCtlArgs a) {
   }
   const int status = !ok ? SPEC_REJECT : (conv ? SPEC_CONVERGED : SPEC_ACCEPT);
   if (status != SPEC_ACCEPT) *a.abort = 1;
+  // The record lives in host memory. Every field is stored write-through (system-scope relaxed
+  // atomic stores: sc0 sc1, no cache write-back), the payload is acknowledged before the sequence word
+  // is stored, so a host that sees seq sees the payload. (A system-scope release fence would write
+  // back the whole L2 - microseconds for nothing here.)
   SpecRecord *r = a.rec;
-  r->loss = fn;
-  r->tgg = tgg;
-  r->alpha0 = sc[SC_ALPHA0];
-  r->accept_prev = sc[SC_ACCEPT];
-  r->status = status;
-  __threadfence_system();
-  r->seq = a.seq;
-  __threadfence_system();
+  const double alpha0 = sc[SC_ALPHA0], accept_prev = sc[SC_ACCEPT];
+  __hip_atomic_store(&r->loss, fn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&r->tgg, tgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&r->alpha0, alpha0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&r->accept_prev, accept_prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&r->status, status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(&r->seq, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 void ls_ctl(hipStream_t s, const LsCtlArgs &a) {
@@ -825,3 +1062,9 @@ void ls_ctl(hipStream_t s, const LsCtlArgs &a) {
 }
 
 } // namespace lbf
+
+#ifdef LBF_KTRACE
+extern "C" int lbf_dbg_ktrace(unsigned long long *host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(lbf::lbf_kt_buf), size_t(n) * 8) == hipSuccess ? 0 : 1;
+}
+#endif

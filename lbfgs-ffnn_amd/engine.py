@@ -88,6 +88,10 @@ class Context:
             sid = self.PROF_KINDS.index(kind) * 16 + int(layer.rstrip("]"))
         check(lib().lbf_prof_select(self.h, sid), "lbf_prof_select")
 
+    def prof_sample(self, every: int = 1):
+        """Time only every `every`-th launch of the selected sections."""
+        check(lib().lbf_prof_sample(self.h, int(every)), "lbf_prof_sample")
+
     def prof_read(self):
         """{section name: (total ms, launches)}; section = kind[layer]."""
         n = C.c_int(0)

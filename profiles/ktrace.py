@@ -1,0 +1,37 @@
+"""Phase timestamps of the small kernels (debug build: make -C lbfgs-ffnn_amd ktrace).
+Runs cfg-2 L-BFGS iterations and prints, per instrumented kernel, the wall-clock offsets (us) of
+its phase marks (thread 0 of block 0, last launch)."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["LBF_LIB_PATH"] = os.path.join(ROOT, "lbfgs-ffnn_amd", "build", "ktrace", "liblbfgs_amd.so")
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402,F401
+import __graft_entry__  # noqa: E402
+
+GROUPS = {"hist_step": range(0, 9), "gram(block0)": range(16, 20), "reduce_fin": range(32, 36)}
+
+
+def main():
+    pkg = __graft_entry__.load_package()
+    from lbfgs_ffnn_amd import _lib  # noqa
+    L = _lib.lib()
+    ctx = pkg.Context(0)
+    Xh, Yh = pkg.synth_mnist(60000)
+    X, Y = torch.from_numpy(Xh).cuda(), torch.from_numpy(Yh).cuda()
+    net = pkg.Mlp(ctx, [784, 128, 10], ["relu", "linear"])
+    P = net.init_params(123, "cpu")
+    run = pkg.LbfgsRun(net, P, X, Y, m=10, max_iters=1 << 20, tol=0.0)
+    run.iterate(15)
+    buf = (C.c_ulonglong * 64)()
+    L.lbf_dbg_ktrace.argtypes = [C.c_void_p, C.c_int]
+    assert L.lbf_dbg_ktrace(buf, 64) == 0
+    for name, rg in GROUPS.items():
+        t0 = buf[rg[0]]
+        print(name, " ".join(f"{(buf[i] - t0) / 100.0:.2f}" for i in rg))
+
+
+if __name__ == "__main__":
+    main()

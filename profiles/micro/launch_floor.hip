@@ -1,0 +1,74 @@
+// Launch-floor micro-benchmark (gfx950): back-to-back dependent launches on one stream.
+//   hipcc --offload-arch=gfx950 -O3 launch_floor.hip -o launch_floor && ./launch_floor
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); return 1; } } while (0)
+
+__global__ void empty_k() {}
+__global__ void write_k(double *p, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = double(i);
+}
+// one block sums n doubles (fixed per-thread rows, then a tree)
+__global__ void onesum_k(const double *p, long long n, double *out) {
+  __shared__ double ws[16];
+  double s = 0.0;
+  for (long long r = threadIdx.x; r < n; r += blockDim.x) s += p[r];
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double x = 0.0;
+    for (int w = 0; w < int(blockDim.x >> 6); ++w) x += ws[w];
+    *out = x;
+  }
+}
+
+int main() {
+  double *buf, *out;
+  const long long N = 1 << 22;
+  CK(hipMalloc(&buf, N * 8));
+  CK(hipMalloc(&out, 64));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t a, b, m;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  CK(hipEventCreateWithFlags(&m, hipEventDisableTiming));
+  const int R = 400;
+  auto time = [&](const char *name, auto body) {
+    for (int i = 0; i < 20; ++i) body();
+    hipEventRecord(a, s);
+    for (int i = 0; i < R; ++i) body();
+    hipEventRecord(b, s);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    printf("%-58s %8.2f us/iter\n", name, ms * 1e3f / R);
+  };
+  time("empty<<<1,64>>>", [&] { hipLaunchKernelGGL(empty_k, 1, 64, 0, s); });
+  time("empty<<<1024,256>>>", [&] { hipLaunchKernelGGL(empty_k, 1024, 256, 0, s); });
+  time("empty + hipEventRecord(disable timing)", [&] {
+    hipLaunchKernelGGL(empty_k, 1, 64, 0, s);
+    hipEventRecord(m, s);
+  });
+  for (long long n : {2048LL, 8192LL}) {
+    for (int th : {256, 1024}) {
+      char nm[128];
+      snprintf(nm, sizeof nm, "write %lld dbl (grid) + onesum<<<1,%d>>>", n, th);
+      time(nm, [&] {
+        hipLaunchKernelGGL(write_k, (unsigned)((n + 255) / 256), 256, 0, s, buf, n);
+        hipLaunchKernelGGL(onesum_k, 1, th, 0, s, buf, n, out);
+      });
+    }
+  }
+  time("write 8192 dbl (grid) alone", [&] { hipLaunchKernelGGL(write_k, 32, 256, 0, s, buf, 8192LL); });
+  time("write 32 MB (grid) alone", [&] { hipLaunchKernelGGL(write_k, (unsigned)(N / 256), 256, 0, s, buf, N); });
+  time("write 32 MB + onesum 8192 <<<1,1024>>>", [&] {
+    hipLaunchKernelGGL(write_k, (unsigned)(N / 256), 256, 0, s, buf, N);
+    hipLaunchKernelGGL(onesum_k, 1, 1024, 0, s, buf, 8192LL, out);
+  });
+  return 0;
+}
