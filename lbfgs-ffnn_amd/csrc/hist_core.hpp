@@ -1,0 +1,267 @@
+// Device-side history step shared by hist_step_kernel (vec_kernels.hip) and the fused optimizer tail
+// (tail.hip): given the dots of the new pair / gradient against the live history, write the new
+// Gram rows, apply the pair acceptance rule of the policy (CPU lbfgs.hpp:77-84 ys > 1e-10; CUDA
+// lbfgs.cuh:160 ys > 1e-10; S-LBFGS s_lbfgs.hpp:253 |ys| > 1e-10), push/evict like
+// RingBuffer::push_back (ring_buffer.hpp:43-59), and run the two-loop recursion on coefficients.
+//
+// With q = g - sum_j alpha_j y_j and z = gamma*q + sum_j (alpha_j - beta_j) s_j, the reference's
+// loops (lbfgs.hpp:119-136) are two triangular recurrences on Gram entries:
+//   backward  alpha_i = rho_i * (gS_i - sum_{j>i} alpha_j SY[i][j])
+//   forward   beta_i  = rho_i * (gamma*(gY_i - sum_j alpha_j YY[i][j]) + sum_{j<i} (alpha_j-beta_j) SY[j][i])
+// and z = sum_i (alpha_i - beta_i) s_i - gamma*alpha_i y_i + gamma*g. Entries that involve the slot
+// written in this step come from the fresh dots (LDS), never from global memory written by this same
+// kernel. Lane l of wave 0 owns rows l and l+64 of the recurrences; the per-step scalar travels by
+// __shfl.
+//
+// Dots layout (sm.dots): live logical index i -> [S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g] at
+// 6i..6i+5 (i < m), then [s.s, s.y, y.y, g.s, g.y, g.g] at 6m..6m+5.
+#pragma once
+
+#include "kernels.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace lbf {
+
+constexpr int COEF_MAXK = 128;
+
+struct HistSmem {
+  double dots[6 * COEF_MAXK + 6];
+  double gS_l[COEF_MAXK], gY_l[COEF_MAXK], rho_l[COEF_MAXK], alpha_l[COEF_MAXK], c_l[COEF_MAXK];
+  int L0[COEF_MAXK + 1], L[COEF_MAXK + 1], inv0[COEF_MAXK + 1];
+  int count0, w, k;
+  double rhow;
+};
+
+struct HistStep {
+  HistView h;
+  int has_pair = 0, has_g = 0, reset = 0, policy = POL_CPU;
+  int want_dir = 1; // -1: force the push (explicit upload), 0: no direction, 1: direction (+ CUDA fallback)
+  int iter = 1;
+  double dsign = -1.0;
+};
+
+__device__ __forceinline__ double hc_wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Live order before the step: sm.count0, sm.w (write slot), sm.L0[], sm.inv0[]. Block-wide; ends
+// with __syncthreads. w is the slot the pair was written to (ist[IST_WSLOT] or given).
+__device__ inline void hist_prologue(const HistStep &a, HistSmem &sm, int w) {
+  const HistView &h = a.h;
+  const int t = threadIdx.x, nt = blockDim.x;
+  if (t == 0) {
+    sm.count0 = a.reset ? 0 : h.ist[IST_COUNT];
+    sm.w = w;
+  }
+  for (int i = t; i < h.slots; i += nt) sm.inv0[i] = -1;
+  __syncthreads();
+  for (int i = t; i < sm.count0; i += nt) {
+    const int j = h.ist[IST_ORDER + i];
+    sm.L0[i] = j;
+    sm.L[i] = j;
+    sm.inv0[j] = i;
+  }
+  __syncthreads();
+}
+
+// Steps B and C (see the file comment). Precondition: hist_prologue done and sm.dots filled, then a
+// __syncthreads. Must be the last phase of the kernel: waves other than 0 return early.
+// sy: k*k doubles of LDS; yyl: yy_cap doubles of LDS (the YY block is staged when k*k <= yy_cap).
+__device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, double *yyl, int yy_cap) {
+  const HistView &h = a.h;
+  const int S_ = h.slots, t = threadIdx.x, nt = blockDim.x, lane = t & 63, wave = t >> 6;
+  const int count0 = sm.count0, w = sm.w;
+  const double *dots = sm.dots;
+  const double *self = dots + 6 * h.m;
+  // ---- B: Gram rows of the new pair and the g-dots -> global (consumed by later steps) ----
+  for (int i = t; i < count0; i += nt) {
+    const int j = sm.L0[i];
+    if (a.has_pair && j == w) continue;
+    if (a.has_pair) {
+      h.SS[w * S_ + j] = dots[6 * i + 0];
+      h.SS[j * S_ + w] = dots[6 * i + 0];
+      h.SY[w * S_ + j] = dots[6 * i + 1]; // s_w . y_j
+      h.SY[j * S_ + w] = dots[6 * i + 2]; // s_j . y_w
+      h.YY[w * S_ + j] = dots[6 * i + 3];
+      h.YY[j * S_ + w] = dots[6 * i + 3];
+    }
+    if (a.has_g) {
+      h.gS[j] = dots[6 * i + 4];
+      h.gY[j] = dots[6 * i + 5];
+    }
+  }
+  if (t == 0) {
+    if (a.has_pair) {
+      h.SS[w * S_ + w] = self[0];
+      h.SY[w * S_ + w] = self[1];
+      h.YY[w * S_ + w] = self[2];
+      if (a.has_g) {
+        h.gS[w] = self[3];
+        h.gY[w] = self[4];
+      }
+    }
+    if (a.has_g) h.scal[SC_GG] = self[5];
+    int count = count0;
+    sm.rhow = (a.has_pair && w < S_) ? h.rho[w] : 0.0;
+    if (a.reset) h.ist[IST_COUNT] = 0;
+    if (a.has_pair) {
+      const double ys = self[1];
+      h.scal[SC_YS] = ys;
+      bool acc = (a.policy == POL_SLBFGS) ? fabs(ys) > 1e-10 : ys > 1e-10;
+      if (a.want_dir < 0) acc = true; // explicit-history upload (lbf_two_loop): always push
+      h.scal[SC_ACCEPT] = acc ? 1.0 : 0.0;
+      if (acc) {
+        sm.rhow = 1.0 / ys;
+        h.rho[w] = sm.rhow;
+        if (count < h.m) {
+          sm.L[count++] = w;
+          if (a.policy != POL_CUDA || count < h.m) {
+            unsigned long long live[3] = {0ull, 0ull, 0ull}; // next free slot: any of the m+1 not live
+            for (int q = 0; q < count; ++q) live[sm.L[q] >> 6] |= 1ull << (sm.L[q] & 63);
+            int f = S_;
+            for (int b = 0; b < 3 && f == S_; ++b)
+              if (~live[b]) f = min(S_, b * 64 + __builtin_ctzll(~live[b]));
+            h.ist[IST_FREE] = f;
+          }
+        } else {
+          const int evicted = sm.L[0];
+          for (int q = 0; q + 1 < h.m; ++q) sm.L[q] = sm.L[q + 1];
+          sm.L[h.m - 1] = w;
+          if (w != evicted) h.ist[IST_FREE] = evicted;
+        }
+        for (int q = 0; q < count; ++q) h.ist[IST_ORDER + q] = sm.L[q];
+        h.ist[IST_COUNT] = count;
+      }
+    }
+    h.scal[SC_COUNT] = double(count);
+    sm.k = count;
+  }
+  __syncthreads();
+  if (a.want_dir <= 0) return;
+
+  // ---- C1: stage the live quantities ----
+  const int k = sm.k;
+  const int *L = sm.L, *inv0 = sm.inv0;
+  auto SYv = [&](int p, int q) -> double { // s_p . y_q
+    if (a.has_pair) {
+      if (p == w && q == w) return self[1];
+      if (p == w) return dots[6 * inv0[q] + 1];
+      if (q == w) return dots[6 * inv0[p] + 2];
+    }
+    return h.SY[p * S_ + q];
+  };
+  auto YYv = [&](int p, int q) -> double {
+    if (a.has_pair) {
+      if (p == w && q == w) return self[2];
+      if (p == w) return dots[6 * inv0[q] + 3];
+      if (q == w) return dots[6 * inv0[p] + 3];
+    }
+    return h.YY[p * S_ + q];
+  };
+  const bool yy_lds = k * k <= yy_cap;
+  for (int e0 = t; e0 < k * k; e0 += nt * 4) { // independent loads in flight
+    double a4[4], b4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + nt * u;
+      a4[u] = b4[u] = 0.0;
+      if (e < k * k) {
+        const int i = e / k, j = e - i * k;
+        a4[u] = SYv(L[i], L[j]);
+        b4[u] = yy_lds ? YYv(L[i], L[j]) : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (e0 + nt * u < k * k) {
+        sy[e0 + nt * u] = a4[u];
+        if (yy_lds) yyl[e0 + nt * u] = b4[u];
+      }
+  }
+  for (int i = t; i < k; i += nt) {
+    const int j = L[i];
+    const bool fresh = a.has_pair && j == w;
+    if (a.has_g) {
+      sm.gS_l[i] = fresh ? self[3] : dots[6 * inv0[j] + 4];
+      sm.gY_l[i] = fresh ? self[4] : dots[6 * inv0[j] + 5];
+    } else {
+      sm.gS_l[i] = h.gS[j];
+      sm.gY_l[i] = h.gY[j];
+    }
+    sm.rho_l[i] = fresh ? sm.rhow : h.rho[j];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+
+  // ---- C2: the recurrences (wave 0) ----
+  const double *gS_l = sm.gS_l, *gY_l = sm.gY_l, *rho_l = sm.rho_l;
+  double *alpha_l = sm.alpha_l, *c_l = sm.c_l;
+  const double gg = a.has_g ? self[5] : h.scal[SC_GG];
+  double gamma = 1.0;
+  if (k > 0) {
+    const double ys = sy[(k - 1) * k + (k - 1)];
+    const double yy = yy_lds ? yyl[(k - 1) * k + (k - 1)] : YYv(L[k - 1], L[k - 1]);
+    if (a.policy == POL_CPU) {
+      gamma = ys / yy; // lbfgs.hpp:127-128, no guard
+    } else if (a.policy == POL_CUDA) {
+      gamma = yy > 0.0 ? ys / yy : 1.0; // lbfgs.cuh:247
+    } else {
+      gamma = fabs(yy) < 1e-12 ? 1.0 : ys / yy; // s_lbfgs.hpp:119-126
+      gamma = fmin(fmax(gamma, 1e-6), 1e6);
+    }
+  }
+  double r0v = lane < k ? gS_l[lane] : 0.0, r1v = lane + 64 < k ? gS_l[lane + 64] : 0.0;
+  for (int i = k - 1; i >= 0; --i) {
+    const double cand = rho_l[i] * ((i >> 6) == 0 ? r0v : r1v);
+    const double ai = __shfl(cand, i & 63, 64);
+    alpha_l[i] = ai; // every lane writes the same value: later reads follow the lane's own write
+    if (lane < i) r0v -= ai * sy[lane * k + i];
+    if (lane + 64 < i) r1v -= ai * sy[(lane + 64) * k + i];
+  }
+  double t0v = 0.0, t1v = 0.0;
+  if (lane < k) {
+    double acc = gY_l[lane];
+    for (int j = 0; j < k; ++j) acc -= alpha_l[j] * (yy_lds ? yyl[lane * k + j] : YYv(L[lane], L[j]));
+    t0v = gamma * acc;
+  }
+  if (lane + 64 < k) {
+    double acc = gY_l[lane + 64];
+    for (int j = 0; j < k; ++j)
+      acc -= alpha_l[j] * (yy_lds ? yyl[(lane + 64) * k + j] : YYv(L[lane + 64], L[j]));
+    t1v = gamma * acc;
+  }
+  for (int i = 0; i < k; ++i) {
+    const double cand = rho_l[i] * ((i >> 6) == 0 ? t0v : t1v);
+    const double ci = alpha_l[i] - __shfl(cand, i & 63, 64);
+    c_l[i] = ci;
+    if (lane > i && lane < k) t0v += ci * sy[i * k + lane];
+    if (lane + 64 > i && lane + 64 < k) t1v += ci * sy[i * k + lane + 64];
+  }
+  const double ds = a.dsign;
+  double part = 0.0;
+  for (int i = lane; i < k; i += 64) part += c_l[i] * gS_l[i] - gamma * alpha_l[i] * gY_l[i];
+  const double gTz = hc_wave_sum(part) + gamma * gg;
+  // lbfgs.cuh:97-104 (CUDA semantics only): not a descent direction -> steepest descent + reset
+  const bool fallback = a.policy == POL_CUDA && a.want_dir == 1 && ds * gTz >= 0.0;
+  for (int i = lane; i < k; i += 64) {
+    h.coef[i] = fallback ? 0.0 : ds * c_l[i];
+    h.coef[S_ + i] = fallback ? 0.0 : ds * (-gamma * alpha_l[i]);
+  }
+  if (lane == 0) {
+    h.coef[2 * S_] = fallback ? -1.0 : ds * gamma;
+    h.scal[SC_RESET] = fallback ? 1.0 : 0.0;
+    h.scal[SC_GTP] = fallback ? -gg : ds * gTz;
+    if (fallback) {
+      h.ist[IST_COUNT] = 0;
+      h.scal[SC_COUNT] = 0.0;
+    }
+    h.scal[SC_GG] = gg;
+    h.scal[SC_GAMMA] = gamma;
+    h.scal[SC_ALPHA0] = (a.iter == 0) ? fmin(1.0, 1.0 / sqrt(gg)) : 1.0;
+  }
+}
+
+} // namespace lbf

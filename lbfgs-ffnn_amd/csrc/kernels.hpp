@@ -71,6 +71,10 @@ void head_fused(hipStream_t s, const float *A, int H, const float *P, int Out, c
                 double *sse_part, const int *abort = nullptr);
 
 // grad[e] = sum_s slab[s*stride + e] * scale (fixed order), e in [0, count)
+// Forward split-K finish: out = act(sum_s slab[s] + bias), slabs summed in split order (fp32, like
+// the GEMM's own accumulation).
+void fwd_reduce_act(hipStream_t s, const float *slab, int splits, long long stride, int M, int N, const float *bias,
+                    int act, float *out, const int *abort);
 void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride, long long count, float *grad,
                   const int *abort = nullptr);
 

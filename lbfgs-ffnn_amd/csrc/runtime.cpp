@@ -80,7 +80,7 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
 // a multiple of the 32-deep LDS tile.
 void Mlp::plan(long long B) {
   if (planned_ == B) return;
-  size_t slab = 0;
+  size_t slab = 0, fslab = 0;
   for (auto &L : layers_) {
     int BM, BN;
     gemm_tile_for(L.out, &BM, &BN);
@@ -94,8 +94,24 @@ void Mlp::plan(long long B) {
     L.k_chunk = int(kc);
     L.slab_off = slab;
     if (splits > 1) slab += size_t(splits) * size_t(M) * L.out; // every layer keeps its own slabs until reduce_all
+    // forward GEMM: with fewer row tiles than CUs (a data-parallel rank's shard), split K so the chip
+    // fills; the partial slabs are summed in split order with the bias and activation afterwards
+    const long long ftiles = cdiv(B, 128) * cdiv(L.out, BN);
+    L.fsplits = 1;
+    L.fk_chunk = L.in;
+    if (ftiles < 192 && L.in >= 256) {
+      long long fs = std::min(cdiv(384, ftiles), (long long)L.in / 128);
+      long long fkc = cdiv(cdiv(L.in, fs), 32) * 32;
+      fs = cdiv(L.in, fkc);
+      if (fs > 1) {
+        L.fsplits = int(fs);
+        L.fk_chunk = int(fkc);
+        fslab = std::max(fslab, size_t(fs) * size_t(B) * L.out);
+      }
+    }
   }
   slab_.ensure(slab);
+  fslab_.ensure(std::max<size_t>(fslab, 1));
   planned_ = B;
 }
 
@@ -150,8 +166,19 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
     d.bias = P + L.off + size_t(L.in) * L.out;
     d.act = L.act;
     d.abort = ctx_->abort;
-    ProfScope ps(ctx_, PK_FWD, int(l));
-    gemm(s, d);
+    if (L.fsplits > 1) {
+      d.epi = EPI_STORE;
+      d.C = fslab_.get();
+      d.splits = L.fsplits;
+      d.k_chunk = L.fk_chunk;
+      d.slab_stride = B * L.out;
+      ProfScope ps(ctx_, PK_FWD, int(l));
+      gemm(s, d);
+      fwd_reduce_act(s, fslab_.get(), L.fsplits, B * L.out, int(B), L.out, d.bias, L.act, A_[l].get(), ctx_->abort);
+    } else {
+      ProfScope ps(ctx_, PK_FWD, int(l));
+      gemm(s, d);
+    }
     in = A_[l].get();
   }
   return in;

@@ -57,6 +57,8 @@ struct Layer {
   int splits = 1;  // split-K factor of the dW GEMM at the planned batch
   int k_chunk = 0;
   size_t slab_off = 0; // this layer's partial slabs inside the shared slab buffer
+  int fsplits = 1;     // split-K factor of the forward GEMM (few row tiles: small per-rank batches)
+  int fk_chunk = 0;
 };
 
 // RAII section: records an event pair around the enclosed launches when profiling is on.
@@ -100,7 +102,7 @@ private:
   size_t nparams_ = 0;
   long long cap_ = -1, planned_ = -1;
   std::vector<DevBuf<float>> A_, D_;
-  DevBuf<float> slab_, head_slab_;
+  DevBuf<float> slab_, head_slab_, fslab_;
   bool use_head_ = true; // fused output layer when the shape allows (LBF_NO_HEAD=1 disables)
   DevBuf<double> loss_part_, dots_part_, sse_, colpart_;
   long long evals_ = 0;

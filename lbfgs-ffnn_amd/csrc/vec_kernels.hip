@@ -6,6 +6,7 @@
 // Sscal with host pointer mode (kernels.cuh:28-50, every scalar a blocking device->host copy), and
 // CudaLBFGS::compute_direction_ring (src/cuda/lbfgs.cuh:206-261, 2k+2 blocking dots + 2k axpys).
 #include "internal.hpp"
+#include "hist_core.hpp"
 #include "kernels.hpp"
 
 #include <hip/hip_runtime.h>
@@ -141,6 +142,42 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float *slab, in
     for (int q = 0; q < nst; ++q) r += part[q * cw + t];
     grad[col] = float(r);
   }
+}
+
+__global__ __launch_bounds__(256) void fwd_reduce_act_kernel(const float *slab, int splits, long long stride, int M,
+                                                             int N, const float *bias, int act, float *out,
+                                                             const int *abort) {
+  if (abort && *abort) return;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)M * N) return;
+  float v[8];
+  float acc = 0.0f;
+  int k = 0;
+  for (; k + 8 <= splits; k += 8) { // independent loads in flight, summed in split order
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = slab[(long long)(k + u) * stride + e];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; k < splits; ++k) acc += slab[(long long)k * stride + e];
+  const int n = int(e % N);
+  const float z = acc + (bias ? bias[n] : 0.0f);
+  float a;
+  switch (act) {
+  case ACT_TANH: a = tanhf(z); break;
+  case ACT_RELU: a = z > 0.0f ? z : 0.0f; break;
+  case ACT_SIGMOID: a = 1.0f / (1.0f + expf(-z)); break;
+  default: a = z;
+  }
+  out[e] = a;
+}
+
+void fwd_reduce_act(hipStream_t s, const float *slab, int splits, long long stride, int M, int N, const float *bias,
+                    int act, float *out, const int *abort) {
+  const long long n = (long long)M * N;
+  hipLaunchKernelGGL(fwd_reduce_act_kernel, dim3(unsigned(cdiv(n, 256))), dim3(256), 0, s, slab, splits, stride, M, N,
+                     bias, act, out, abort);
+  LBF_KERNEL_CHECK();
 }
 
 void reduce_slabs(hipStream_t s, const float *slab, int splits, long long stride, long long count, float *grad,
@@ -590,47 +627,31 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// History step (one workgroup): (A) reduce the Gram sweep's per-workgroup partials, (B) write the
-// new pair's Gram rows and g-dots, apply the acceptance rule of the policy (CPU lbfgs.hpp:77-84
-// ys > 1e-10; CUDA lbfgs.cuh:160 ys > 1e-10; S-LBFGS s_lbfgs.hpp:253 |ys| > 1e-10) and push/evict
-// like RingBuffer::push_back (ring_buffer.hpp:43-59), (C) run the two-loop recursion on
-// coefficients. With q = g - sum_j alpha_j y_j and z = gamma*q + sum_j (alpha_j - beta_j) s_j, the
-// reference's loops (lbfgs.hpp:119-136) are two triangular recurrences on Gram entries:
-//   backward  alpha_i = rho_i * (gS_i - sum_{j>i} alpha_j SY[i][j])
-//   forward   beta_i  = rho_i * (gamma*(gY_i - sum_j alpha_j YY[i][j]) + sum_{j<i} (alpha_j-beta_j) SY[j][i])
-// and z = sum_i (alpha_i - beta_i) s_i - gamma*alpha_i y_i + gamma*g. Entries that involve the slot
-// written in this step come from the freshly reduced dots (LDS), never from global memory written by
-// this same kernel. Lane l of wave 0 owns rows l and l+64 of the recurrences; the per-step scalar
-// travels by __shfl.
+// History step (one workgroup): (A) reduce the Gram sweep's per-workgroup partials, then the push and
+// the two-loop recurrences of hist_core.hpp.
 // ---------------------------------------------------------------------------------------------
-static constexpr int COEF_MAXK = 128;
 static constexpr int HIST_STAGE_DOUBLES = 4096;   // up to 32 KB of partial rows staged per round
 static constexpr int HIST_STATIC_LDS = 16 * 1024; // bound on the kernel's static LDS
 
 __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
   if (a.h.abort && *a.h.abort) return;
   KT(0);
-  extern __shared__ double sy[]; // [k][k] live s_i . y_j after the push (logical order)
-  __shared__ double dots[6 * COEF_MAXK + 6];
-  __shared__ double gS_l[COEF_MAXK], gY_l[COEF_MAXK], rho_l[COEF_MAXK], alpha_l[COEF_MAXK], c_l[COEF_MAXK];
-  __shared__ int L0[COEF_MAXK + 1], L[COEF_MAXK + 1], inv0[COEF_MAXK + 1];
-  __shared__ int s_count0, s_w, s_k;
-  __shared__ double s_rhow;
+  extern __shared__ double sy[]; // [k][k] live s_i . y_j after the push (logical order), then staging
+  __shared__ HistSmem sm;
   const HistView &h = a.h;
-  const int S_ = h.slots, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  if (t == 0) {
-    s_count0 = a.reset ? 0 : h.ist[IST_COUNT];
-    s_w = h.ist[IST_WSLOT];
-  }
-  for (int i = t; i < S_; i += 256) inv0[i] = -1;
-  __syncthreads();
+  const int t = threadIdx.x;
+  HistStep st;
+  st.h = a.h;
+  st.has_pair = a.has_pair;
+  st.has_g = a.has_g;
+  st.reset = a.reset;
+  st.policy = a.policy;
+  st.want_dir = a.want_dir;
+  st.iter = a.iter;
+  st.dsign = a.dsign;
+  hist_prologue(st, sm, h.ist[IST_WSLOT]);
   KT(1);
-  const int count0 = s_count0, w = s_w;
-  for (int i = t; i < count0; i += 256) {
-    const int j = h.ist[IST_ORDER + i];
-    L0[i] = j;
-    inv0[j] = i;
-  }
+  const int count0 = sm.count0;
   // ---- A: reduce the columns in use. Tiles of partial rows are staged into LDS with every load in
   // flight at once (one global round trip per tile), then thread q sums column q in row order. ----
   const int ncols = 6 * h.m + 6;
@@ -671,202 +692,11 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
 #pragma unroll
   for (int i = 0; i < (6 * COEF_MAXK + 6 + 255) / 256; ++i) {
     const int q = t + 256 * i;
-    if (q < nneed) dots[q < 6 * count0 ? q : 6 * h.m + (q - 6 * count0)] = colacc[i];
+    if (q < nneed) sm.dots[q < 6 * count0 ? q : 6 * h.m + (q - 6 * count0)] = colacc[i];
   }
   __syncthreads();
   KT(2);
-  const double *self = dots + 6 * h.m;
-  // ---- B: Gram rows of the new pair and the g-dots -> global (consumed by later steps) ----
-  if (wave == 0) {
-    for (int i = lane; i < count0; i += 64) {
-      const int j = L0[i];
-      if (a.has_pair && j == w) continue;
-      if (a.has_pair) {
-        h.SS[w * S_ + j] = dots[6 * i + 0];
-        h.SS[j * S_ + w] = dots[6 * i + 0];
-        h.SY[w * S_ + j] = dots[6 * i + 1]; // s_w . y_j
-        h.SY[j * S_ + w] = dots[6 * i + 2]; // s_j . y_w
-        h.YY[w * S_ + j] = dots[6 * i + 3];
-        h.YY[j * S_ + w] = dots[6 * i + 3];
-      }
-      if (a.has_g) {
-        h.gS[j] = dots[6 * i + 4];
-        h.gY[j] = dots[6 * i + 5];
-      }
-    }
-  }
-  if (t == 0) {
-    if (a.has_pair) {
-      h.SS[w * S_ + w] = self[0];
-      h.SY[w * S_ + w] = self[1];
-      h.YY[w * S_ + w] = self[2];
-      if (a.has_g) {
-        h.gS[w] = self[3];
-        h.gY[w] = self[4];
-      }
-    }
-    if (a.has_g) h.scal[SC_GG] = self[5];
-    int count = count0;
-    for (int i = 0; i < count0; ++i) L[i] = L0[i];
-    s_rhow = (a.has_pair && w < S_) ? h.rho[w] : 0.0;
-    if (a.reset) h.ist[IST_COUNT] = 0;
-    if (a.has_pair) {
-      const double ys = self[1];
-      h.scal[SC_YS] = ys;
-      bool acc = (a.policy == POL_SLBFGS) ? fabs(ys) > 1e-10 : ys > 1e-10;
-      if (a.want_dir < 0) acc = true; // explicit-history upload (lbf_two_loop): always push
-      h.scal[SC_ACCEPT] = acc ? 1.0 : 0.0;
-      if (acc) {
-        s_rhow = 1.0 / ys;
-        h.rho[w] = s_rhow;
-        if (count < h.m) {
-          L[count++] = w;
-          if (a.policy != POL_CUDA || count < h.m) {
-            int f = 0; // next free slot: any of the m+1 slots not live
-            for (; f < S_; ++f) {
-              bool live = false;
-              for (int q = 0; q < count; ++q) live |= (L[q] == f);
-              if (!live) break;
-            }
-            h.ist[IST_FREE] = f;
-          }
-        } else {
-          const int evicted = L[0];
-          for (int q = 0; q + 1 < h.m; ++q) L[q] = L[q + 1];
-          L[h.m - 1] = w;
-          if (w != evicted) h.ist[IST_FREE] = evicted;
-        }
-        for (int q = 0; q < count; ++q) h.ist[IST_ORDER + q] = L[q];
-        h.ist[IST_COUNT] = count;
-      }
-    }
-    h.scal[SC_COUNT] = double(count);
-    s_k = count;
-  }
-  __syncthreads();
-  KT(3);
-  if (a.want_dir <= 0) return;
-
-  // ---- C1: stage the live quantities ----
-  const int k = s_k;
-  auto SYv = [&](int p, int q) -> double { // s_p . y_q
-    if (a.has_pair) {
-      if (p == w && q == w) return self[1];
-      if (p == w) return dots[6 * inv0[q] + 1];
-      if (q == w) return dots[6 * inv0[p] + 2];
-    }
-    return h.SY[p * S_ + q];
-  };
-  auto YYv = [&](int p, int q) -> double {
-    if (a.has_pair) {
-      if (p == w && q == w) return self[2];
-      if (p == w) return dots[6 * inv0[q] + 3];
-      if (q == w) return dots[6 * inv0[p] + 3];
-    }
-    return h.YY[p * S_ + q];
-  };
-  double *yyl = stage; // the staging area is free again: live YY block (k x k)
-  for (int e0 = t; e0 < k * k; e0 += 256 * 4) {
-    double a4[4], b4[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + 256 * u;
-      a4[u] = b4[u] = 0.0;
-      if (e < k * k) {
-        const int i = e / k, j = e - i * k;
-        a4[u] = SYv(L[i], L[j]);
-        b4[u] = YYv(L[i], L[j]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (e0 + 256 * u < k * k) {
-        sy[e0 + 256 * u] = a4[u];
-        yyl[e0 + 256 * u] = b4[u];
-      }
-  }
-  for (int i = t; i < k; i += 256) {
-    const int j = L[i];
-    const bool fresh = a.has_pair && j == w;
-    if (a.has_g) {
-      gS_l[i] = fresh ? self[3] : dots[6 * inv0[j] + 4];
-      gY_l[i] = fresh ? self[4] : dots[6 * inv0[j] + 5];
-    } else {
-      gS_l[i] = h.gS[j];
-      gY_l[i] = h.gY[j];
-    }
-    rho_l[i] = fresh ? s_rhow : h.rho[j];
-  }
-  __syncthreads();
-  KT(4);
-  if (wave != 0) return;
-
-  // ---- C2: the recurrences (wave 0) ----
-  const double gg = a.has_g ? self[5] : h.scal[SC_GG];
-  double gamma = 1.0;
-  if (k > 0) {
-    const double ys = sy[(k - 1) * k + (k - 1)], yy = yyl[(k - 1) * k + (k - 1)];
-    if (a.policy == POL_CPU) {
-      gamma = ys / yy; // lbfgs.hpp:127-128, no guard
-    } else if (a.policy == POL_CUDA) {
-      gamma = yy > 0.0 ? ys / yy : 1.0; // lbfgs.cuh:247
-    } else {
-      gamma = fabs(yy) < 1e-12 ? 1.0 : ys / yy; // s_lbfgs.hpp:119-126
-      gamma = fmin(fmax(gamma, 1e-6), 1e6);
-    }
-  }
-  double r0v = lane < k ? gS_l[lane] : 0.0, r1v = lane + 64 < k ? gS_l[lane + 64] : 0.0;
-  for (int i = k - 1; i >= 0; --i) {
-    const double cand = rho_l[i] * ((i >> 6) == 0 ? r0v : r1v);
-    const double ai = __shfl(cand, i & 63, 64);
-    alpha_l[i] = ai; // every lane writes the same value: later reads follow the lane's own write
-    if (lane < i) r0v -= ai * sy[lane * k + i];
-    if (lane + 64 < i) r1v -= ai * sy[(lane + 64) * k + i];
-  }
-  KT(5);
-  double t0v = 0.0, t1v = 0.0;
-  if (lane < k) {
-    double acc = gY_l[lane];
-    for (int j = 0; j < k; ++j) acc -= alpha_l[j] * yyl[lane * k + j];
-    t0v = gamma * acc;
-  }
-  if (lane + 64 < k) {
-    double acc = gY_l[lane + 64];
-    for (int j = 0; j < k; ++j) acc -= alpha_l[j] * yyl[(lane + 64) * k + j];
-    t1v = gamma * acc;
-  }
-  KT(6);
-  for (int i = 0; i < k; ++i) {
-    const double cand = rho_l[i] * ((i >> 6) == 0 ? t0v : t1v);
-    const double ci = alpha_l[i] - __shfl(cand, i & 63, 64);
-    c_l[i] = ci;
-    if (lane > i && lane < k) t0v += ci * sy[i * k + lane];
-    if (lane + 64 > i && lane + 64 < k) t1v += ci * sy[i * k + lane + 64];
-  }
-  KT(7);
-  const double ds = a.dsign;
-  double part = 0.0;
-  for (int i = lane; i < k; i += 64) part += c_l[i] * gS_l[i] - gamma * alpha_l[i] * gY_l[i];
-  const double gTz = wave_sum(part) + gamma * gg;
-  // lbfgs.cuh:97-104 (CUDA semantics only): not a descent direction -> steepest descent + reset
-  const bool fallback = a.policy == POL_CUDA && a.want_dir == 1 && ds * gTz >= 0.0;
-  for (int i = lane; i < k; i += 64) {
-    h.coef[i] = fallback ? 0.0 : ds * c_l[i];
-    h.coef[S_ + i] = fallback ? 0.0 : ds * (-gamma * alpha_l[i]);
-  }
-  if (lane == 0) {
-    h.coef[2 * S_] = fallback ? -1.0 : ds * gamma;
-    h.scal[SC_RESET] = fallback ? 1.0 : 0.0;
-    h.scal[SC_GTP] = fallback ? -gg : ds * gTz;
-    if (fallback) {
-      h.ist[IST_COUNT] = 0;
-      h.scal[SC_COUNT] = 0.0;
-    }
-    h.scal[SC_GG] = gg;
-    h.scal[SC_GAMMA] = gamma;
-    h.scal[SC_ALPHA0] = (a.iter == 0) ? fmin(1.0, 1.0 / sqrt(gg)) : 1.0;
-  }
-  KT(8);
+  hist_core(st, sm, sy, stage, a.stage);
 }
 
 void hist_coef(hipStream_t s, const CoefArgs &a) {
