@@ -59,7 +59,39 @@ struct GemmK {
   long long ldaux;
   int aux_act;
   const int *abort;
+  int side_planes; // blockIdx.z < side_planes: side job (dispatched first); GEMM split = z - side_planes
+  const float *side_slab;
+  int side_splits;
+  long long side_stride, side_count;
+  float *side_dst;
 };
+
+// Side job (see GemmDesc): one 64-column group x 4 split stripes per block, fp64 in split order.
+__device__ __forceinline__ void gemm_side_job(const GemmK &g, double *red) {
+  const int t = threadIdx.x, lane = t & 63, stripe = t >> 6;
+  const int nside = gridDim.x * gridDim.y * g.side_planes;
+  const int id = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  for (long long c0 = (long long)id * 64; c0 < g.side_count; c0 += (long long)nside * 64) {
+    const long long c = c0 + lane;
+    double acc = 0.0;
+    if (c < g.side_count) {
+      const float *src = g.side_slab + c;
+      int k = stripe;
+      for (; k + 28 < g.side_splits; k += 32) { // eight independent loads in flight
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[(long long)(k + 4 * u) * g.side_stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += double(v[u]);
+      }
+      for (; k < g.side_splits; k += 4) acc += double(src[(long long)k * g.side_stride]);
+    }
+    red[t] = acc;
+    __syncthreads();
+    if (stripe == 0 && c < g.side_count) g.side_dst[c] = float(((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane]);
+    __syncthreads();
+  }
+}
 
 // k-contiguous operand: R rows x 32 k. Thread chunk c -> row c>>3, k-quad c&7.
 template <int R, bool GATHER>
@@ -135,12 +167,17 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
   constexpr int BSZ = BKC ? BN * LDK : BK * (BN + 4);
   __shared__ __attribute__((aligned(16))) float lds[2 * (ASZ + BSZ)];
   if (g.abort && *g.abort) return;
+  if (int(blockIdx.z) < g.side_planes) {
+    gemm_side_job(g, reinterpret_cast<double *>(lds));
+    return;
+  }
+  const int zsplit = int(blockIdx.z) - g.side_planes;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 31, lh = lane >> 5;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-  const int kb = blockIdx.z * g.k_chunk;
+  const int kb = zsplit * g.k_chunk;
   const int ke = min(g.K, kb + g.k_chunk);
 
   f32x16 acc[TM][TN];
@@ -235,7 +272,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
   }
 
   // Epilogue: lanes 0-31 own consecutive columns -> each register row is a 128-B coalesced store.
-  float *C = g.C + (EPI == EPI_STORE ? (long long)blockIdx.z * g.slab_stride : 0LL);
+  float *C = g.C + (EPI == EPI_STORE ? (long long)zsplit * g.slab_stride : 0LL);
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int n = n0 + wn * TN * 32 + tn * 32 + li;
@@ -287,7 +324,14 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.ldaux = d.ldaux;
   k.aux_act = d.aux_act;
   k.abort = d.abort;
-  dim3 grid((d.N + BN - 1) / BN, (d.M + BM - 1) / BM, d.splits > 1 ? d.splits : 1);
+  const long long gx = (d.N + BN - 1) / BN, gy = (d.M + BM - 1) / BM;
+  k.side_planes = (d.side_slab && d.side_count > 0) ? int(cdiv(cdiv(d.side_count, 64), gx * gy)) : 0;
+  k.side_slab = d.side_slab;
+  k.side_splits = d.side_splits;
+  k.side_stride = d.side_stride;
+  k.side_count = d.side_count;
+  k.side_dst = d.side_dst;
+  dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
   if (d.a_idx)
     hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true>), grid, dim3(256), 0, s, k);
   else

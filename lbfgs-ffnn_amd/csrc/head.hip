@@ -17,6 +17,7 @@
 // step s (a permutation of the summation order), so k-contiguous operands are ds_read_b128 runs.
 #include "internal.hpp"
 #include "kernels.hpp"
+#include "wave.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -43,11 +44,7 @@ __device__ __forceinline__ float h_dact(int a, float y) {
   }
 }
 
-__device__ __forceinline__ double h_wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+__device__ __forceinline__ double h_wave_sum(double v) { return wave_sum_f64(v); }
 
 constexpr int HMAX = 256;
 constexpr int HMAX_OUT = 16;

@@ -10,14 +10,16 @@
 //   forward   beta_i  = rho_i * (gamma*(gY_i - sum_j alpha_j YY[i][j]) + sum_{j<i} (alpha_j-beta_j) SY[j][i])
 // and z = sum_i (alpha_i - beta_i) s_i - gamma*alpha_i y_i + gamma*g. Entries that involve the slot
 // written in this step come from the fresh dots (LDS), never from global memory written by this same
-// kernel. Lane l of wave 0 owns rows l and l+64 of the recurrences; the per-step scalar travels by
-// __shfl.
+// kernel. Lane l of wave 0 owns rows l and l+64 of the recurrences; the per-step scalar is broadcast
+// with v_readlane.
 //
 // Dots layout (sm.dots): live logical index i -> [S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g] at
 // 6i..6i+5 (i < m), then [s.s, s.y, y.y, g.s, g.y, g.g] at 6m..6m+5.
 #pragma once
 
+#include "internal.hpp"
 #include "kernels.hpp"
+#include "wave.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -41,11 +43,16 @@ struct HistStep {
   double dsign = -1.0;
 };
 
-__device__ __forceinline__ double hc_wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Ring slot the next pair is written to.
+__device__ __forceinline__ int hist_write_slot(const int *ist, int m, int policy, int reset) {
+  const int count = reset ? 0 : ist[IST_COUNT];
+  // CUDA semantics (lbfgs.cuh:149-169): the slot at hist_head is overwritten even when the pair is
+  // then rejected; when the ring is full that slot is the oldest live pair.
+  if (policy == POL_CUDA && count == m) return ist[IST_ORDER + 0];
+  return ist[IST_FREE];
 }
+
+__device__ __forceinline__ double hc_wave_sum(double v) { return wave_sum_f64(v); }
 
 // Live order before the step: sm.count0, sm.w (write slot), sm.L0[], sm.inv0[]. Block-wide; ends
 // with __syncthreads. w is the slot the pair was written to (ist[IST_WSLOT] or given).
@@ -69,13 +76,15 @@ __device__ inline void hist_prologue(const HistStep &a, HistSmem &sm, int w) {
 
 // Steps B and C (see the file comment). Precondition: hist_prologue done and sm.dots filled, then a
 // __syncthreads. Must be the last phase of the kernel: waves other than 0 return early.
-// sy: k*k doubles of LDS; yyl: yy_cap doubles of LDS (the YY block is staged when k*k <= yy_cap).
-__device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, double *yyl, int yy_cap) {
+// sy: sy_cap >= k*k doubles of LDS (SY, plus its transpose when 2*k*k fit); yyl: yy_cap doubles of
+// LDS (the YY block is staged when k*k <= yy_cap).
+__device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, int sy_cap, double *yyl, int yy_cap) {
   const HistView &h = a.h;
   const int S_ = h.slots, t = threadIdx.x, nt = blockDim.x, lane = t & 63, wave = t >> 6;
   const int count0 = sm.count0, w = sm.w;
   const double *dots = sm.dots;
   const double *self = dots + 6 * h.m;
+  KT(56);
   // ---- B: Gram rows of the new pair and the g-dots -> global (consumed by later steps) ----
   for (int i = t; i < count0; i += nt) {
     const int j = sm.L0[i];
@@ -138,8 +147,10 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, do
     }
     h.scal[SC_COUNT] = double(count);
     sm.k = count;
+    KT(57);
   }
   __syncthreads();
+  KT(58);
   if (a.want_dir <= 0) return;
 
   // ---- C1: stage the live quantities ----
@@ -162,6 +173,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, do
     return h.YY[p * S_ + q];
   };
   const bool yy_lds = k * k <= yy_cap;
+  const bool sy_t = 2 * k * k <= sy_cap;
   for (int e0 = t; e0 < k * k; e0 += nt * 4) { // independent loads in flight
     double a4[4], b4[4];
 #pragma unroll
@@ -175,11 +187,14 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, do
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (e0 + nt * u < k * k) {
-        sy[e0 + nt * u] = a4[u];
-        if (yy_lds) yyl[e0 + nt * u] = b4[u];
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + nt * u;
+      if (e < k * k) {
+        sy[e] = a4[u];
+        if (sy_t) sy[k * k + (e % k) * k + e / k] = a4[u]; // transposed copy
+        if (yy_lds) yyl[e] = b4[u];
       }
+    }
   }
   for (int i = t; i < k; i += nt) {
     const int j = L[i];
@@ -194,11 +209,13 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, do
     sm.rho_l[i] = fresh ? sm.rhow : h.rho[j];
   }
   __syncthreads();
+  KT(59);
   if (wave != 0) return;
 
-  // ---- C2: the recurrences (wave 0) ----
+  // ---- C2: the recurrences (wave 0). Lane l owns indices l and l+64: alpha, c and the running
+  // sums live in its registers; the step's scalar is broadcast with v_readlane. LDS reads are
+  // unit-stride across lanes: SY^T for the backward sweep, YY by symmetry, SY rows forward. ----
   const double *gS_l = sm.gS_l, *gY_l = sm.gY_l, *rho_l = sm.rho_l;
-  double *alpha_l = sm.alpha_l, *c_l = sm.c_l;
   const double gg = a.has_g ? self[5] : h.scal[SC_GG];
   double gamma = 1.0;
   if (k > 0) {
@@ -213,42 +230,113 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, do
       gamma = fmin(fmax(gamma, 1e-6), 1e6);
     }
   }
-  double r0v = lane < k ? gS_l[lane] : 0.0, r1v = lane + 64 < k ? gS_l[lane + 64] : 0.0;
-  for (int i = k - 1; i >= 0; --i) {
-    const double cand = rho_l[i] * ((i >> 6) == 0 ? r0v : r1v);
-    const double ai = __shfl(cand, i & 63, 64);
-    alpha_l[i] = ai; // every lane writes the same value: later reads follow the lane's own write
-    if (lane < i) r0v -= ai * sy[lane * k + i];
-    if (lane + 64 < i) r1v -= ai * sy[(lane + 64) * k + i];
+  const double *syT = sy + k * k; // syT[i*k + l] = SY[l][i] (when sy_t)
+  double al0 = 0.0, al1 = 0.0;     // alpha of indices lane, lane + 64
+  double c0 = 0.0, c1 = 0.0;       // alpha - beta of indices lane, lane + 64
+  if (k <= 64 && sy_t && yy_lds) {
+    // Fast path: the LDS operands of 8 steps are loaded ahead of them (unit stride across lanes), so
+    // each step is VALU + v_readlane only.
+    const double rho_me = lane < k ? rho_l[lane] : 0.0;
+    double r = lane < k ? gS_l[lane] : 0.0;
+    KT(63);
+    KTC(64);
+    for (int i0 = k - 1; i0 >= 0; i0 -= 8) { // backward: alpha_i = rho_i (gS_i - sum_{j>i} alpha_j SY[i][j])
+      double col[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 - u;
+        col[u] = (i >= 0 && lane < i) ? syT[i * k + lane] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 - u;
+        if (i >= 0) {
+          const double ai = lane_f64(rho_me * r, i);
+          if (lane == i) al0 = ai;
+          r = lane < i ? r - ai * col[u] : r;
+        }
+      }
+    }
+    KTC(65);
+    KT(60);
+    double acc = lane < k ? gY_l[lane] : 0.0; // gY_l - sum_j alpha_j YY[l][j]  (YY symmetric)
+    for (int j0 = 0; j0 < k; j0 += 8) {
+      double yv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) yv[u] = (j0 + u < k && lane < k) ? yyl[(j0 + u) * k + lane] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (j0 + u < k) acc -= lane_f64(al0, j0 + u) * yv[u];
+    }
+    double tv = gamma * acc;
+    for (int i0 = 0; i0 < k; i0 += 8) { // forward: beta_i = rho_i t_i ; t_l += (alpha_i - beta_i) SY[i][l]
+      double row[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u;
+        row[u] = (i < k && lane > i && lane < k) ? sy[i * k + lane] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u;
+        if (i < k) {
+          const double cand = rho_me * tv;
+          const double ci = lane_f64(al0, i) - lane_f64(cand, i);
+          if (lane == i) c0 = ci;
+          tv = (lane > i && lane < k) ? tv + ci * row[u] : tv;
+        }
+      }
+    }
+  } else {
+    double r0v = lane < k ? gS_l[lane] : 0.0, r1v = lane + 64 < k ? gS_l[lane + 64] : 0.0;
+    for (int i = k - 1; i >= 0; --i) {
+      const double cand = rho_l[i] * ((i >> 6) == 0 ? r0v : r1v);
+      const double ai = lane_f64(cand, i & 63);
+      if (lane == (i & 63)) {
+        if (i < 64) al0 = ai;
+        else al1 = ai;
+      }
+      if (lane < i) r0v -= ai * (sy_t ? syT[i * k + lane] : sy[lane * k + i]);
+      if (lane + 64 < i) r1v -= ai * (sy_t ? syT[i * k + lane + 64] : sy[(lane + 64) * k + i]);
+    }
+    KT(60);
+    double t0v = 0.0, t1v = 0.0;
+    {
+      double acc0 = lane < k ? gY_l[lane] : 0.0, acc1 = lane + 64 < k ? gY_l[lane + 64] : 0.0;
+      for (int j = 0; j < k; ++j) {
+        const double aj = lane_f64(j < 64 ? al0 : al1, j & 63);
+        if (lane < k) acc0 -= aj * (yy_lds ? yyl[j * k + lane] : YYv(L[j], L[lane]));
+        if (lane + 64 < k) acc1 -= aj * (yy_lds ? yyl[j * k + lane + 64] : YYv(L[j], L[lane + 64]));
+      }
+      t0v = gamma * acc0;
+      t1v = gamma * acc1;
+    }
+    for (int i = 0; i < k; ++i) {
+      const double cand = rho_l[i] * ((i >> 6) == 0 ? t0v : t1v);
+      const double ci = lane_f64(i < 64 ? al0 : al1, i & 63) - lane_f64(cand, i & 63);
+      if (lane == (i & 63)) {
+        if (i < 64) c0 = ci;
+        else c1 = ci;
+      }
+      if (lane > i && lane < k) t0v += ci * sy[i * k + lane];
+      if (lane + 64 > i && lane + 64 < k) t1v += ci * sy[i * k + lane + 64];
+    }
   }
-  double t0v = 0.0, t1v = 0.0;
-  if (lane < k) {
-    double acc = gY_l[lane];
-    for (int j = 0; j < k; ++j) acc -= alpha_l[j] * (yy_lds ? yyl[lane * k + j] : YYv(L[lane], L[j]));
-    t0v = gamma * acc;
-  }
-  if (lane + 64 < k) {
-    double acc = gY_l[lane + 64];
-    for (int j = 0; j < k; ++j)
-      acc -= alpha_l[j] * (yy_lds ? yyl[(lane + 64) * k + j] : YYv(L[lane + 64], L[j]));
-    t1v = gamma * acc;
-  }
-  for (int i = 0; i < k; ++i) {
-    const double cand = rho_l[i] * ((i >> 6) == 0 ? t0v : t1v);
-    const double ci = alpha_l[i] - __shfl(cand, i & 63, 64);
-    c_l[i] = ci;
-    if (lane > i && lane < k) t0v += ci * sy[i * k + lane];
-    if (lane + 64 > i && lane + 64 < k) t1v += ci * sy[i * k + lane + 64];
-  }
+  KT(61);
   const double ds = a.dsign;
   double part = 0.0;
-  for (int i = lane; i < k; i += 64) part += c_l[i] * gS_l[i] - gamma * alpha_l[i] * gY_l[i];
+  if (lane < k) part += c0 * gS_l[lane] - gamma * al0 * gY_l[lane];
+  if (lane + 64 < k) part += c1 * gS_l[lane + 64] - gamma * al1 * gY_l[lane + 64];
   const double gTz = hc_wave_sum(part) + gamma * gg;
   // lbfgs.cuh:97-104 (CUDA semantics only): not a descent direction -> steepest descent + reset
   const bool fallback = a.policy == POL_CUDA && a.want_dir == 1 && ds * gTz >= 0.0;
-  for (int i = lane; i < k; i += 64) {
-    h.coef[i] = fallback ? 0.0 : ds * c_l[i];
-    h.coef[S_ + i] = fallback ? 0.0 : ds * (-gamma * alpha_l[i]);
+  if (lane < k) {
+    h.coef[lane] = fallback ? 0.0 : ds * c0;
+    h.coef[S_ + lane] = fallback ? 0.0 : ds * (-gamma * al0);
+  }
+  if (lane + 64 < k) {
+    h.coef[lane + 64] = fallback ? 0.0 : ds * c1;
+    h.coef[S_ + lane + 64] = fallback ? 0.0 : ds * (-gamma * al1);
   }
   if (lane == 0) {
     h.coef[2 * S_] = fallback ? -1.0 : ds * gamma;
@@ -262,6 +350,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, do
     h.scal[SC_GAMMA] = gamma;
     h.scal[SC_ALPHA0] = (a.iter == 0) ? fmin(1.0, 1.0 / sqrt(gg)) : 1.0;
   }
+  KT(62);
 }
 
 } // namespace lbf

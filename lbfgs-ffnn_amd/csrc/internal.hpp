@@ -90,12 +90,19 @@ inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
 // Phase timestamps for kernel tuning (debug build only: make ktrace). KT(slot) stores the 100 MHz
 // wall clock from thread 0 of block 0; lbf_dbg_ktrace() copies the slots to the host.
 #ifdef LBF_KTRACE
-extern __device__ unsigned long long lbf_kt_buf[256];
+static __device__ unsigned long long lbf_kt_buf[256]; // one per translation unit (no RDC)
 #define KT(slot)                                                                                        \
   do {                                                                                                  \
     if (blockIdx.x == 0 && threadIdx.x == 0) lbf_kt_buf[slot] = wall_clock64();                         \
   } while (0)
+#define KTC(slot)                                                                                       \
+  do {                                                                                                  \
+    if (blockIdx.x == 0 && threadIdx.x == 0) lbf_kt_buf[slot] = clock64();                              \
+  } while (0)
 #else
+#define KTC(slot)                                                                                       \
+  do {                                                                                                  \
+  } while (0)
 #define KT(slot)                                                                                        \
   do {                                                                                                  \
   } while (0)

@@ -43,6 +43,13 @@ struct GemmDesc {
   long long ldaux = 0;
   int aux_act = ACT_LINEAR;
   const int *abort = nullptr; // speculative execution: the kernel is a no-op when *abort != 0
+  // Side job riding in an extra z-plane of the launch: side_dst[c] = sum_s side_slab[s*stride + c]
+  // (fixed split order, fp64) for c < side_count. Used to finish the fused head's [dW ; db] slabs
+  // while the next layer's dW GEMM runs.
+  const float *side_slab = nullptr;
+  int side_splits = 0;
+  long long side_stride = 0, side_count = 0;
+  float *side_dst = nullptr;
 };
 
 void gemm(hipStream_t s, const GemmDesc &d);
@@ -242,10 +249,35 @@ struct CoefArgs {
   int has_pair = 0, has_g = 0, reset = 0, policy = POL_CPU;
   int want_dir = 1;
   int iter = 1;
-  int stage = 0; // LDS doubles for staging partial rows (set by hist_coef)
+  int stage = 0;  // LDS doubles for staging partial rows (set by hist_coef)
+  int sy_cap = 0; // LDS doubles for SY (and its transpose) (set by hist_coef)
   double dsign = -1.0;
 };
 void hist_coef(hipStream_t s, const CoefArgs &a);
+
+// Fused optimizer tail of a speculative L-BFGS iteration (tail.hip): the evaluation's gradient
+// columns, the new pair s = x_t - x_prev, y = g_t - g_prev written into the ring's write slot, the
+// Gram sweep of (s, y, g_t) against the live history (one partial row per block), then one block
+// that takes the line-search decision and, on acceptance, pushes the pair and computes the next
+// direction's coefficients (hist_core.hpp). Row layout (nc = 6m + 8 doubles): the Gram sweep's
+// columns (see hist_core.hpp), then g.p and w.w.
+constexpr int TAIL_MAXM = 32;
+struct TailArgs {
+  RedAllArgs ra;                // every segment with parts == 1; ra.w = x_t, ra.p = direction
+  const float *hilo = nullptr;  // data parallel: all-reduced SSE (hi, lo) behind the gradient
+  HistView h;
+  int has_pair = 0;
+  const float *x_prev = nullptr, *g_prev = nullptr;
+  int policy = POL_CPU;
+  int iter_next = 1;
+  LsCtlArgs ls;
+  double *rows = nullptr; // [nb][nc]
+  double *dots = nullptr; // [nc]
+  int nb = 0, nc = 0; // nb = ra.ncg blocks (one 64-column group each)
+};
+void tail_reduce(hipStream_t s, const TailArgs &a); // tail_reduce + tail_cols launches
+void tail_fin(hipStream_t s, const TailArgs &a);    // one block
+int tail_vpw(int m);                                // vectors per wave of the Gram sweep (0: unsupported)
 
 struct CombineArgs {
   HistView h;

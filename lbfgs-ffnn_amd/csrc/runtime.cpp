@@ -142,6 +142,15 @@ void Mlp::ensure(long long B) {
   sse_.ensure(1);
 }
 
+// Layer l's dW slabs are reduced by side blocks of layer l-1's dW launch: the fused head's always,
+// other layers' when they have many split-K slabs over few columns.
+bool Mlp::side_reduced(int l, bool fused, int nloss) const {
+  if (l <= 0 || l >= int(layers_.size())) return false;
+  (void)nloss;
+  if (fused && l == int(layers_.size()) - 1) return true;
+  return layers_[l].splits > 2 * RA_SPLITS_PER_PART;
+}
+
 const float *Mlp::forward(const float *P, const float *X, const int *idx, long long B, int nrun) {
   ensure(B);
   hipStream_t s = ctx_->stream;
@@ -185,7 +194,7 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
 }
 
 void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
-                    double inv_scale, double lambda, const float *pdir, double *scal) {
+                    double inv_scale, double lambda, const float *pdir, double *scal, const TailFuse *tf) {
   hipStream_t s = ctx_->stream;
   const int nl = int(layers_.size());
   const Layer &Lo = layers_[nl - 1];
@@ -230,6 +239,18 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     d.splits = L.splits;
     d.k_chunk = L.k_chunk;
     d.abort = ctx_->abort;
+    if (l + 1 < nl && side_reduced(l + 1, fused, nloss)) {
+      // finish layer l+1's [dW ; db] slabs (the fused head's, or many split-K slabs) in side blocks
+      // of this launch, while its GEMM runs
+      const Layer &N1 = layers_[l + 1];
+      const long long nseg = (long long)(N1.in + 1) * N1.out;
+      const bool head = fused && l + 1 == nl - 1;
+      d.side_slab = head ? head_slab_.get() : slab_.get() + N1.slab_off;
+      d.side_splits = head ? nloss : N1.splits;
+      d.side_stride = nseg;
+      d.side_count = nseg;
+      d.side_dst = G + N1.off;
+    }
     const long long seg = (long long)(L.in + 1) * L.out;
     if (L.splits > 1) {
       d.C = slab_.get() + L.slab_off;
@@ -285,9 +306,8 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     g.count = (long long)(L.in + 1) * L.out;
     g.goff = (long long)L.off;
     g.stride = g.count;
-    if (fused && l == nl - 1) {
-      g.slab = head_slab_.get();
-      g.splits = nloss;
+    if (side_reduced(l, fused, nloss)) {
+      // finished by the side blocks of the next dW launch: as written
     } else if (L.splits > 1) {
       g.slab = slab_.get() + L.slab_off;
       g.splits = L.splits;
@@ -306,6 +326,57 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     ra.ncg += ncols;
   }
   ra.nseg = nl;
+  bool tail_ok = tf != nullptr;
+  for (int l = 0; l < nl && tail_ok; ++l) tail_ok = ra.seg[l].parts == 1;
+  if (tail_ok) {
+    // fused optimizer tail (tail.hip); data parallel: local reduce -> all-reduce -> tail over G
+    TailArgs ta;
+    const float *hilo = nullptr;
+    if (ctx_->nranks > 1) {
+      RedAllArgs loc = ra;
+      loc.dots = 0;
+      {
+        ProfScope ps(ctx_, PK_SLAB, 0);
+        reduce_all(s, loc);
+        sse_pack(s, loss_part_.get(), nloss, G + nparams_, ctx_->abort);
+      }
+      {
+        ProfScope ps(ctx_, PK_ALLREDUCE);
+        ctx_->allreduce(G, nparams_ + 2);
+      }
+      hilo = G + nparams_;
+      for (int l = 0; l < nl; ++l) {
+        ra.seg[l].slab = nullptr;
+        ra.seg[l].splits = 0;
+      }
+    }
+    ta.ra = ra;
+    ta.hilo = hilo;
+    ta.h = tf->h;
+    ta.h.abort = ctx_->abort;
+    ta.has_pair = tf->has_pair;
+    ta.x_prev = tf->x_prev;
+    ta.g_prev = tf->g_prev;
+    ta.policy = tf->policy;
+    ta.iter_next = tf->iter_next;
+    ta.ls = tf->ls;
+    ta.nc = 6 * tf->h.m + 8;
+    ta.nb = ra.ncg; // one 64-column group per block: latency-bound work wants every CU busy
+    trows_.ensure(size_t(ta.nb) * ta.nc);
+    tdots_.ensure(size_t(ta.nc));
+    ta.rows = trows_.get();
+    ta.dots = tdots_.get();
+    {
+      ProfScope ps(ctx_, PK_GRAM, 1);
+      tail_reduce(s, ta);
+    }
+    {
+      ProfScope ps(ctx_, PK_COEF, 1);
+      tail_fin(s, ta);
+    }
+    ++evals_;
+    return;
+  }
   {
     ProfScope ps(ctx_, PK_SLAB, 0);
     reduce_all(s, ra);

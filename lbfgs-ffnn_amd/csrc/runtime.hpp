@@ -51,6 +51,17 @@ struct Ctx {
   void allreduce(float *buf, size_t count);
 };
 
+// Fused optimizer tail request (speculative L-BFGS fast path, tail.hip): the pair inputs, the
+// history and the line-search decision taken after the evaluation.
+struct TailFuse {
+  HistView h;
+  int has_pair = 0;
+  const float *x_prev = nullptr, *g_prev = nullptr;
+  int policy = POL_CPU;
+  int iter_next = 1;
+  LsCtlArgs ls;
+};
+
 struct Layer {
   int in, out, act;
   size_t off;      // flat offset of the [(in+1) x out] segment
@@ -91,12 +102,13 @@ public:
   //   pdir : optional direction for the g.p dot.
   //   scal : device fp64 status block (SC_LOSS, SC_TGG, SC_TGP, SC_WW, SC_SSE written).
   void loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
-                 double inv_scale, double lambda, const float *pdir, double *scal);
+                 double inv_scale, double lambda, const float *pdir, double *scal, const TailFuse *tf = nullptr);
   long long evals() const { return evals_; }
   void discard_evals(long long k) { evals_ -= k; } // speculative evaluations that were aborted
 
 private:
   void ensure(long long B);
+  bool side_reduced(int l, bool fused, int nloss) const;
   Ctx *ctx_;
   std::vector<Layer> layers_;
   size_t nparams_ = 0;
@@ -104,7 +116,7 @@ private:
   std::vector<DevBuf<float>> A_, D_;
   DevBuf<float> slab_, head_slab_, fslab_;
   bool use_head_ = true; // fused output layer when the shape allows (LBF_NO_HEAD=1 disables)
-  DevBuf<double> loss_part_, dots_part_, sse_, colpart_;
+  DevBuf<double> loss_part_, dots_part_, sse_, colpart_, trows_, tdots_;
   long long evals_ = 0;
   void plan(long long B);
 };

@@ -67,6 +67,9 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
   depth_ = 3;
   if (const char *e = std::getenv("LBF_SPEC_DEPTH")) depth_ = std::max(0, std::min(16, std::atoi(e)));
   if (!obj_->async()) depth_ = 0;
+  // Fused optimizer tail on the speculative path (LBF_FUSED_TAIL=0 disables).
+  fuse_ = depth_ > 0 && obj_->fused_tail() && prm_.m > 0 && prm_.m <= TAIL_MAXM;
+  if (const char *e = std::getenv("LBF_FUSED_TAIL")) fuse_ = fuse_ && e[0] != '0';
   if (depth_ > 0) {
     abort_.resize(1);
     LBF_HIP(hipMemsetAsync(abort_.get(), 0, sizeof(int), ctx_->stream));
@@ -158,8 +161,23 @@ void LbfgsSolver::restore(const Roles &r) {
   pending_reset_ = r.reset;
 }
 
-float LbfgsSolver::begin_iteration() {
+float LbfgsSolver::begin_iteration(const LsCtlArgs *ls) {
   const bool armijo = prm_.line_search == LBF_LS_ARMIJO;
+  if (ls && dir_ready_) { // the previous fused tail computed this direction's coefficients
+    float alpha = 1.0f;
+    hist_.combine(g_, p_.get(), x_, xt_, nullptr, !armijo, armijo ? double(alpha) : 0.0);
+    TailFuse tf;
+    tf.h = hist_.view();
+    tf.has_pair = prm_.m > 0;
+    tf.x_prev = x_;
+    tf.g_prev = g_;
+    tf.policy = armijo ? POL_CUDA : POL_CPU;
+    tf.iter_next = iter_ + 1;
+    tf.ls = *ls;
+    tf.ls.alphaf = alpha;
+    obj_->eval_fused(xt_, gt_, p_.get(), hist_.scal(), tf);
+    return alpha;
+  }
   GramArgs ga;
   ga.policy = armijo ? POL_CUDA : POL_CPU;
   ga.has_g = 1;
@@ -180,7 +198,20 @@ float LbfgsSolver::begin_iteration() {
   } else {
     hist_.combine(g_, p_.get(), x_, xt_, nullptr, true, 0.0); // xt = x + alpha0 p
   }
-  eval(xt_, gt_, p_.get());
+  if (ls) {
+    TailFuse tf;
+    tf.h = hist_.view();
+    tf.has_pair = prm_.m > 0;
+    tf.x_prev = x_;
+    tf.g_prev = g_;
+    tf.policy = armijo ? POL_CUDA : POL_CPU;
+    tf.iter_next = iter_ + 1;
+    tf.ls = *ls;
+    tf.ls.alphaf = alpha;
+    obj_->eval_fused(xt_, gt_, p_.get(), hist_.scal(), tf);
+  } else {
+    eval(xt_, gt_, p_.get());
+  }
   return alpha;
 }
 
@@ -368,7 +399,6 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
     while (issued < iters && int(q.size()) < depth_) {
       Flight f;
       f.roles = roles();
-      f.alpha = begin_iteration();
       f.seq = seq_++;
       LsCtlArgs a;
       a.scal = hist_.scal();
@@ -383,8 +413,14 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
       a.c1 = prm_.c1;
       a.c2 = prm_.c2;
       a.tol = prm_.tol;
-      a.alphaf = f.alpha;
-      ls_ctl(ctx_->stream, a);
+      if (fuse_) {
+        f.alpha = begin_iteration(&a); // decision inside the fused tail
+        dir_ready_ = true;
+      } else {
+        f.alpha = begin_iteration();
+        a.alphaf = f.alpha;
+        ls_ctl(ctx_->stream, a);
+      }
       f.prof_end = ctx_->prof.recs.size();
       q.push_back(f);
       host_fold = false;
@@ -400,6 +436,7 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
     if (f.roles.pair) mark_prev_accepted(rec, r.accept_prev);
     if (r.status == SPEC_REJECT) {
       drain(q, f.prof_end);
+      dir_ready_ = false; // the host finishes this iteration; the next one builds its direction
       restore(f.roles);
       read_status();
       if (armijo)
@@ -424,6 +461,7 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
       // the iterations queued behind were aborted: return to the roles right after this step
       if (!q.empty()) restore(q.front().roles);
       drain(q, f.prof_end);
+      dir_ready_ = false; // the fused tail does not push the pair of a converged step
       issued = done;
       host_fold = true;
     }

@@ -22,6 +22,9 @@ struct Objective {
   // Asynchronous objectives can be enqueued ahead of the host's line-search decisions.
   virtual bool async() const { return false; }
   virtual void discard_evals(long long) {}
+  // Evaluation followed by the fused optimizer tail (tail.hip); only when fused_tail() is true.
+  virtual bool fused_tail() const { return false; }
+  virtual void eval_fused(const float *, float *, const float *, double *, const TailFuse &) {}
 };
 
 // The MLP's fused loss+grad over the rank's shard (mean over n_global samples).
@@ -39,6 +42,10 @@ struct MlpObjective : Objective {
   long long evals() const override { return net->evals(); }
   bool async() const override { return true; }
   void discard_evals(long long k) override { net->discard_evals(k); }
+  bool fused_tail() const override { return true; }
+  void eval_fused(const float *x, float *g, const float *pdir, double *scal, const TailFuse &tf) override {
+    net->loss_grad(x, g, X, Y, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal, &tf);
+  }
 };
 
 // A user callback with the reference's LossGradFun contract: returns the loss, writes the gradient
@@ -82,8 +89,9 @@ private:
   int iterate_spec(int iters, lbf_record *rec);
   bool entry_converged() const;
   // First trial of an iteration (history update, direction, x + alpha p, evaluation), enqueued only.
-  // Returns the Armijo trial step (Wolfe takes alpha0 from the device status block).
-  float begin_iteration();
+  // Returns the Armijo trial step (Wolfe takes alpha0 from the device status block). With `ls`, the
+  // evaluation carries the fused tail: decision + (on acceptance) the next direction's coefficients.
+  float begin_iteration(const LsCtlArgs *ls = nullptr);
   // Rest of the iteration once hs_ holds the first trial's status: further trials, role rotation,
   // record.
   void finish_wolfe(lbf_record *rec);
@@ -111,6 +119,8 @@ private:
   static constexpr int kSpecRing = 32;
   int depth_ = 0;
   int seq_ = 0;
+  bool fuse_ = false;      // fused optimizer tail on the speculative path
+  bool dir_ready_ = false; // the last fused tail left the next direction's coefficients on the device
   DevBuf<int> abort_;
   SpecRecord *spec_rec_ = nullptr;
 

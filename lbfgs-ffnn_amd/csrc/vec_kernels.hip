@@ -8,6 +8,7 @@
 #include "internal.hpp"
 #include "hist_core.hpp"
 #include "kernels.hpp"
+#include "wave.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -15,20 +16,13 @@
 
 namespace lbf {
 
-#ifdef LBF_KTRACE
-__device__ unsigned long long lbf_kt_buf[256];
-#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------------------------
 // wave / block reductions (fixed butterfly order -> bitwise reproducible)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+__device__ __forceinline__ double wave_sum(double v) { return wave_sum_f64(v); }
 
 // Sum NV values over a 256- or 512-thread block; result valid in thread 0. scratch: NV*16 doubles.
 template <int NV>
@@ -498,13 +492,6 @@ int gram_nwg(long long n) {
 }
 static long long gram_chunk(long long n, int nwg) { return cdiv(cdiv(n, nwg), 4) * 4; }
 
-__device__ __forceinline__ int hist_write_slot(const int *ist, int m, int policy, int reset) {
-  const int count = reset ? 0 : ist[IST_COUNT];
-  // CUDA semantics (lbfgs.cuh:149-169): the slot at hist_head is overwritten even when the pair is
-  // then rejected; when the ring is full that slot is the oldest live pair.
-  if (policy == POL_CUDA && count == m) return ist[IST_ORDER + 0];
-  return ist[IST_FREE];
-}
 
 __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, long long chunk, double *partials) {
   if (a.h.abort && *a.h.abort) return;
@@ -656,7 +643,7 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
   // flight at once (one global round trip per tile), then thread q sums column q in row order. ----
   const int ncols = 6 * h.m + 6;
   const int nneed = 6 * count0 + 6;
-  double *stage = sy + size_t(h.m) * h.m; // dynamic LDS after the k x k block
+  double *stage = sy + a.sy_cap; // dynamic LDS after the SY block(s)
   const int rt = max(1, min(a.nwg, a.stage / nneed));
   double colacc[(6 * COEF_MAXK + 6 + 255) / 256];
 #pragma unroll
@@ -696,7 +683,7 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
   }
   __syncthreads();
   KT(2);
-  hist_core(st, sm, sy, stage, a.stage);
+  hist_core(st, sm, sy, a.sy_cap, stage, a.stage);
 }
 
 void hist_coef(hipStream_t s, const CoefArgs &a) {
@@ -709,10 +696,12 @@ void hist_coef(hipStream_t s, const CoefArgs &a) {
     attr_set = true;
   }
   CoefArgs c = a;
-  const long long room = (160 * 1024 - HIST_STATIC_LDS) / 8 - (long long)a.h.m * a.h.m;
-  c.stage = int(std::min<long long>(HIST_STAGE_DOUBLES, room));
-  LBF_REQUIRE(c.stage >= 6 * a.h.m + 6, "hist_step: LDS staging too small");
-  const size_t shmem = (size_t(a.h.m) * a.h.m + size_t(c.stage)) * sizeof(double);
+  const long long total = (160 * 1024 - HIST_STATIC_LDS) / 8, m2 = (long long)a.h.m * a.h.m;
+  const long long need_stage = 6LL * a.h.m + 6;
+  c.sy_cap = int(std::min(2 * m2, total - need_stage)); // SY, and its transpose when it fits
+  LBF_REQUIRE(c.sy_cap >= m2, "hist_step: LDS too small for the SY block");
+  c.stage = int(std::min<long long>(HIST_STAGE_DOUBLES, total - c.sy_cap));
+  const size_t shmem = (size_t(c.sy_cap) + size_t(c.stage)) * sizeof(double);
   hipLaunchKernelGGL(hist_step_kernel, dim3(1), dim3(256), shmem, s, c);
   LBF_KERNEL_CHECK();
 }

@@ -11,7 +11,9 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402,F401
 import __graft_entry__  # noqa: E402
 
-GROUPS = {"hist_step": range(0, 9), "gram(block0)": range(16, 20), "reduce_fin": range(32, 36)}
+GROUPS = {"hist_step": range(0, 9), "gram(block0)": range(16, 20), "reduce_fin": range(32, 36),
+          "tail_fin": range(40, 45), "tail_reduce(block0)": range(48, 55),
+          "hist_core(in tail_fin)": range(56, 63)}
 
 
 def main():
@@ -25,9 +27,19 @@ def main():
     P = net.init_params(123, "cpu")
     run = pkg.LbfgsRun(net, P, X, Y, m=10, max_iters=1 << 20, tol=0.0)
     run.iterate(15)
-    buf = (C.c_ulonglong * 64)()
+    os.environ["LBF_SPEC_DEPTH"] = "0"  # the host-driven path for the classic kernels
+    run = pkg.LbfgsRun(net, P, X, Y, m=10, max_iters=1 << 20, tol=0.0)
+    run.iterate(15)
+    buf = (C.c_ulonglong * 80)()
+    tbuf = (C.c_ulonglong * 80)()
     L.lbf_dbg_ktrace.argtypes = [C.c_void_p, C.c_int]
-    assert L.lbf_dbg_ktrace(buf, 64) == 0
+    L.lbf_dbg_ktrace_tail.argtypes = [C.c_void_p, C.c_int]
+    assert L.lbf_dbg_ktrace(buf, 80) == 0 and L.lbf_dbg_ktrace_tail(tbuf, 80) == 0
+    for i in range(40, 64):
+        buf[i] = tbuf[i]
+    wall = (tbuf[60] - tbuf[63]) / 100.0
+    cyc = tbuf[65] - tbuf[64]
+    print(f"backward sweep: {wall:.2f} us wall, {cyc} shader cycles -> {cyc / max(wall, 1e-9):.0f} MHz")
     for name, rg in GROUPS.items():
         t0 = buf[rg[0]]
         print(name, " ".join(f"{(buf[i] - t0) / 100.0:.2f}" for i in rg))

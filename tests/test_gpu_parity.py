@@ -246,13 +246,14 @@ def test_lbfgs_full_size_decreases(ctx, pkg):
     assert hist["loss"][-1] < 0.5 * hist["loss"][0]
 
 
-def _spec_run(pkg, ctx, monkeypatch, depth, line_search, tol, iters, chunks=1):
+def _spec_run(pkg, ctx, monkeypatch, depth, line_search, tol, iters, chunks=1, fused=True, m=5):
     monkeypatch.setenv("LBF_SPEC_DEPTH", str(depth))
+    monkeypatch.setenv("LBF_FUSED_TAIL", "1" if fused else "0")
     dims, acts = [784, 32, 10], ["relu", "linear"]
     Xh, Yh = pkg.synth_mnist(256)
     net = pkg.Mlp(ctx, dims, acts)
     P = net.init_params(7, "cuda" if line_search == "armijo" else "cpu")
-    run = pkg.LbfgsRun(net, P, dev(Xh), dev(Yh), line_search=line_search, m=5, max_iters=iters, tol=tol)
+    run = pkg.LbfgsRun(net, P, dev(Xh), dev(Yh), line_search=line_search, m=m, max_iters=iters, tol=tol)
     for c in range(chunks):
         run.iterate(iters // chunks)
     info = run.info
@@ -261,23 +262,51 @@ def _spec_run(pkg, ctx, monkeypatch, depth, line_search, tol, iters, chunks=1):
     return h, (info.iterations, info.n_evals, info.final_loss, info.final_grad_norm), host(P)
 
 
+def _same(h, ref, keys=("loss", "grad_norm", "alpha", "ls_trials", "accepted")):
+    return all(np.array_equal(h[k], ref[k]) for k in keys)
+
+
 @pytest.mark.parametrize("line_search", ["wolfe", "armijo"])
 def test_speculative_line_search_is_exact(ctx, pkg, monkeypatch, line_search):
-    """The speculative pipeline (ls_ctl + abort flag, solvers.cpp iterate_spec) reproduces the host-driven
-    loop bit for bit: records, evaluation count, final parameters — across rejections of the first trial,
-    convergence inside the speculation window, and solves split into several iterate() calls."""
+    """Speculation (ls_ctl + abort flag, solvers.cpp iterate_spec) without the fused tail reproduces
+    the host-driven loop bit for bit: records, evaluation count, final parameters — across rejections
+    of the first trial, convergence inside the speculation window, and split iterate() calls."""
     ref, ref_info, ref_P = _spec_run(pkg, ctx, monkeypatch, 0, line_search, 0.0, 40)
     assert np.any(ref["ls_trials"][1:] > 1), "problem must exercise rejected first trials"
     for depth, chunks in [(1, 1), (3, 1), (8, 1), (3, 4)]:
-        h, info, P = _spec_run(pkg, ctx, monkeypatch, depth, line_search, 0.0, 40, chunks)
-        for k in ("loss", "grad_norm", "alpha", "ls_trials", "accepted"):
-            assert np.array_equal(h[k], ref[k]), (depth, chunks, k)
+        h, info, P = _spec_run(pkg, ctx, monkeypatch, depth, line_search, 0.0, 40, chunks, fused=False)
+        assert _same(h, ref), (depth, chunks)
         assert info == ref_info, (depth, info, ref_info)
         assert np.array_equal(P, ref_P)
-    # convergence in the middle of a speculation window
     tol = float(ref["grad_norm"][12]) * (1 + 1e-6)
     ref_c, ref_ci, ref_cP = _spec_run(pkg, ctx, monkeypatch, 0, line_search, tol, 40)
     assert len(ref_c["loss"]) < 40
-    h, info, P = _spec_run(pkg, ctx, monkeypatch, 4, line_search, tol, 40)
+    h, info, P = _spec_run(pkg, ctx, monkeypatch, 4, line_search, tol, 40, fused=False)
     assert info == ref_ci
     assert np.array_equal(h["loss"], ref_c["loss"]) and np.array_equal(P, ref_cP)
+
+
+@pytest.mark.parametrize("line_search", ["wolfe", "armijo"])
+@pytest.mark.parametrize("m", [5, 20])
+def test_fused_tail_matches_host_loop(ctx, pkg, monkeypatch, line_search, m):
+    """Fused optimizer tail (tail.hip): identical at every speculation depth and split of iterate();
+    against the host-driven loop the only difference is the fp64 summation order of the Gram dots, so
+    the line-search decisions are the same and the losses agree to 1e-9 relative."""
+    ref, ref_info, ref_P = _spec_run(pkg, ctx, monkeypatch, 0, line_search, 0.0, 30, m=m)
+    base, base_info, base_P = _spec_run(pkg, ctx, monkeypatch, 1, line_search, 0.0, 30, m=m)
+    for depth, chunks in [(3, 1), (8, 1), (3, 5)]:
+        h, info, P = _spec_run(pkg, ctx, monkeypatch, depth, line_search, 0.0, 30, chunks, m=m)
+        assert _same(h, base), (depth, chunks)
+        assert info == base_info and np.array_equal(P, base_P)
+    assert np.array_equal(base["ls_trials"], ref["ls_trials"])
+    assert np.array_equal(base["accepted"], ref["accepted"])
+    assert base_info[:2] == ref_info[:2]
+    r = np.abs(base["loss"] - ref["loss"]) / np.abs(ref["loss"])
+    assert r.max() <= 1e-9, r
+    assert rel(base_P, ref_P) <= 1e-6
+    # convergence inside the speculation window
+    tol = float(ref["grad_norm"][12]) * (1 + 1e-6)
+    ref_c, ref_ci, _ = _spec_run(pkg, ctx, monkeypatch, 0, line_search, tol, 30, m=m)
+    h, info, _ = _spec_run(pkg, ctx, monkeypatch, 4, line_search, tol, 30, m=m)
+    assert info[:2] == ref_ci[:2]
+    assert np.allclose(h["loss"], ref_c["loss"], rtol=1e-9, atol=0)
