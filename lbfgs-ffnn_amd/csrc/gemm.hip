@@ -13,6 +13,7 @@
 // step s: a k-contiguous operand is then 16 consecutive floats per lane (4 x ds_read_b128) and an
 // mn-contiguous operand is one conflict-free ds_read_b32 per step.
 // Workgroup: 256 threads = 4 waves in a WM x WN grid, each wave TM x TN tiles of 32x32.
+#include "head_core.hpp"
 #include "internal.hpp"
 #include "kernels.hpp"
 
@@ -64,6 +65,13 @@ struct GemmK {
   int side_splits;
   long long side_stride, side_count;
   float *side_dst;
+  const float *head_P;
+  int head_out, head_act;
+  const float *head_Y;
+  const int *head_idx;
+  double head_inv_scale;
+  float *head_delta, *head_slab;
+  double *head_sse;
 };
 
 // Side job (see GemmDesc): one 64-column group x 4 split stripes per block, fp64 in split order.
@@ -165,7 +173,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32, LDK = BK + 4;
   constexpr int ASZ = AKC ? BM * LDK : BK * (BM + 4);
   constexpr int BSZ = BKC ? BN * LDK : BK * (BN + 4);
-  __shared__ __attribute__((aligned(16))) float lds[2 * (ASZ + BSZ)];
+  constexpr int LDS_F = (EPI == EPI_HEAD && headc::smem_floats(BN) > 2 * (ASZ + BSZ)) ? headc::smem_floats(BN)
+                                                                                    : 2 * (ASZ + BSZ);
+  __shared__ __attribute__((aligned(16))) float lds[LDS_F];
   if (g.abort && *g.abort) return;
   if (int(blockIdx.z) < g.side_planes) {
     gemm_side_job(g, reinterpret_cast<double *>(lds));
@@ -271,6 +281,61 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
     }
   }
 
+  if constexpr (EPI == EPI_HEAD) {
+    // Output layer on the tile (head_core.hpp): per 64-row half, the activations go accumulators ->
+    // LDS (bias + activation; columns >= N zero) and the head runs on them. n0 == 0 (N <= BN).
+    __syncthreads(); // main loop done with the LDS
+    const headc::Smem hs = headc::carve(lds, g.N);
+    headc::stage_w(hs, g.head_P, g.head_out);
+    headc::f32x4 cw[headc::QMAX];
+#pragma unroll
+    for (int q = 0; q < headc::QMAX; ++q) cw[q] = (headc::f32x4){0.f, 0.f, 0.f, 0.f};
+    double sse = 0.0;
+    headc::TileArgs ta;
+    ta.Y = g.head_Y;
+    ta.idx = g.head_idx;
+    ta.Out = g.head_out;
+    ta.act_out = g.head_act;
+    ta.act_prev = g.act;
+    ta.sc = float(g.head_inv_scale);
+    ta.delta = g.head_delta;
+    ta.vec = (g.N & 3) == 0 && (reinterpret_cast<uintptr_t>(g.head_delta) & 15) == 0;
+    for (int half = 0; half < (BM + headc::TB - 1) / headc::TB; ++half) {
+      const long long b0 = (long long)m0 + half * headc::TB;
+      const int rows_tile = min(headc::TB, BM - half * headc::TB);
+      const int rows = int(min((long long)rows_tile, (long long)g.M - b0));
+      if (rows <= 0) break;
+      for (int e = threadIdx.x; e < (headc::TB - rows_tile) * hs.Hp; e += 256) { // rows the tile lacks
+        const int r = rows_tile + e / hs.Hp, c = e % hs.Hp;
+        hs.As[r * hs.LDA + c] = 0.0f;
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int local = wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if ((local / headc::TB) == half) {
+              const int col = wn * TN * 32 + tn * 32 + li;
+              if (col < hs.Hp) // the tile may be wider than the head's padded width
+                hs.As[(local % headc::TB) * hs.LDA + col] =
+                    col < g.N ? act_apply(g.act, acc[tm][tn][r] + g.bias[col]) : 0.0f;
+            }
+          }
+      if (hs.Hp > BN)
+        for (int e = threadIdx.x; e < rows_tile * (hs.Hp - BN); e += 256) { // padding beyond the tile width
+          const int r = e / (hs.Hp - BN), c = BN + e % (hs.Hp - BN);
+          hs.As[r * hs.LDA + c] = 0.0f;
+        }
+      __syncthreads();
+      headc::tile(hs, ta, b0, rows, cw, sse);
+    }
+    headc::write_partials(hs, g.head_out, cw, sse, g.head_slab + (long long)blockIdx.y * (g.N + 1) * g.head_out,
+                          g.head_sse + blockIdx.y);
+    return;
+  }
+
   // Epilogue: lanes 0-31 own consecutive columns -> each register row is a 128-B coalesced store.
   float *C = g.C + (EPI == EPI_STORE ? (long long)zsplit * g.slab_stride : 0LL);
 #pragma unroll
@@ -331,6 +396,15 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.side_stride = d.side_stride;
   k.side_count = d.side_count;
   k.side_dst = d.side_dst;
+  k.head_P = d.head_P;
+  k.head_out = d.head_out;
+  k.head_act = d.head_act;
+  k.head_Y = d.head_Y;
+  k.head_idx = d.head_idx;
+  k.head_inv_scale = d.head_inv_scale;
+  k.head_delta = d.head_delta;
+  k.head_slab = d.head_slab;
+  k.head_sse = d.head_sse;
   dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
   if (d.a_idx)
     hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true>), grid, dim3(256), 0, s, k);
@@ -339,21 +413,41 @@ void launch(hipStream_t s, const GemmDesc &d) {
 }
 
 template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const GemmDesc &d) {
-  if (d.N > 64) launch<2, 2, 2, 2, AKC, BKC, EPI>(s, d);       // 128 x 128
+  if (d.tile == TILE_32x128) launch<1, 4, 1, 1, AKC, BKC, EPI>(s, d);     // 32 x 128
+  else if (d.tile == TILE_64x64) launch<2, 2, 1, 1, AKC, BKC, EPI>(s, d); // 64 x 64
+  else if (d.N > 64) launch<2, 2, 2, 2, AKC, BKC, EPI>(s, d);            // 128 x 128
   else if (d.N > 32) launch<2, 2, 2, 1, AKC, BKC, EPI>(s, d);  // 128 x 64
   else launch<4, 1, 1, 1, AKC, BKC, EPI>(s, d);                // 128 x 32
 }
 
 } // namespace
 
-void gemm_tile_for(int N, int *BM, int *BN) {
+void gemm_tile_for(int N, int tile, int *BM, int *BN) {
+  if (tile == TILE_32x128) {
+    *BM = 32;
+    *BN = 128;
+    return;
+  }
+  if (tile == TILE_64x64) {
+    *BM = 64;
+    *BN = 64;
+    return;
+  }
   *BM = 128;
   *BN = N > 64 ? 128 : (N > 32 ? 64 : 32);
 }
 
+int gemm_row_tiles(int M, int tile) { return tile == TILE_32x128 ? (M + 31) / 32 : (M + 127) / 128; }
+
 void gemm(hipStream_t s, const GemmDesc &d) {
   if (d.M <= 0 || d.N <= 0) return;
-  if (d.epi == EPI_FWD && d.a_kc && !d.b_kc) dispatch_tile<true, false, EPI_FWD>(s, d);
+  if (d.epi == EPI_HEAD) {
+    int BM, BN;
+    gemm_tile_for(d.N, d.tile, &BM, &BN);
+    if (!(d.a_kc && !d.b_kc) || d.N > BN || d.splits > 1 || d.head_out < 1 || d.head_out > headc::HMAX_OUT)
+      throw std::runtime_error("gemm: EPI_HEAD needs an unsplit forward GEMM with N <= the tile width");
+    dispatch_tile<true, false, EPI_HEAD>(s, d);
+  } else if (d.epi == EPI_FWD && d.a_kc && !d.b_kc) dispatch_tile<true, false, EPI_FWD>(s, d);
   else if (d.epi == EPI_DX && d.a_kc && d.b_kc) dispatch_tile<true, true, EPI_DX>(s, d);
   else if (d.epi == EPI_STORE && !d.a_kc && !d.b_kc) dispatch_tile<false, false, EPI_STORE>(s, d);
   else if (d.epi == EPI_STORE && d.a_kc && !d.b_kc) dispatch_tile<true, false, EPI_STORE>(s, d);

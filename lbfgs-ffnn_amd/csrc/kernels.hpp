@@ -21,7 +21,10 @@ enum Act : int { ACT_LINEAR = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_SIGMOID = 3 };
 //            DX    C = acc * act'(aux[m*ldaux + n])       (act' from the post-activation value)
 //            STORE C(+ split*slab_stride) = acc           (split-K partial slabs)
 // ------------------------------------------------------------------------------------------------
-enum GemmEpi : int { EPI_FWD = 0, EPI_DX = 1, EPI_STORE = 2 };
+// Tile shapes: TILE_AUTO = 128 rows x (128 | 64 | 32 by N); TILE_32x128 (few row tiles: a rank's
+// shard); TILE_64x64 (split-K weight gradients with fewer, longer splits).
+enum GemmTile : int { TILE_AUTO = 0, TILE_32x128 = 1, TILE_64x64 = 2 };
+enum GemmEpi : int { EPI_FWD = 0, EPI_DX = 1, EPI_STORE = 2, EPI_HEAD = 3 };
 
 struct GemmDesc {
   int M = 0, N = 0, K = 0;
@@ -37,6 +40,7 @@ struct GemmDesc {
   long long ldc = 0, slab_stride = 0;
   int splits = 1, k_chunk = 0;
   int epi = EPI_FWD;
+  int tile = TILE_AUTO;
   const float *bias = nullptr;
   int act = ACT_LINEAR;
   const float *aux = nullptr;
@@ -50,11 +54,22 @@ struct GemmDesc {
   int side_splits = 0;
   long long side_stride = 0, side_count = 0;
   float *side_dst = nullptr;
+  // EPI_HEAD (forward GEMM of the last hidden layer, N <= the tile width): bias + activation, then the
+  // output layer on each 64-row half in LDS (head_core.hpp) instead of storing the activations.
+  const float *head_P = nullptr; // [W ; b] of the output layer
+  int head_out = 0, head_act = ACT_LINEAR;
+  const float *head_Y = nullptr;
+  const int *head_idx = nullptr; // minibatch rows of Y (nullable)
+  double head_inv_scale = 1.0;
+  float *head_delta = nullptr, *head_slab = nullptr; // slab per workgroup: [(N+1) x head_out]
+  double *head_sse = nullptr;                        // SSE partial per workgroup
 };
+// Row tiles of the forward GEMM for M rows and N columns (== EPI_HEAD partial slabs).
+int gemm_row_tiles(int M, int tile);
 
 void gemm(hipStream_t s, const GemmDesc &d);
 // Tile (BM, BN) the dispatcher picks for a given N (used by the split-K planner).
-void gemm_tile_for(int N, int *BM, int *BN);
+void gemm_tile_for(int N, int tile, int *BM, int *BN);
 
 // ------------------------------------------------------------------------------------------------
 // Vector / reduction kernels (vec_kernels.hip). All reductions are deterministic: per-workgroup

@@ -74,6 +74,10 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
   nparams_ = off;
   const char *nh = std::getenv("LBF_NO_HEAD");
   use_head_ = !(nh && nh[0] == '1');
+  const char *ng = std::getenv("LBF_NO_GEMM_HEAD");
+  use_gemm_head_ = !(ng && ng[0] == '1');
+  if (const char *e = std::getenv("LBF_FWD_TILE32")) fwd_small_ = e[0] != '0';
+  if (const char *e = std::getenv("LBF_DW_TILE64")) dw64_ = e[0] != '0';
 }
 
 // Split-K plan of every dW GEMM for batch B: aim for ~512 workgroups (2 per CU) per GEMM, k chunks
@@ -83,10 +87,14 @@ void Mlp::plan(long long B) {
   size_t slab = 0, fslab = 0;
   for (auto &L : layers_) {
     int BM, BN;
-    gemm_tile_for(L.out, &BM, &BN);
     const long long M = L.in + 1;
+    // dW: 64x64 tiles over narrow outputs -> fewer, longer K splits (a third of the slab traffic)
+    // (only for short K: at long K the 128x128 tile's reuse wins over the slab savings)
+    L.dtile = (dw64_ && L.out <= 128 && M <= 1024 && B <= 16384) ? TILE_64x64 : TILE_AUTO;
+    gemm_tile_for(L.out, L.dtile, &BM, &BN);
     const long long tiles = cdiv(M, BM) * cdiv(L.out, BN);
-    long long splits = std::max(1LL, std::min(cdiv(512, tiles), cdiv(B, 128)));
+    const long long min_chunk = L.dtile == TILE_64x64 ? 256 : 128;
+    long long splits = std::max(1LL, std::min(cdiv(512, tiles), cdiv(B, min_chunk)));
     long long kc = cdiv(cdiv(B, splits), 32) * 32;
     if (kc <= 0) kc = 32;
     splits = std::max(1LL, cdiv(B, kc));
@@ -96,10 +104,15 @@ void Mlp::plan(long long B) {
     if (splits > 1) slab += size_t(splits) * size_t(M) * L.out; // every layer keeps its own slabs until reduce_all
     // forward GEMM: with fewer row tiles than CUs (a data-parallel rank's shard), split K so the chip
     // fills; the partial slabs are summed in split order with the bias and activation afterwards
-    const long long ftiles = cdiv(B, 128) * cdiv(L.out, BN);
+    int fBM, fBN;
+    gemm_tile_for(L.out, TILE_AUTO, &fBM, &fBN);
+    const long long ftiles = cdiv(B, 128) * cdiv(L.out, fBN);
     L.fsplits = 1;
     L.fk_chunk = L.in;
-    if (ftiles < 192 && L.in >= 256) {
+    L.ftile = TILE_AUTO;
+    if (fwd_small_ && L.out <= 128 && cdiv(B, 128) < 256) {
+      L.ftile = TILE_32x128; // four times the row tiles, full rows (the head can still fuse), no split
+    } else if (ftiles < 192 && L.in >= 256) {
       long long fs = std::min(cdiv(384, ftiles), (long long)L.in / 128);
       long long fkc = cdiv(cdiv(L.in, fs), 32) * 32;
       fs = cdiv(L.in, fkc);
@@ -130,7 +143,8 @@ void Mlp::ensure(long long B) {
   const Layer &Lo = layers_[nl - 1];
   size_t nloss = size_t(loss_partials_wg(std::max(1LL, B), Lo.out));
   if (nl >= 2 && head_supported(Lo.in, Lo.out)) {
-    const size_t hw = size_t(head_nwg(B, Lo.in));
+    const size_t hw =
+        size_t(std::max(head_nwg(B, Lo.in), gemm_row_tiles(int(std::max(1LL, B)), layers_[nl - 2].ftile)));
     nloss = std::max(nloss, hw);
     head_slab_.ensure(hw * size_t(Lo.in + 1) * Lo.out);
   }
@@ -151,6 +165,29 @@ bool Mlp::side_reduced(int l, bool fused, int nloss) const {
   return layers_[l].splits > 2 * RA_SPLITS_PER_PART;
 }
 
+GemmDesc Mlp::fwd_desc(size_t l, const float *P, const float *in, const int *idx, long long B) const {
+  const Layer &L = layers_[l];
+  GemmDesc d;
+  d.M = int(B);
+  d.N = L.out;
+  d.K = L.in;
+  d.A = in;
+  d.lda = L.in;
+  d.a_kc = true;
+  d.a_idx = (l == 0) ? idx : nullptr;
+  d.B = P + L.off; // W as [In][Out] row-major (column-major Out x In)
+  d.ldb = L.out;
+  d.b_kc = false;
+  d.C = A_[l].get();
+  d.ldc = L.out;
+  d.epi = EPI_FWD;
+  d.bias = P + L.off + size_t(L.in) * L.out;
+  d.act = L.act;
+  d.abort = ctx_->abort;
+  d.tile = L.ftile;
+  return d;
+}
+
 const float *Mlp::forward(const float *P, const float *X, const int *idx, long long B, int nrun) {
   ensure(B);
   hipStream_t s = ctx_->stream;
@@ -158,23 +195,7 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
   const size_t nr = nrun < 0 ? layers_.size() : size_t(nrun);
   for (size_t l = 0; l < nr; ++l) {
     const Layer &L = layers_[l];
-    GemmDesc d;
-    d.M = int(B);
-    d.N = L.out;
-    d.K = L.in;
-    d.A = in;
-    d.lda = L.in;
-    d.a_kc = true;
-    d.a_idx = (l == 0) ? idx : nullptr;
-    d.B = P + L.off; // W as [In][Out] row-major (column-major Out x In)
-    d.ldb = L.out;
-    d.b_kc = false;
-    d.C = A_[l].get();
-    d.ldc = L.out;
-    d.epi = EPI_FWD;
-    d.bias = P + L.off + size_t(L.in) * L.out;
-    d.act = L.act;
-    d.abort = ctx_->abort;
+    GemmDesc d = fwd_desc(l, P, in, idx, B);
     if (L.fsplits > 1) {
       d.epi = EPI_STORE;
       d.C = fslab_.get();
@@ -199,9 +220,30 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
   const int nl = int(layers_.size());
   const Layer &Lo = layers_[nl - 1];
   const bool fused = use_head_ && nl >= 2 && head_supported(Lo.in, Lo.out);
-  forward(P, X, idx, B, fused ? nl - 1 : nl);
+  ensure(B);
+  // the output layer inside the last hidden layer's forward GEMM (EPI_HEAD), when that GEMM is one
+  // unsplit tile column: its activations then never reach HBM
+  const bool gemm_head = fused && use_gemm_head_ && layers_[nl - 2].fsplits == 1 && Lo.in <= 128;
+  forward(P, X, idx, B, fused ? (gemm_head ? nl - 2 : nl - 1) : nl);
   int nloss, lstart;
-  if (fused) {
+  if (gemm_head) {
+    nloss = gemm_row_tiles(int(B), layers_[nl - 2].ftile);
+    GemmDesc d = fwd_desc(size_t(nl - 2), P, nl >= 3 ? A_[nl - 3].get() : X, idx, B);
+    d.epi = EPI_HEAD;
+    d.C = nullptr;
+    d.head_P = P + Lo.off;
+    d.head_out = Lo.out;
+    d.head_act = Lo.act;
+    d.head_Y = Y;
+    d.head_idx = idx;
+    d.head_inv_scale = inv_scale;
+    d.head_delta = D_[nl - 2].get();
+    d.head_slab = head_slab_.get();
+    d.head_sse = loss_part_.get();
+    ProfScope ps(ctx_, PK_FWD, nl - 2);
+    gemm(s, d);
+    lstart = nl - 2;
+  } else if (fused) {
     // last layer: forward + loss + dZ + delta + [dW ; db] partials in one kernel (head.hip)
     nloss = head_nwg(B, Lo.in);
     {
@@ -239,6 +281,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     d.splits = L.splits;
     d.k_chunk = L.k_chunk;
     d.abort = ctx_->abort;
+    d.tile = L.dtile;
     if (l + 1 < nl && side_reduced(l + 1, fused, nloss)) {
       // finish layer l+1's [dW ; db] slabs (the fused head's, or many split-K slabs) in side blocks
       // of this launch, while its GEMM runs

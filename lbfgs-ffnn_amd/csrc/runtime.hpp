@@ -70,6 +70,8 @@ struct Layer {
   size_t slab_off = 0; // this layer's partial slabs inside the shared slab buffer
   int fsplits = 1;     // split-K factor of the forward GEMM (few row tiles: small per-rank batches)
   int fk_chunk = 0;
+  int ftile = 0;       // forward GEMM tile (GemmTile)
+  int dtile = 0;       // dW GEMM tile (GemmTile)
 };
 
 // RAII section: records an event pair around the enclosed launches when profiling is on.
@@ -109,13 +111,17 @@ public:
 private:
   void ensure(long long B);
   bool side_reduced(int l, bool fused, int nloss) const;
+  GemmDesc fwd_desc(size_t l, const float *P, const float *in, const int *idx, long long B) const;
   Ctx *ctx_;
   std::vector<Layer> layers_;
   size_t nparams_ = 0;
   long long cap_ = -1, planned_ = -1;
   std::vector<DevBuf<float>> A_, D_;
   DevBuf<float> slab_, head_slab_, fslab_;
-  bool use_head_ = true; // fused output layer when the shape allows (LBF_NO_HEAD=1 disables)
+  bool use_head_ = true;      // fused output layer when the shape allows (LBF_NO_HEAD=1 disables)
+  bool use_gemm_head_ = true; // ... inside the forward GEMM's epilogue (LBF_NO_GEMM_HEAD=1 disables)
+  int fwd_small_ = 1;         // 32x128 forward tiles for few row tiles (LBF_FWD_TILE32=0 disables)
+  int dw64_ = 1;              // 64x64 dW tiles with fewer splits (LBF_DW_TILE64=0 disables)
   DevBuf<double> loss_part_, dots_part_, sse_, colpart_, trows_, tdots_;
   long long evals_ = 0;
   void plan(long long B);
