@@ -13,35 +13,19 @@
 // step s: a k-contiguous operand is then 16 consecutive floats per lane (4 x ds_read_b128) and an
 // mn-contiguous operand is one conflict-free ds_read_b32 per step.
 // Workgroup: 256 threads = 4 waves in a WM x WN grid, each wave TM x TN tiles of 32x32.
+#include "act.hpp"
 #include "head_core.hpp"
 #include "internal.hpp"
 #include "kernels.hpp"
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 namespace lbf {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ float act_apply(int a, float x) {
-  switch (a) {
-  case ACT_TANH: return tanhf(x);
-  case ACT_RELU: return x > 0.0f ? x : 0.0f;
-  case ACT_SIGMOID: return 1.0f / (1.0f + expf(-x));
-  default: return x;
-  }
-}
-// Derivative expressed through the post-activation value y (src/cuda/kernels.cuh:109-133); equal to
-// the CPU path's act'(Z) (src/layer.hpp:16-47) in exact arithmetic.
-__device__ __forceinline__ float act_deriv_out(int a, float y) {
-  switch (a) {
-  case ACT_TANH: return 1.0f - y * y;
-  case ACT_RELU: return y > 0.0f ? 1.0f : 0.0f;
-  case ACT_SIGMOID: return y * (1.0f - y);
-  default: return 1.0f;
-  }
-}
 
 struct GemmK {
   int M, N, K, k_chunk;
@@ -76,13 +60,13 @@ struct GemmK {
 
 // Side job (see GemmDesc): one 64-column group x 4 split stripes per block, fp64 in split order.
 __device__ __forceinline__ void gemm_side_job(const GemmK &g, double *red) {
-  const int t = threadIdx.x, lane = t & 63, stripe = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, stripe = t >> 6; // stripes 0-3 (extra waves idle)
   const int nside = gridDim.x * gridDim.y * g.side_planes;
   const int id = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
   for (long long c0 = (long long)id * 64; c0 < g.side_count; c0 += (long long)nside * 64) {
     const long long c = c0 + lane;
     double acc = 0.0;
-    if (c < g.side_count) {
+    if (c < g.side_count && stripe < 4) {
       const float *src = g.side_slab + c;
       int k = stripe;
       for (; k + 28 < g.side_splits; k += 32) { // eight independent loads in flight
@@ -94,7 +78,7 @@ __device__ __forceinline__ void gemm_side_job(const GemmK &g, double *red) {
       }
       for (; k < g.side_splits; k += 4) acc += double(src[(long long)k * g.side_stride]);
     }
-    red[t] = acc;
+    if (stripe < 4) red[t] = acc;
     __syncthreads();
     if (stripe == 0 && c < g.side_count) g.side_dst[c] = float(((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane]);
     __syncthreads();
@@ -104,10 +88,10 @@ __device__ __forceinline__ void gemm_side_job(const GemmK &g, double *red) {
 // k-contiguous operand: R rows x 32 k. Thread chunk c -> row c>>3, k-quad c&7.
 template <int R, bool GATHER>
 __device__ __forceinline__ void load_kc(f32x4 (&r)[R / 32], const float *base, long long ld, const int *idx,
-                                        int row0, int rows, int k0, int kend, int vec) {
+                                        int row0, int rows, int k0, int kend, int vec, int tid) {
 #pragma unroll
   for (int i = 0; i < R / 32; ++i) {
-    const int c = threadIdx.x + i * 256;
+    const int c = tid + i * 256;
     const int row = row0 + (c >> 3);
     const int k = k0 + (c & 7) * 4;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -125,23 +109,91 @@ __device__ __forceinline__ void load_kc(f32x4 (&r)[R / 32], const float *base, l
   }
 }
 template <int R>
-__device__ __forceinline__ void store_kc(float *lds, const f32x4 (&r)[R / 32]) {
+__device__ __forceinline__ void store_kc(float *lds, const f32x4 (&r)[R / 32], int tid) {
   constexpr int LDK = 36;
 #pragma unroll
   for (int i = 0; i < R / 32; ++i) {
-    const int c = threadIdx.x + i * 256;
+    const int c = tid + i * 256;
     *reinterpret_cast<f32x4 *>(lds + (c >> 3) * LDK + (c & 7) * 4) = r[i];
+  }
+}
+
+// FAST variants (K % 4 == 0, 16-B aligned rows, cvalid % 4 == 0): every load is issued
+// unconditionally from a clamped address and its value is always consumed; validity is applied when
+// the tile is written to LDS (integer AND, plus the appended ones column). No divergent branches and
+// no use right after the load, so the compiler counts outstanding loads (s_waitcnt vmcnt(N)) and the
+// prefetched k-tiles stay in flight.
+__device__ __forceinline__ f32x4 mask4(const f32x4 v, bool ok) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const unsigned m = ok ? 0xffffffffu : 0u;
+  const u32x4 b = __builtin_bit_cast(u32x4, v) & (u32x4){m, m, m, m};
+  return __builtin_bit_cast(f32x4, b);
+}
+template <int R, bool GATHER>
+__device__ __forceinline__ void load_kc_fast(f32x4 (&r)[R / 32], const float *base, long long ld, const int *idx,
+                                             int row0, int rows, int k0, int kend, int tid) {
+#pragma unroll
+  for (int i = 0; i < R / 32; ++i) {
+    const int c = tid + i * 256;
+    const int row = row0 + (c >> 3);
+    const int k = k0 + (c & 7) * 4;
+    const bool ok = row < rows && k < kend;
+    const int rr = ok ? row : 0; // row 0, column 0: always a valid address
+    const long long grow = GATHER ? (long long)idx[rr] : (long long)rr;
+    r[i] = *reinterpret_cast<const f32x4 *>(base + grow * ld + (ok ? k : 0));
+  }
+}
+template <int R>
+__device__ __forceinline__ void store_kc_fast(float *lds, const f32x4 (&r)[R / 32], int row0, int rows, int k0,
+                                              int kend, int tid) {
+  constexpr int LDK = 36;
+#pragma unroll
+  for (int i = 0; i < R / 32; ++i) {
+    const int c = tid + i * 256;
+    const bool ok = row0 + (c >> 3) < rows && k0 + (c & 7) * 4 < kend;
+    *reinterpret_cast<f32x4 *>(lds + (c >> 3) * LDK + (c & 7) * 4) = mask4(r[i], ok);
+  }
+}
+template <int R, bool GATHER>
+__device__ __forceinline__ void load_mc_fast(f32x4 (&r)[R / 32], const float *base, long long ld, const int *idx,
+                                             int col0, int cvalid, int k0, int kend, int tid) {
+  constexpr int Q = R / 4;
+#pragma unroll
+  for (int i = 0; i < R / 32; ++i) {
+    const int c = tid + i * 256;
+    const int k = k0 + c / Q;
+    const int col = col0 + (c % Q) * 4;
+    const bool ok = k < kend && col < cvalid;
+    const int kk = ok ? k : 0; // row 0, column 0: always a valid address
+    const long long grow = GATHER ? (long long)idx[kk] : (long long)kk;
+    r[i] = *reinterpret_cast<const f32x4 *>(base + grow * ld + (ok ? col : 0));
+  }
+}
+template <int R>
+__device__ __forceinline__ void store_mc_fast(float *lds, const f32x4 (&r)[R / 32], int col0, int cvalid, int ones,
+                                              int k0, int kend, int tid) {
+  constexpr int Q = R / 4, LD = R + 4;
+#pragma unroll
+  for (int i = 0; i < R / 32; ++i) {
+    const int c = tid + i * 256;
+    const int k = k0 + c / Q;
+    const int col = col0 + (c % Q) * 4;
+    f32x4 v = mask4(r[i], k < kend && col < cvalid);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (k < kend && col + j == ones) v[j] = 1.0f; // appended ones column (bias row of [dW ; db])
+    *reinterpret_cast<f32x4 *>(lds + (c / Q) * LD + (c % Q) * 4) = v;
   }
 }
 
 // mn-contiguous operand: 32 k-rows x R columns. Thread chunk c -> k-row c/(R/4), column quad c%(R/4).
 template <int R, bool GATHER>
 __device__ __forceinline__ void load_mc(f32x4 (&r)[R / 32], const float *base, long long ld, const int *idx,
-                                        int col0, int cvalid, int ones, int k0, int kend, int vec) {
+                                        int col0, int cvalid, int ones, int k0, int kend, int vec, int tid) {
   constexpr int Q = R / 4;
 #pragma unroll
   for (int i = 0; i < R / 32; ++i) {
-    const int c = threadIdx.x + i * 256;
+    const int c = tid + i * 256;
     const int k = k0 + c / Q;
     const int col = col0 + (c % Q) * 4;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -159,22 +211,27 @@ __device__ __forceinline__ void load_mc(f32x4 (&r)[R / 32], const float *base, l
   }
 }
 template <int R>
-__device__ __forceinline__ void store_mc(float *lds, const f32x4 (&r)[R / 32]) {
+__device__ __forceinline__ void store_mc(float *lds, const f32x4 (&r)[R / 32], int tid) {
   constexpr int Q = R / 4, LD = R + 4;
 #pragma unroll
   for (int i = 0; i < R / 32; ++i) {
-    const int c = threadIdx.x + i * 256;
+    const int c = tid + i * 256;
     *reinterpret_cast<f32x4 *>(lds + (c / Q) * LD + (c % Q) * 4) = r[i];
   }
 }
 
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
+// KW k-groups of 4 waves each (KW = 2: 8 waves, two per SIMD, for tiles too small to fill the chip
+// with one wave per SIMD): group q runs k-steps [16q/KW, 16(q+1)/KW) of every 32-deep tile on the
+// same output sub-tile, and the groups' accumulators are summed through LDS in group order.
+// PF: k-tiles whose global loads are in flight (register sets rotated in a PF-unrolled loop), so a
+// load has PF compute phases to land instead of one.
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int KW, int PF, bool FAST>
+__global__ __launch_bounds__(256 * KW, 2) void gemm_kernel(const GemmK g) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32, LDK = BK + 4;
   constexpr int ASZ = AKC ? BM * LDK : BK * (BM + 4);
   constexpr int BSZ = BKC ? BN * LDK : BK * (BN + 4);
-  constexpr int LDS_F = (EPI == EPI_HEAD && headc::smem_floats(BN) > 2 * (ASZ + BSZ)) ? headc::smem_floats(BN)
-                                                                                    : 2 * (ASZ + BSZ);
+  constexpr int HEAD_F = headc::smem_floats_epi(BN, BM);
+  constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > 2 * (ASZ + BSZ)) ? HEAD_F : 2 * (ASZ + BSZ);
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
   if (g.abort && *g.abort) return;
   if (int(blockIdx.z) < g.side_planes) {
@@ -183,7 +240,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
   }
   const int zsplit = int(blockIdx.z) - g.side_planes;
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3, kgrp = KW > 1 ? int(threadIdx.x >> 8) : 0;
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 31, lh = lane >> 5;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
@@ -198,20 +255,53 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 
-  f32x4 ra[BM / 32], rb[BN / 32];
-  auto gload = [&](int k0) {
-    if constexpr (AKC) load_kc<BM, GATHER>(ra, g.A, g.lda, g.a_idx, m0, g.M, k0, ke, g.a_vec);
-    else load_mc<BM, GATHER>(ra, g.A, g.lda, g.a_idx, m0, g.a_mvalid, g.a_ones, k0, ke, g.a_vec);
-    if constexpr (BKC) load_kc<BN, false>(rb, g.B, g.ldb, nullptr, n0, g.N, k0, ke, g.b_vec);
-    else load_mc<BN, false>(rb, g.B, g.ldb, nullptr, n0, g.N, -1, k0, ke, g.b_vec);
+  // staging: 256 threads per operand; with two k-groups, group 0 stages A and group 1 stages B
+  const int tid = threadIdx.x & 255;
+  const bool stage_a = KW == 1 || kgrp == 0, stage_b = KW == 1 || kgrp == 1;
+  f32x4 ra[PF][BM / 32], rb[PF][BN / 32];
+  auto gload = [&](auto &sa, auto &sb, int k0) {
+    if constexpr (FAST) {
+      if (stage_a) {
+        if constexpr (AKC) load_kc_fast<BM, GATHER>(sa, g.A, g.lda, g.a_idx, m0, g.M, k0, ke, tid);
+        else load_mc_fast<BM, GATHER>(sa, g.A, g.lda, g.a_idx, m0, g.a_mvalid, k0, ke, tid);
+      }
+      if (stage_b) {
+        if constexpr (BKC) load_kc_fast<BN, false>(sb, g.B, g.ldb, nullptr, n0, g.N, k0, ke, tid);
+        else load_mc_fast<BN, false>(sb, g.B, g.ldb, nullptr, n0, g.N, k0, ke, tid);
+      }
+    } else {
+      if (stage_a) {
+        if constexpr (AKC) load_kc<BM, GATHER>(sa, g.A, g.lda, g.a_idx, m0, g.M, k0, ke, g.a_vec, tid);
+        else load_mc<BM, GATHER>(sa, g.A, g.lda, g.a_idx, m0, g.a_mvalid, g.a_ones, k0, ke, g.a_vec, tid);
+      }
+      if (stage_b) {
+        if constexpr (BKC) load_kc<BN, false>(sb, g.B, g.ldb, nullptr, n0, g.N, k0, ke, g.b_vec, tid);
+        else load_mc<BN, false>(sb, g.B, g.ldb, nullptr, n0, g.N, -1, k0, ke, g.b_vec, tid);
+      }
+    }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](const auto &sa, const auto &sb, int buf, int k0) {
     float *As = lds + buf * (ASZ + BSZ);
     float *Bs = As + ASZ;
-    if constexpr (AKC) store_kc<BM>(As, ra);
-    else store_mc<BM>(As, ra);
-    if constexpr (BKC) store_kc<BN>(Bs, rb);
-    else store_mc<BN>(Bs, rb);
+    if constexpr (FAST) {
+      if (stage_a) {
+        if constexpr (AKC) store_kc_fast<BM>(As, sa, m0, g.M, k0, ke, tid);
+        else store_mc_fast<BM>(As, sa, m0, g.a_mvalid, g.a_ones, k0, ke, tid);
+      }
+      if (stage_b) {
+        if constexpr (BKC) store_kc_fast<BN>(Bs, sb, n0, g.N, k0, ke, tid);
+        else store_mc_fast<BN>(Bs, sb, n0, g.N, -1, k0, ke, tid);
+      }
+      return;
+    }
+    if (stage_a) {
+      if constexpr (AKC) store_kc<BM>(As, sa, tid);
+      else store_mc<BM>(As, sa, tid);
+    }
+    if (stage_b) {
+      if constexpr (BKC) store_kc<BN>(Bs, sb, tid);
+      else store_mc<BN>(Bs, sb, tid);
+    }
   };
   auto compute = [&](int buf) {
     const float *As = lds + buf * (ASZ + BSZ);
@@ -247,6 +337,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
     }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
+      if (KW > 1 && s / (16 / KW) != kgrp) continue; // this k-group's steps only
       float av[TM], bv[TN];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
@@ -266,30 +357,80 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
     }
   };
 
+  if (EPI == EPI_HEAD) KT(0);
+  if (EPI == EPI_HEAD) KTB(0);
+  // EPI_HEAD: the head's HBM inputs (W, biases, targets) are loaded while the last k-tile computes
+  headc::EpiPrefetch<BN, BM, 256 * KW> hpre;
   if (kb < ke) {
-    gload(kb);
-    sstore(0);
+    const int nk = (ke - kb + BK - 1) / BK;
+    const int nloop = EPI == EPI_HEAD ? nk - 1 : nk; // EPI_HEAD peels the last k-tile
+    // register set p holds k-tile i with i % PF == p; LDS buffer i & 1 holds k-tile i while computed
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+      if (p < nk) gload(ra[p], rb[p], kb + p * BK);
+    sstore(ra[0], rb[0], 0, kb);
     __syncthreads();
-    int buf = 0;
-    for (int k0 = kb; k0 < ke; k0 += BK) {
-      const bool more = k0 + BK < ke;
-      if (more) gload(k0 + BK);
-      compute(buf);
-      if (more) sstore(buf ^ 1);
-      __syncthreads();
-      buf ^= 1;
+    for (int i0 = 0; i0 < nloop; i0 += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int i = i0 + u;
+        if (i >= nloop) break;
+        if (PF > 1 && i + PF < nk) gload(ra[u], rb[u], kb + (i + PF) * BK); // set u's tile i is in LDS
+        if (PF == 1 && i + 1 < nk) gload(ra[0], rb[0], kb + (i + 1) * BK);
+        compute(i & 1);
+        if (i + 1 < nk) sstore(ra[(u + 1) % PF], rb[(u + 1) % PF], (i + 1) & 1, kb + (i + 1) * BK);
+        __syncthreads();
+        if (EPI == EPI_HEAD && i < 24) KT(1 + i);
+      }
     }
+    if constexpr (EPI == EPI_HEAD) {
+      hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
+      compute((nk - 1) & 1);
+      __syncthreads();
+      KT(25);
+    }
+  } else if constexpr (EPI == EPI_HEAD) {
+    hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
+  }
+  if constexpr (KW > 1) { // group sums through LDS, in group order (group 0 keeps the result)
+    float *red = lds;
+    constexpr int PER = TM * TN * 16;
+    for (int q = 1; q < KW; ++q) {
+      if (kgrp == q) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[((a * TN + b) * 16 + r) * 256 + (threadIdx.x & 255)] = acc[a][b][r];
+      }
+      __syncthreads();
+      if (kgrp == 0) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] += red[((a * TN + b) * 16 + r) * 256 + threadIdx.x];
+      }
+      __syncthreads();
+    }
+    static_assert(PER * 256 <= LDS_F, "k-group reduction buffer");
   }
 
   if constexpr (EPI == EPI_HEAD) {
-    // Output layer on the tile (head_core.hpp): per 64-row half, the activations go accumulators ->
-    // LDS (bias + activation; columns >= N zero) and the head runs on them. n0 == 0 (N <= BN).
-    __syncthreads(); // main loop done with the LDS
+    KTB(1);
+    // Output layer on the tile (head_core.hpp): the prefetched W / biases / targets go to LDS, then per
+    // 64-row half the activations go accumulators -> LDS (bias + activation; columns >= N zero) and
+    // the head runs on them. n0 == 0 (N <= BN).
+    constexpr int QM = headc::qstrips(BN);
     const headc::Smem hs = headc::carve(lds, g.N);
-    headc::stage_w(hs, g.head_P, g.head_out);
-    headc::f32x4 cw[headc::QMAX];
+    hpre.store(hs);
+    KT(26);
+    KTB(2);
+    headc::f32x4 cw[QM];
 #pragma unroll
-    for (int q = 0; q < headc::QMAX; ++q) cw[q] = (headc::f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < QM; ++q) cw[q] = (headc::f32x4){0.f, 0.f, 0.f, 0.f};
     double sse = 0.0;
     headc::TileArgs ta;
     ta.Y = g.head_Y;
@@ -305,66 +446,89 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const GemmK g) {
       const int rows_tile = min(headc::TB, BM - half * headc::TB);
       const int rows = int(min((long long)rows_tile, (long long)g.M - b0));
       if (rows <= 0) break;
-      for (int e = threadIdx.x; e < (headc::TB - rows_tile) * hs.Hp; e += 256) { // rows the tile lacks
+      ta.ys = hs.ys + half * headc::TB * 16;
+      if (half == 0) __syncthreads(); // hb (read below) written by hpre.store
+      for (int e = threadIdx.x; e < (headc::TB - rows_tile) * hs.Hp; e += 256 * KW) { // rows the tile lacks
         const int r = rows_tile + e / hs.Hp, c = e % hs.Hp;
         hs.As[r * hs.LDA + c] = 0.0f;
       }
+      with_act(g.act, [&](auto AC) __attribute__((always_inline)) {
+        constexpr int A = decltype(AC)::value;
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
+        for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
+          for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * TN * 32 + tn * 32 + li;
+            const int local0 = wm * TM * 32 + tm * 32;
+            if (kgrp == 0 && local0 / headc::TB == half && col < hs.Hp) { // the tile may be wider than Hp
+              const float bn = hs.hb[col];
+              const bool in = col < g.N;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int local = wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if ((local / headc::TB) == half) {
-              const int col = wn * TN * 32 + tn * 32 + li;
-              if (col < hs.Hp) // the tile may be wider than the head's padded width
-                hs.As[(local % headc::TB) * hs.LDA + col] =
-                    col < g.N ? act_apply(g.act, acc[tm][tn][r] + g.bias[col]) : 0.0f;
+              for (int r = 0; r < 16; ++r) {
+                const int local = local0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                hs.As[(local % headc::TB) * hs.LDA + col] = in ? act_c<A>(acc[tm][tn][r] + bn) : 0.0f;
+              }
             }
           }
+      });
       if (hs.Hp > BN)
-        for (int e = threadIdx.x; e < rows_tile * (hs.Hp - BN); e += 256) { // padding beyond the tile width
+        for (int e = threadIdx.x; e < rows_tile * (hs.Hp - BN); e += 256 * KW) { // padding beyond the tile width
           const int r = e / (hs.Hp - BN), c = BN + e % (hs.Hp - BN);
           hs.As[r * hs.LDA + c] = 0.0f;
         }
       __syncthreads();
-      headc::tile(hs, ta, b0, rows, cw, sse);
+      KT(28 + 2 * half);
+      KTB(3 + 2 * half);
+      headc::tile<(KW > 1), QM>(hs, ta, b0, rows, cw, sse);
+      KT(29 + 2 * half);
+      KTB(4 + 2 * half);
     }
+    KT(32);
     headc::write_partials(hs, g.head_out, cw, sse, g.head_slab + (long long)blockIdx.y * (g.N + 1) * g.head_out,
                           g.head_sse + blockIdx.y);
+    KT(33);
+    KTB(7);
     return;
   }
 
+  if (KW > 1 && kgrp != 0) return; // group 0 holds the sums
   // Epilogue: lanes 0-31 own consecutive columns -> each register row is a 128-B coalesced store.
   float *C = g.C + (EPI == EPI_STORE ? (long long)zsplit * g.slab_stride : 0LL);
+  with_act(EPI == EPI_FWD ? g.act : (EPI == EPI_DX ? g.aux_act : int(ACT_LINEAR)),
+           [&](auto AC) __attribute__((always_inline)) {
+    constexpr int A = decltype(AC)::value;
 #pragma unroll
-  for (int tn = 0; tn < TN; ++tn) {
-    const int n = n0 + wn * TN * 32 + tn * 32 + li;
-    if (n >= g.N) continue;
-    float bn = 0.0f;
-    if constexpr (EPI == EPI_FWD) bn = g.bias ? g.bias[n] : 0.0f;
+    for (int tn = 0; tn < TN; ++tn) {
+      const int n = n0 + wn * TN * 32 + tn * 32 + li;
+      if (n >= g.N) continue;
+      float bn = 0.0f;
+      if constexpr (EPI == EPI_FWD) bn = g.bias ? g.bias[n] : 0.0f;
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
+      for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m >= g.M) continue;
-        float v = acc[tm][tn][r];
-        if constexpr (EPI == EPI_FWD) v = act_apply(g.act, v + bn);
-        if constexpr (EPI == EPI_DX) v *= act_deriv_out(g.aux_act, g.aux[(long long)m * g.ldaux + n]);
-        C[(long long)m * g.ldc + n] = v;
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (m >= g.M) continue;
+          float v = acc[tm][tn][r];
+          if constexpr (EPI == EPI_FWD) v = act_c<A>(v + bn);
+          if constexpr (EPI == EPI_DX) v *= dact_c<A>(g.aux[(long long)m * g.ldaux + n]);
+          C[(long long)m * g.ldc + n] = v;
+        }
       }
     }
-  }
+  });
 }
 
 namespace {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI>
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int KW = 1, int PF = 1>
 void launch(hipStream_t s, const GemmDesc &d) {
+  // FAST loads: K % 4 == 0, vector-aligned operands, column counts % 4 == 0
+  const bool fast = d.K % 4 == 0 && (d.lda % 4 == 0) && (d.ldb % 4 == 0) &&
+                    ((reinterpret_cast<uintptr_t>(d.A) | reinterpret_cast<uintptr_t>(d.B)) & 15) == 0 &&
+                    (AKC || (d.a_mvalid > 0 ? d.a_mvalid : d.M) % 4 == 0) && (BKC || d.N % 4 == 0);
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   GemmK k;
   k.M = d.M;
@@ -406,18 +570,36 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.head_slab = d.head_slab;
   k.head_sse = d.head_sse;
   dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
-  if (d.a_idx)
-    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true>), grid, dim3(256), 0, s, k);
-  else
-    hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false>), grid, dim3(256), 0, s, k);
+  const dim3 block(256 * KW);
+  if (fast) {
+    if (d.a_idx) hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, KW, PF, true>), grid, block, 0, s, k);
+    else hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, KW, PF, true>), grid, block, 0, s, k);
+  } else { // general shapes: guarded loads, one k-tile in flight
+    if (d.a_idx) hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, KW, 1, false>), grid, block, 0, s, k);
+    else hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, KW, 1, false>), grid, block, 0, s, k);
+  }
+}
+
+int env_int(const char *name, int dflt) {
+  const char *e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
 }
 
 template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const GemmDesc &d) {
-  if (d.tile == TILE_32x128) launch<1, 4, 1, 1, AKC, BKC, EPI>(s, d);     // 32 x 128
-  else if (d.tile == TILE_64x64) launch<2, 2, 1, 1, AKC, BKC, EPI>(s, d); // 64 x 64
-  else if (d.N > 64) launch<2, 2, 2, 2, AKC, BKC, EPI>(s, d);            // 128 x 128
-  else if (d.N > 32) launch<2, 2, 2, 1, AKC, BKC, EPI>(s, d);  // 128 x 64
-  else launch<4, 1, 1, 1, AKC, BKC, EPI>(s, d);                // 128 x 32
+  static const int pf_big = env_int("LBF_GEMM_PF", 2), pf_small = env_int("LBF_GEMM_PF_SMALL", 2);
+  if (d.tile == TILE_32x128) { // 32 x 128, two k-groups
+    if (pf_small >= 4) launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 4>(s, d);
+    else if (pf_small >= 2) launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 2>(s, d);
+    else launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 1>(s, d);
+  } else if (d.tile == TILE_64x64) { // 64 x 64
+    if (pf_small >= 2) launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 2>(s, d);
+    else launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 1>(s, d);
+  } else if (d.N > 64) { // 128 x 128
+    if (pf_big >= 3) launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 3>(s, d);
+    else if (pf_big >= 2) launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 2>(s, d);
+    else launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 1>(s, d);
+  } else if (d.N > 32) launch<2, 2, 2, 1, AKC, BKC, EPI>(s, d); // 128 x 64
+  else launch<4, 1, 1, 1, AKC, BKC, EPI>(s, d);                 // 128 x 32
 }
 
 } // namespace
@@ -456,3 +638,12 @@ void gemm(hipStream_t s, const GemmDesc &d) {
 }
 
 } // namespace lbf
+
+#ifdef LBF_KTRACE
+extern "C" int lbf_dbg_ktrace_gemm(unsigned long long *host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(lbf::lbf_kt_buf), size_t(n) * 8) == hipSuccess ? 0 : 1;
+}
+extern "C" int lbf_dbg_ktrace_gemm_blk(unsigned long long *host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(lbf::lbf_kt_blk), sizeof(lbf::lbf_kt_blk)) == hipSuccess ? 0 : 1;
+}
+#endif

@@ -30,6 +30,7 @@ using namespace headc;
 
 constexpr int MAX_WG = 512; // 2 workgroups per CU
 
+template <int QM>
 __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const float *P, int Out, const float *Y,
                                                    const int *idx, long long B, int act_out, int act_prev,
                                                    double inv_scale, float *delta, float *slab, double *sse_part,
@@ -42,13 +43,14 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
   const bool vec = (H & 3) == 0 && ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(delta)) & 15) == 0;
   const int Hq = H >> 2;
   stage_w(sm, P, Out);
-  f32x4 cw[QMAX];
+  f32x4 cw[QM];
 #pragma unroll
-  for (int q = 0; q < QMAX; ++q) cw[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < QM; ++q) cw[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
   double sse = 0.0;
   TileArgs ta;
   ta.Y = Y;
   ta.idx = idx;
+  ta.ys = nullptr;
   ta.Out = Out;
   ta.act_out = act_out;
   ta.act_prev = act_prev;
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
       }
     }
     __syncthreads();
-    tile(sm, ta, b0, rows, cw, sse);
+    tile<false, QM>(sm, ta, b0, rows, cw, sse);
   }
   write_partials(sm, Out, cw, sse, slab + (long long)blockIdx.x * (H + 1) * Out, sse_part + blockIdx.x);
 }
@@ -96,12 +98,25 @@ void head_fused(hipStream_t s, const float *A, int H, const float *P, int Out, c
   const size_t shmem = size_t(smem_floats(H)) * sizeof(float);
   static bool set = false;
   if (!set) {
-    LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(head_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048));
+    const void *fns[] = {reinterpret_cast<const void *>(head_kernel<1>), reinterpret_cast<const void *>(head_kernel<2>),
+                         reinterpret_cast<const void *>(head_kernel<3>), reinterpret_cast<const void *>(head_kernel<4>),
+                         reinterpret_cast<const void *>(head_kernel<5>)};
+    for (const void *f : fns)
+      LBF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048));
     set = true;
   }
-  hipLaunchKernelGGL(head_kernel, dim3(head_nwg(B, H)), dim3(256), shmem, s, A, H, P, Out, Y, idx, B, act_out,
-                     act_prev, inv_scale, delta, slab, sse_part, abort);
+  const dim3 grid(head_nwg(B, H)), block(256);
+#define LBF_HEAD_LAUNCH(Q)                                                                                    \
+  hipLaunchKernelGGL(head_kernel<Q>, grid, block, shmem, s, A, H, P, Out, Y, idx, B, act_out, act_prev, inv_scale, \
+                     delta, slab, sse_part, abort)
+  switch (qstrips(H)) {
+  case 1: LBF_HEAD_LAUNCH(1); break;
+  case 2: LBF_HEAD_LAUNCH(2); break;
+  case 3: LBF_HEAD_LAUNCH(3); break;
+  case 4: LBF_HEAD_LAUNCH(4); break;
+  default: LBF_HEAD_LAUNCH(5); break;
+  }
+#undef LBF_HEAD_LAUNCH
   LBF_KERNEL_CHECK();
 }
 

@@ -88,18 +88,29 @@ private:
 inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
 
 // Phase timestamps for kernel tuning (debug build only: make ktrace). KT(slot) stores the 100 MHz
-// wall clock from thread 0 of block 0; lbf_dbg_ktrace() copies the slots to the host.
+// wall clock from thread 0 of block (0,0,0); lbf_dbg_ktrace() copies the slots to the host.
 #ifdef LBF_KTRACE
 static __device__ unsigned long long lbf_kt_buf[256]; // one per translation unit (no RDC)
 #define KT(slot)                                                                                        \
   do {                                                                                                  \
-    if (blockIdx.x == 0 && threadIdx.x == 0) lbf_kt_buf[slot] = wall_clock64();                         \
+    if ((blockIdx.x | blockIdx.y | blockIdx.z | threadIdx.x) == 0) lbf_kt_buf[slot] = wall_clock64();                         \
   } while (0)
 #define KTC(slot)                                                                                       \
   do {                                                                                                  \
-    if (blockIdx.x == 0 && threadIdx.x == 0) lbf_kt_buf[slot] = clock64();                              \
+    if ((blockIdx.x | blockIdx.y | blockIdx.z | threadIdx.x) == 0) lbf_kt_buf[slot] = clock64();                              \
+  } while (0)
+// KTB(slot): per-block stamps (thread 0 of every block with blockIdx.z == 0, first 1024 blocks) for
+// the distribution of phase times across the grid.
+static __device__ unsigned long long lbf_kt_blk[8 * 1024];
+#define KTB(slot)                                                                                       \
+  do {                                                                                                  \
+    const unsigned lin_ = blockIdx.y * gridDim.x + blockIdx.x;                                          \
+    if (threadIdx.x == 0 && blockIdx.z == 0 && lin_ < 1024) lbf_kt_blk[(slot) * 1024 + lin_] = wall_clock64(); \
   } while (0)
 #else
+#define KTB(slot)                                                                                       \
+  do {                                                                                                  \
+  } while (0)
 #define KTC(slot)                                                                                       \
   do {                                                                                                  \
   } while (0)

@@ -5,6 +5,7 @@
 // Replaces: diff_kernel / sum_rows_kernel (src/cuda/kernels.cuh:136-153), cublasSdot / Snrm2 / Saxpy /
 // Sscal with host pointer mode (kernels.cuh:28-50, every scalar a blocking device->host copy), and
 // CudaLBFGS::compute_direction_ring (src/cuda/lbfgs.cuh:206-261, 2k+2 blocking dots + 2k axpys).
+#include "act.hpp"
 #include "internal.hpp"
 #include "hist_core.hpp"
 #include "kernels.hpp"
@@ -43,15 +44,6 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double *scratch) {
     }
   }
   __syncthreads();
-}
-
-__device__ __forceinline__ float act_deriv_out(int a, float y) {
-  switch (a) {
-  case ACT_TANH: return 1.0f - y * y;
-  case ACT_RELU: return y > 0.0f ? 1.0f : 0.0f;
-  case ACT_SIGMOID: return y * (1.0f - y);
-  default: return 1.0f;
-  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -99,7 +91,7 @@ __global__ __launch_bounds__(256) void loss_diff_kernel(const float *A, long lon
     const long long yr = idx ? (long long)idx[b] : b;
     const float d = a - Y[yr * ldy + o];
     acc[0] += double(d) * double(d);
-    dZ[b * ldz + o] = d * act_deriv_out(act, a) * sc;
+    dZ[b * ldz + o] = d * dact_rt(act, a) * sc;
   }
   block_sum<1>(acc, scratch);
   if (threadIdx.x == 0) partials[blockIdx.x] = acc[0];
@@ -156,14 +148,7 @@ __global__ __launch_bounds__(256) void fwd_reduce_act_kernel(const float *slab, 
   for (; k < splits; ++k) acc += slab[(long long)k * stride + e];
   const int n = int(e % N);
   const float z = acc + (bias ? bias[n] : 0.0f);
-  float a;
-  switch (act) {
-  case ACT_TANH: a = tanhf(z); break;
-  case ACT_RELU: a = z > 0.0f ? z : 0.0f; break;
-  case ACT_SIGMOID: a = 1.0f / (1.0f + expf(-z)); break;
-  default: a = z;
-  }
-  out[e] = a;
+  out[e] = act_rt(act, z);
 }
 
 void fwd_reduce_act(hipStream_t s, const float *slab, int splits, long long stride, int M, int N, const float *bias,

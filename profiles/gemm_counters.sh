@@ -10,7 +10,7 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
            "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS"; do
   i=$((i+1))
-  NS=60000 timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $O/p$i -o run -- python3 $R/profiles/gemm_probe.py > $O/p$i.log 2>&1
+  NS=${NS:-60000} timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d $O/p$i -o run -- python3 $R/profiles/gemm_probe.py > $O/p$i.log 2>&1
 done
 python3 - <<'PY'
 import csv, glob, os, collections
