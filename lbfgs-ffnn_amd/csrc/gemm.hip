@@ -220,6 +220,112 @@ __device__ __forceinline__ void store_mc(float *lds, const f32x4 (&r)[R / 32], i
   }
 }
 
+// Epilogues shared by both main loops: the fused output layer (EPI_HEAD) or the bias/activation/
+// derivative/slab store of the accumulators.
+template <int WM, int WN, int TM, int TN, int EPI, int KW, class HPre>
+__device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][TN], float *lds, HPre &hpre, int zsplit,
+                                              int m0, int n0, int wm, int wn, int li, int lh, int kgrp) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  if constexpr (EPI == EPI_HEAD) {
+    KTB(1);
+    // Output layer on the tile (head_core.hpp): the prefetched W / biases / targets go to LDS, then per
+    // 64-row half the activations go accumulators -> LDS (bias + activation; columns >= N zero) and
+    // the head runs on them. n0 == 0 (N <= BN).
+    constexpr int QM = headc::qstrips(BN);
+    const headc::Smem hs = headc::carve(lds, g.N);
+    hpre.store(hs);
+    KT(26);
+    KTB(2);
+    headc::f32x4 cw[QM];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) cw[q] = (headc::f32x4){0.f, 0.f, 0.f, 0.f};
+    double sse = 0.0;
+    headc::TileArgs ta;
+    ta.Y = g.head_Y;
+    ta.idx = g.head_idx;
+    ta.Out = g.head_out;
+    ta.act_out = g.head_act;
+    ta.act_prev = g.act;
+    ta.sc = float(g.head_inv_scale);
+    ta.delta = g.head_delta;
+    ta.vec = (g.N & 3) == 0 && (reinterpret_cast<uintptr_t>(g.head_delta) & 15) == 0;
+    for (int half = 0; half < (BM + headc::TB - 1) / headc::TB; ++half) {
+      const long long b0 = (long long)m0 + half * headc::TB;
+      const int rows_tile = min(headc::TB, BM - half * headc::TB);
+      const int rows = int(min((long long)rows_tile, (long long)g.M - b0));
+      if (rows <= 0) break;
+      ta.ys = hs.ys + half * headc::TB * 16;
+      if (half == 0) __syncthreads(); // hb (read below) written by hpre.store
+      for (int e = threadIdx.x; e < (headc::TB - rows_tile) * hs.Hp; e += 256 * KW) { // rows the tile lacks
+        const int r = rows_tile + e / hs.Hp, c = e % hs.Hp;
+        hs.As[r * hs.LDA + c] = 0.0f;
+      }
+      with_act(g.act, [&](auto AC) __attribute__((always_inline)) {
+        constexpr int A = decltype(AC)::value;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn) {
+            const int col = wn * TN * 32 + tn * 32 + li;
+            const int local0 = wm * TM * 32 + tm * 32;
+            if (kgrp == 0 && local0 / headc::TB == half && col < hs.Hp) { // the tile may be wider than Hp
+              const float bn = hs.hb[col];
+              const bool in = col < g.N;
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const int local = local0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                hs.As[(local % headc::TB) * hs.LDA + col] = in ? act_c<A>(acc[tm][tn][r] + bn) : 0.0f;
+              }
+            }
+          }
+      });
+      if (hs.Hp > BN)
+        for (int e = threadIdx.x; e < rows_tile * (hs.Hp - BN); e += 256 * KW) { // padding beyond the tile width
+          const int r = e / (hs.Hp - BN), c = BN + e % (hs.Hp - BN);
+          hs.As[r * hs.LDA + c] = 0.0f;
+        }
+      __syncthreads();
+      KT(28 + 2 * half);
+      KTB(3 + 2 * half);
+      headc::tile<(KW > 1), QM>(hs, ta, b0, rows, cw, sse);
+      KT(29 + 2 * half);
+      KTB(4 + 2 * half);
+    }
+    KT(32);
+    headc::write_partials(hs, g.head_out, cw, sse, g.head_slab + (long long)blockIdx.y * (g.N + 1) * g.head_out,
+                          g.head_sse + blockIdx.y);
+    KT(33);
+    KTB(7);
+    return;
+  }
+  if (KW > 1 && kgrp != 0) return; // group 0 holds the sums
+  // Epilogue: lanes 0-31 own consecutive columns -> each register row is a 128-B coalesced store.
+  float *C = g.C + (EPI == EPI_STORE ? (long long)zsplit * g.slab_stride : 0LL);
+  with_act(EPI == EPI_FWD ? g.act : (EPI == EPI_DX ? g.aux_act : int(ACT_LINEAR)),
+           [&](auto AC) __attribute__((always_inline)) {
+    constexpr int A = decltype(AC)::value;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int n = n0 + wn * TN * 32 + tn * 32 + li;
+      if (n >= g.N) continue;
+      float bn = 0.0f;
+      if constexpr (EPI == EPI_FWD) bn = g.bias ? g.bias[n] : 0.0f;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (m >= g.M) continue;
+          float v = acc[tm][tn][r];
+          if constexpr (EPI == EPI_FWD) v = act_c<A>(v + bn);
+          if constexpr (EPI == EPI_DX) v *= dact_c<A>(g.aux[(long long)m * g.ldaux + n]);
+          C[(long long)m * g.ldc + n] = v;
+        }
+      }
+    }
+  });
+}
+
 // KW k-groups of 4 waves each (KW = 2: 8 waves, two per SIMD, for tiles too small to fill the chip
 // with one wave per SIMD): group q runs k-steps [16q/KW, 16(q+1)/KW) of every 32-deep tile on the
 // same output sub-tile, and the groups' accumulators are summed through LDS in group order.
@@ -418,112 +524,212 @@ __global__ __launch_bounds__(256 * KW, 2) void gemm_kernel(const GemmK g) {
     static_assert(PER * 256 <= LDS_F, "k-group reduction buffer");
   }
 
-  if constexpr (EPI == EPI_HEAD) {
-    KTB(1);
-    // Output layer on the tile (head_core.hpp): the prefetched W / biases / targets go to LDS, then per
-    // 64-row half the activations go accumulators -> LDS (bias + activation; columns >= N zero) and
-    // the head runs on them. n0 == 0 (N <= BN).
-    constexpr int QM = headc::qstrips(BN);
-    const headc::Smem hs = headc::carve(lds, g.N);
-    hpre.store(hs);
-    KT(26);
-    KTB(2);
-    headc::f32x4 cw[QM];
-#pragma unroll
-    for (int q = 0; q < QM; ++q) cw[q] = (headc::f32x4){0.f, 0.f, 0.f, 0.f};
-    double sse = 0.0;
-    headc::TileArgs ta;
-    ta.Y = g.head_Y;
-    ta.idx = g.head_idx;
-    ta.Out = g.head_out;
-    ta.act_out = g.head_act;
-    ta.act_prev = g.act;
-    ta.sc = float(g.head_inv_scale);
-    ta.delta = g.head_delta;
-    ta.vec = (g.N & 3) == 0 && (reinterpret_cast<uintptr_t>(g.head_delta) & 15) == 0;
-    for (int half = 0; half < (BM + headc::TB - 1) / headc::TB; ++half) {
-      const long long b0 = (long long)m0 + half * headc::TB;
-      const int rows_tile = min(headc::TB, BM - half * headc::TB);
-      const int rows = int(min((long long)rows_tile, (long long)g.M - b0));
-      if (rows <= 0) break;
-      ta.ys = hs.ys + half * headc::TB * 16;
-      if (half == 0) __syncthreads(); // hb (read below) written by hpre.store
-      for (int e = threadIdx.x; e < (headc::TB - rows_tile) * hs.Hp; e += 256 * KW) { // rows the tile lacks
-        const int r = rows_tile + e / hs.Hp, c = e % hs.Hp;
-        hs.As[r * hs.LDA + c] = 0.0f;
-      }
-      with_act(g.act, [&](auto AC) __attribute__((always_inline)) {
-        constexpr int A = decltype(AC)::value;
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn) {
-            const int col = wn * TN * 32 + tn * 32 + li;
-            const int local0 = wm * TM * 32 + tm * 32;
-            if (kgrp == 0 && local0 / headc::TB == half && col < hs.Hp) { // the tile may be wider than Hp
-              const float bn = hs.hb[col];
-              const bool in = col < g.N;
-#pragma unroll
-              for (int r = 0; r < 16; ++r) {
-                const int local = local0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                hs.As[(local % headc::TB) * hs.LDA + col] = in ? act_c<A>(acc[tm][tn][r] + bn) : 0.0f;
-              }
-            }
-          }
-      });
-      if (hs.Hp > BN)
-        for (int e = threadIdx.x; e < rows_tile * (hs.Hp - BN); e += 256 * KW) { // padding beyond the tile width
-          const int r = e / (hs.Hp - BN), c = BN + e % (hs.Hp - BN);
-          hs.As[r * hs.LDA + c] = 0.0f;
-        }
-      __syncthreads();
-      KT(28 + 2 * half);
-      KTB(3 + 2 * half);
-      headc::tile<(KW > 1), QM>(hs, ta, b0, rows, cw, sse);
-      KT(29 + 2 * half);
-      KTB(4 + 2 * half);
-    }
-    KT(32);
-    headc::write_partials(hs, g.head_out, cw, sse, g.head_slab + (long long)blockIdx.y * (g.N + 1) * g.head_out,
-                          g.head_sse + blockIdx.y);
-    KT(33);
-    KTB(7);
+  gemm_epilogue<WM, WN, TM, TN, EPI, KW>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, kgrp);
+}
+
+// ------------------------------------------------------------------------------------------------
+// LDS-DMA main loop (global_load_lds_dwordx4): operand tiles go HBM -> LDS with no register staging,
+// NS tile buffers in a ring, NS-1 k-tiles in flight. Each wave issues the same P = (BM+BN)/32 1-KiB
+// pieces per k-tile, so "k-tile i has landed" is a counted s_waitcnt vmcnt(P * tiles issued after
+// it) plus a raw s_barrier (a __syncthreads would drain every tile in flight).
+// The DMA writes 64 lanes x 16 B contiguously, so the LDS images are unpadded and the bank-conflict
+// swizzle is applied through the per-lane SOURCE address:
+//   k-contiguous [R][32]: 16-B chunk slot c of row r holds global chunk c ^ ((r >> 1) & 7)
+//       (a ds_read_b128 quarter-wave covers 16 distinct bank groups);
+//   mn-contiguous [32][R] (R >= 64): row k holds its chunks XOR 8 when k >= 16 (column ^ 32), so the
+//       two lane halves (k = s and k = 16 + s) of a ds_read_b32 use opposite bank halves.
+// Out-of-range chunks (rows >= M, k >= K, columns >= N) read a zero chunk; the bias "ones" column reads
+// {1,0,0,0}. Requires K % 4 == 0, 16-B aligned rows and column counts % 4 == 0 (FAST shapes).
+// ------------------------------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) const float lbf_glds_const[8] = {0.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+__device__ __forceinline__ void glds16(const float *src, float *lds_dst) {
+  __builtin_amdgcn_global_load_lds((glb_void_t *)src, (lds_void_t *)lds_dst, 16, 0, 0);
+}
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// wait until at most `ahead` k-tiles (P pieces each) of this wave are still in flight
+template <int P, int NS> __device__ __forceinline__ void vm_wait_tiles(int ahead) {
+  static_assert(NS >= 2 && NS <= 6, "stages");
+  if (NS >= 6 && ahead >= 4) vm_wait<4 * P>();
+  else if (NS >= 5 && ahead >= 3) vm_wait<3 * P>();
+  else if (NS >= 4 && ahead >= 2) vm_wait<2 * P>();
+  else if (NS >= 3 && ahead >= 1) vm_wait<P>();
+  else vm_wait<0>();
+}
+
+// One 1-KiB piece of a k-tile: per-lane source for k-tile t.
+struct GldsPiece {
+  unsigned long long p0; // source address at the block's first k-tile (the zero / ones chunk if out of range)
+  unsigned long long step; // bytes per k-tile (0 for the constant chunks)
+  int kq;                  // k offset of this lane's chunk / row inside a k-tile
+};
+
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS>
+__global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32;
+  constexpr int ASZ = BM * BK, STG = (BM + BN) * BK;
+  constexpr int PA = BM / 8, P = (BM + BN) / 32; // A pieces per k-tile, pieces per wave per k-tile
+  static_assert((BM + BN) % 32 == 0, "pieces per wave");
+  static_assert(AKC || BM >= 64, "mn-contiguous swizzle needs >= 64 columns");
+  static_assert(BKC || BN >= 64, "mn-contiguous swizzle needs >= 64 columns");
+  constexpr int HEAD_F = headc::smem_floats_epi(BN, BM);
+  constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > NS * STG) ? HEAD_F : NS * STG;
+  __shared__ __attribute__((aligned(16))) float lds[LDS_F];
+  if (g.abort && *g.abort) return;
+  if (int(blockIdx.z) < g.side_planes) {
+    gemm_side_job(g, reinterpret_cast<double *>(lds));
     return;
   }
+  const int zsplit = int(blockIdx.z) - g.side_planes;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 31, lh = lane >> 5;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int kb = zsplit * g.k_chunk;
+  const int ke = min(g.K, kb + g.k_chunk);
 
-  if (KW > 1 && kgrp != 0) return; // group 0 holds the sums
-  // Epilogue: lanes 0-31 own consecutive columns -> each register row is a 128-B coalesced store.
-  float *C = g.C + (EPI == EPI_STORE ? (long long)zsplit * g.slab_stride : 0LL);
-  with_act(EPI == EPI_FWD ? g.act : (EPI == EPI_DX ? g.aux_act : int(ACT_LINEAR)),
-           [&](auto AC) __attribute__((always_inline)) {
-    constexpr int A = decltype(AC)::value;
+  f32x16 acc[TM][TN];
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-      const int n = n0 + wn * TN * 32 + tn * 32 + li;
-      if (n >= g.N) continue;
-      float bn = 0.0f;
-      if constexpr (EPI == EPI_FWD) bn = g.bias ? g.bias[n] : 0.0f;
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+  // ---- this wave's pieces: j = wave + 4 i; j < PA -> A, else B ----
+  const unsigned long long zero_u = reinterpret_cast<unsigned long long>(lbf_glds_const);
+  GldsPiece pc[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    const int j = wave + 4 * i;
+    const bool isA = j < PA;
+    const int jj = isA ? j : j - PA;
+    const bool kc = isA ? AKC : BKC;
+    const float *base = isA ? g.A : g.B;
+    const long long ld = isA ? g.lda : g.ldb;
+    GldsPiece q;
+    bool ok, ones = false;
+    const float *src;
+    if (kc) { // rows 8jj .. 8jj+7, 8 chunks each
+      const int r = 8 * jj + (lane >> 3);
+      const int gc = (lane & 7) ^ ((r >> 1) & 7);
+      const int row = (isA ? m0 : n0) + r;
+      ok = row < (isA ? g.M : g.N);
+      long long grow = ok ? row : 0;
+      if (GATHER && isA && ok) grow = g.a_idx[row];
+      src = base + grow * ld + kb + 4 * gc;
+      q.step = BK * sizeof(float);
+      q.kq = 4 * gc;
+    } else { // R columns per k-row, 256 / R k-rows per piece
+      const int R = isA ? BM : BN;
+      const int kl = jj * (256 / R) + (lane * 4) / R;
+      const int gc = ((lane * 4) % R / 4) ^ (((kl >> 4) & 1) * 8);
+      const int col = (isA ? m0 : n0) + 4 * gc;
+      ok = col < (isA ? g.a_mvalid : g.N);
+      ones = isA && col == g.a_ones;
+      src = base + (long long)(kb + kl) * ld + (ok ? col : 0);
+      q.step = (unsigned long long)(BK * ld) * sizeof(float);
+      q.kq = kl;
+    }
+    q.p0 = ok ? reinterpret_cast<unsigned long long>(src) : zero_u + (ones ? 16 : 0);
+    if (!ok) q.step = 0;
+    pc[i] = q;
+  }
+  auto issue = [&](int t) {
+    float *stage = lds + (t % NS) * STG;
+    const int kt = kb + t * BK;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int j = wave + 4 * i;
+      const unsigned long long a = pc[i].p0 + (unsigned long long)t * pc[i].step;
+      glds16(reinterpret_cast<const float *>(kt + pc[i].kq < ke ? a : zero_u),
+             stage + (j < PA ? j * 256 : ASZ + (j - PA) * 256));
+    }
+  };
+  auto compute = [&](int buf) {
+    const float *As = lds + buf * STG;
+    const float *Bs = As + ASZ;
+    float af[TM][AKC ? 16 : 1], bf[TN][BKC ? 16 : 1];
+    if constexpr (AKC) {
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
+        const int row = wm * TM * 32 + tm * 32 + li;
+        const int sw = (row >> 1) & 7;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (m >= g.M) continue;
-          float v = acc[tm][tn][r];
-          if constexpr (EPI == EPI_FWD) v = act_c<A>(v + bn);
-          if constexpr (EPI == EPI_DX) v *= dact_c<A>(g.aux[(long long)m * g.ldaux + n]);
-          C[(long long)m * g.ldc + n] = v;
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = *reinterpret_cast<const f32x4 *>(As + row * BK + 4 * ((lh * 4 + q) ^ sw));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[tm][q * 4 + e] = v[e];
         }
       }
     }
-  });
+    if constexpr (BKC) {
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wn * TN * 32 + tn * 32 + li;
+        const int sw = (row >> 1) & 7;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = *reinterpret_cast<const f32x4 *>(Bs + row * BK + 4 * ((lh * 4 + q) ^ sw));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bf[tn][q * 4 + e] = v[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        if constexpr (AKC) av[tm] = af[tm][s];
+        else av[tm] = As[(lh * 16 + s) * BM + ((wm * TM * 32 + tm * 32 + li) ^ (lh << 5))];
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        if constexpr (BKC) bv[tn] = bf[tn][s];
+        else bv[tn] = Bs[(lh * 16 + s) * BN + ((wn * TN * 32 + tn * 32 + li) ^ (lh << 5))];
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
+    }
+  };
+
+  if (EPI == EPI_HEAD) KTB(0);
+  headc::EpiPrefetch<BN, BM, 256> hpre;
+  if constexpr (EPI == EPI_HEAD) hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
+  const int nk = kb < ke ? (ke - kb + BK - 1) / BK : 0;
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(t);
+  for (int i = 0; i < nk; ++i) {
+    vm_wait_tiles<P, NS>(min(NS - 2, nk - 1 - i)); // this wave's pieces of k-tile i landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier(); // everyone's pieces landed; buffer (i - 1) % NS no longer read
+    if (i + NS - 1 < nk) issue(i + NS - 1);
+    compute(i % NS);
+  }
+  __syncthreads(); // the LDS is the epilogue's now
+  gemm_epilogue<WM, WN, TM, TN, EPI, 1>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, 0);
 }
 
 namespace {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int KW = 1, int PF = 1>
+int env_int(const char *name, int dflt) {
+  const char *e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+// NS > 0: the LDS-DMA kernel with NS tile buffers where the shape allows it (FAST shapes, no gathered
+// mn-contiguous operand); otherwise the register-staged kernel (KW k-groups, PF register sets).
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int KW = 1, int PF = 1, int NS = 0>
 void launch(hipStream_t s, const GemmDesc &d) {
   // FAST loads: K % 4 == 0, vector-aligned operands, column counts % 4 == 0
   const bool fast = d.K % 4 == 0 && (d.lda % 4 == 0) && (d.ldb % 4 == 0) &&
@@ -570,6 +776,14 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.head_slab = d.head_slab;
   k.head_sse = d.head_sse;
   dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
+  static const bool glds_on = env_int("LBF_GEMM_GLDS", 1) != 0;
+  if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
+    if (fast && glds_on && (AKC || !d.a_idx)) {
+      if (d.a_idx) hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, NS>), grid, dim3(256), 0, s, k);
+      else hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, NS>), grid, dim3(256), 0, s, k);
+      return;
+    }
+  }
   const dim3 block(256 * KW);
   if (fast) {
     if (d.a_idx) hipLaunchKernelGGL((gemm_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, KW, PF, true>), grid, block, 0, s, k);
@@ -580,26 +794,20 @@ void launch(hipStream_t s, const GemmDesc &d) {
   }
 }
 
-int env_int(const char *name, int dflt) {
-  const char *e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-
 template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const GemmDesc &d) {
   static const int pf_big = env_int("LBF_GEMM_PF", 2), pf_small = env_int("LBF_GEMM_PF_SMALL", 2);
-  if (d.tile == TILE_32x128) { // 32 x 128, two k-groups
-    if (pf_small >= 4) launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 4>(s, d);
-    else if (pf_small >= 2) launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 2>(s, d);
-    else launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 1>(s, d);
-  } else if (d.tile == TILE_64x64) { // 64 x 64
-    if (pf_small >= 2) launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 2>(s, d);
-    else launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 1>(s, d);
-  } else if (d.N > 64) { // 128 x 128
-    if (pf_big >= 3) launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 3>(s, d);
-    else if (pf_big >= 2) launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 2>(s, d);
-    else launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 1>(s, d);
-  } else if (d.N > 32) launch<2, 2, 2, 1, AKC, BKC, EPI>(s, d); // 128 x 64
-  else launch<4, 1, 1, 1, AKC, BKC, EPI>(s, d);                 // 128 x 32
+  // LDS-DMA stages: as many tile buffers as fit two workgroups per CU (80 KB each)
+  if (d.tile == TILE_32x128) { // 32 x 128 (20 KB per stage)
+    if (pf_small >= 2) launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 2, 4>(s, d);
+    else launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 1, 4>(s, d);
+  } else if (d.tile == TILE_64x64) { // 64 x 64 (16 KB per stage)
+    if (pf_small >= 2) launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 2, 5>(s, d);
+    else launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 1, 5>(s, d);
+  } else if (d.N > 64) { // 128 x 128 (32 KB per stage)
+    if (pf_big >= 2) launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 2, 2>(s, d);
+    else launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 1, 2>(s, d);
+  } else if (d.N > 32) launch<2, 2, 2, 1, AKC, BKC, EPI, 1, 1, 3>(s, d); // 128 x 64 (24 KB per stage)
+  else launch<4, 1, 1, 1, AKC, BKC, EPI, 1, 1, 3>(s, d);                 // 128 x 32 (20 KB per stage)
 }
 
 } // namespace

@@ -41,9 +41,14 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   const HistView &h = a.h;
   const int t = threadIdx.x, lane = t & 63, stripe = t >> 6, wave = stripe;
   KT(48);
+  KTB(0);
+#ifdef LBF_KTRACE
+  if (t == 0 && blockIdx.x >= 1024 && blockIdx.x < 2048) lbf_kt_blk[5 * 1024 + blockIdx.x - 1024] = wall_clock64();
+#endif
   // the ring header in one round trip (count, free slot, order)
   if (t < IST_ORDER + h.m) ist[t] = h.ist[t];
   __syncthreads();
+  KTB(1);
   const int count0 = ist[IST_COUNT];
   const int w = hist_write_slot(ist, h.m, a.policy, 0);
   if (blockIdx.x == 0 && t == 0) h.ist[IST_WSLOT] = w;
@@ -95,6 +100,7 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   part[stripe][lane] = acc;
   __syncthreads();
   KT(51);
+  KTB(2);
   double *row = a.rows + (long long)blockIdx.x * a.nc;
   if (wave == 0) {
     float gv = 0.f, sv = 0.f, yv = 0.f;
@@ -131,6 +137,7 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   KT(52);
   __syncthreads();
   KT(53);
+  KTB(3);
   // ---- Gram sweep of this column group ----
   const double s = lsv[lane], y = lyv[lane], g = lgv[lane];
 #pragma unroll
@@ -148,6 +155,10 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
     }
   }
   KT(54);
+  KTB(4);
+#ifdef LBF_KTRACE
+  if (t == 0 && blockIdx.x >= 1024 && blockIdx.x < 2048) lbf_kt_blk[6 * 1024 + blockIdx.x - 1024] = wall_clock64();
+#endif
 }
 
 // dots[c] = sum over rows in row order (per-thread strided rows, then a fixed tree).
@@ -297,5 +308,8 @@ void tail_fin(hipStream_t s, const TailArgs &a) {
 #ifdef LBF_KTRACE
 extern "C" int lbf_dbg_ktrace_tail(unsigned long long *host, int n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(lbf::lbf_kt_buf), size_t(n) * 8) == hipSuccess ? 0 : 1;
+}
+extern "C" int lbf_dbg_ktrace_tail_blk(unsigned long long *host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(lbf::lbf_kt_blk), sizeof(lbf::lbf_kt_blk)) == hipSuccess ? 0 : 1;
 }
 #endif

@@ -40,6 +40,28 @@ def main():
     wall = (tbuf[60] - tbuf[63]) / 100.0
     cyc = tbuf[65] - tbuf[64]
     print(f"backward sweep: {wall:.2f} us wall, {cyc} shader cycles -> {cyc / max(wall, 1e-9):.0f} MHz")
+    blk = (C.c_ulonglong * 8192)()
+    L.lbf_dbg_ktrace_tail_blk.argtypes = [C.c_void_p]
+    assert L.lbf_dbg_ktrace_tail_blk(blk) == 0
+    nb = 1024
+    S = [[blk[k * 1024 + i] for i in range(nb)] for k in range(5)]
+    t0 = min(S[0])
+    q = lambda v: sorted(v)[len(v) // 2]
+    names = ["header", "loads", "wave0 dots", "gram sweep"]
+    st = [(x - t0) / 100 for x in S[0]]
+    line = [f"start {min(st):.2f}/{q(st):.2f}/{max(st):.2f}"]
+    for k in range(1, 5):
+        d = [(S[k][i] - S[k - 1][i]) / 100 for i in range(nb)]
+        line.append(f"{names[k-1]} {min(d):.2f}/{q(d):.2f}/{max(d):.2f}")
+    en = [(x - t0) / 100 for x in S[4]]
+    line.append(f"end {min(en):.2f}/{q(en):.2f}/{max(en):.2f}")
+    print("tail_reduce blocks 0..1023 (min/med/max us):", "  ".join(line))
+    hi = [i for i in range(1024) if S[0][i] and blk[5 * 1024 + i] > t0 and blk[6 * 1024 + i] > blk[5 * 1024 + i]]
+    if hi:
+        s2 = [(blk[5 * 1024 + i] - t0) / 100 for i in hi]
+        e2 = [(blk[6 * 1024 + i] - t0) / 100 for i in hi]
+        print(f"tail_reduce blocks >=1024 ({len(hi)}): start {min(s2):.2f}/{q(s2):.2f}/{max(s2):.2f}  "
+              f"end {min(e2):.2f}/{q(e2):.2f}/{max(e2):.2f}")
     for name, rg in GROUPS.items():
         t0 = buf[rg[0]]
         print(name, " ".join(f"{(buf[i] - t0) / 100.0:.2f}" for i in rg))
