@@ -77,6 +77,9 @@ void gemm_tile_for(int N, int tile, int *BM, int *BN);
 // ------------------------------------------------------------------------------------------------
 // out[c] = sum_r P[r*ncols + c], r in [0, nrows), fixed order.    (one wave per column)
 void reduce_rows(hipStream_t s, const double *P, int nrows, int ncols, double *out);
+// Partial fold of a tall table: `groups` row groups -> out[g][ncols] (fixed order); returns the number of
+// row groups actually written.
+int fold_rows(hipStream_t s, const double *P, int nrows, int ncols, int groups, double *out);
 
 // Output layer: d = act_out(Z) already in A_out; diff = A_out - Y[idx? idx[b] : b];
 // dZ = diff * act'(A_out) * inv_scale ; per-WG partial of sum(diff^2) -> partials[wg].

@@ -461,7 +461,7 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
   const size_t nd = slots + 3 * size_t(slots) * slots + 2 * slots + (2 * slots + 1) + SC_N;
   dstate_.resize(nd);
   part_.resize(size_t(gram_nwg(n)) * gram_ncols(m));
-  red_.resize(size_t(gram_ncols(m)));
+  red_.resize(size_t(kGramFold) * gram_ncols(m));
   v_.m = m;
   v_.slots = slots;
   v_.n = n;
@@ -508,6 +508,11 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
   c.h.abort = ctx_->abort;
   c.partials = part_.get();
   c.nwg = gram_nwg(v_.n);
+  if (c.nwg > 2 * kGramFold) { // tall partial table (large n): fold it on many blocks first, so the
+    ProfScope pf(ctx_, PK_COEF); // single-workgroup history step reads kGramFold rows, not thousands
+    c.nwg = fold_rows(s, part_.get(), c.nwg, gram_ncols(v_.m), kGramFold, red_.get());
+    c.partials = red_.get();
+  }
   c.has_pair = g.has_pair;
   c.has_g = g.has_g;
   c.reset = g.reset;

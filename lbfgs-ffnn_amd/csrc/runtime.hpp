@@ -128,6 +128,9 @@ private:
 };
 
 // Device-resident history of (s, y) pairs and its fp64 Gram state.
+// Row groups the Gram sweep's partial table is folded into before the history step (large n).
+constexpr int kGramFold = 32;
+
 class History {
 public:
   History(Ctx *ctx, int m, long long n);

@@ -67,8 +67,10 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
   depth_ = 3;
   if (const char *e = std::getenv("LBF_SPEC_DEPTH")) depth_ = std::max(0, std::min(16, std::atoi(e)));
   if (!obj_->async()) depth_ = 0;
-  // Fused optimizer tail on the speculative path (LBF_FUSED_TAIL=0 disables).
-  fuse_ = depth_ > 0 && obj_->fused_tail() && prm_.m > 0 && prm_.m <= TAIL_MAXM;
+  // Fused optimizer tail on the speculative path (LBF_FUSED_TAIL=0 disables). It is a latency design
+  // (one block per 64 coordinates, a partial row each): past kFusedTailMaxN the classic Gram sweep +
+  // folded history step moves fewer bytes.
+  fuse_ = depth_ > 0 && obj_->fused_tail() && prm_.m > 0 && prm_.m <= TAIL_MAXM && n_ <= kFusedTailMaxN;
   if (const char *e = std::getenv("LBF_FUSED_TAIL")) fuse_ = fuse_ && e[0] != '0';
   if (depth_ > 0) {
     abort_.resize(1);

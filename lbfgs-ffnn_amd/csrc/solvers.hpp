@@ -117,6 +117,7 @@ private:
   void drain(std::deque<Flight> &q, size_t prof_end);
   void wait_record(int seq, SpecRecord *out);
   static constexpr int kSpecRing = 32;
+  static constexpr long long kFusedTailMaxN = 1LL << 21;
   int depth_ = 0;
   int seq_ = 0;
   bool fuse_ = false;      // fused optimizer tail on the speculative path

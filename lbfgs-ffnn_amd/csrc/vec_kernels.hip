@@ -66,6 +66,42 @@ void reduce_rows(hipStream_t s, const double *P, int nrows, int ncols, double *o
 }
 
 // ---------------------------------------------------------------------------------------------
+// fold_rows: out[j][c] = sum_{r in group j} P[r][c]; group j = rows [j*per, (j+1)*per). One block per
+// (64-column group, row group): lane = column (coalesced 512-B row segments), wave w takes rows
+// w, w+4, ... of the group, the four wave sums are added in a fixed order. Used to shrink a tall
+// partial table (the Gram sweep's [nwg][6m+6] at large n) before a single-workgroup consumer.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fold_rows_kernel(const double *P, int nrows, int ncols, int per, double *out) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * per, r1 = min(nrows, r0 + per);
+  double s = 0.0;
+  if (c < ncols) {
+    for (int r = r0 + wave; r < r1; r += 4 * 8) { // eight independent loads in flight per lane
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = r + 4 * u < r1 ? P[(long long)(r + 4 * u) * ncols + c] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+  }
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && c < ncols)
+    out[(long long)blockIdx.y * ncols + c] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+}
+
+int fold_rows(hipStream_t s, const double *P, int nrows, int ncols, int groups, double *out) {
+  const int per = int(cdiv(nrows, groups));
+  const int g = int(cdiv(nrows, per));
+  hipLaunchKernelGGL(fold_rows_kernel, dim3(unsigned(cdiv(ncols, 64)), unsigned(g)), dim3(256), 0, s, P, nrows,
+                     ncols, per, out);
+  LBF_KERNEL_CHECK();
+  return g;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Output layer: diff = A_out - Y ; dZ = diff * act'(A_out) * inv_scale ; partial sum(diff^2).
 // src/cuda/network.cuh:97-107 (diff, 0.5*dot(diff,diff)/B, diff*=1/B) and layer.cuh:72 (act').
 // ---------------------------------------------------------------------------------------------
