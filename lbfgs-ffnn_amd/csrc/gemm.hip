@@ -722,11 +722,6 @@ namespace {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-int env_int(const char *name, int dflt) {
-  const char *e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-
 // NS > 0: the LDS-DMA kernel with NS tile buffers where the shape allows it (FAST shapes, no gathered
 // mn-contiguous operand); otherwise the register-staged kernel (KW k-groups, PF register sets).
 template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int KW = 1, int PF = 1, int NS = 0>

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -86,6 +87,11 @@ private:
 };
 
 inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
+// Integer tuning knob from the environment (read once by the caller's static).
+inline int env_int(const char *name, int dflt) {
+  const char *e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
 
 // Phase timestamps for kernel tuning (debug build only: make ktrace). KT(slot) stores the 100 MHz
 // wall clock from thread 0 of block (0,0,0); lbf_dbg_ktrace() copies the slots to the host.

@@ -500,20 +500,38 @@ void average_slots(hipStream_t s, long long n, const float *W, long long ld, con
 // Partial columns per workgroup: live logical index i -> [S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g]
 // at 6*i..6*i+5 (i < m), then [s.s, s.y, y.y, g.s, g.y, g.g] at 6*m..6*m+5.
 // ---------------------------------------------------------------------------------------------
+// History loads: nontemporal (NT) when the ring is far larger than the 256 MB Infinity Cache, so the
+// once-read stream does not evict what the evaluation keeps there (MI355X_MICROARCH.md nt-weights;
+// profiles/micro/streams.hip: 5.2 -> 5.7 TB/s on the cfg-5 ring).
+template <bool NT>
+__device__ __forceinline__ f32x4 hist_load(const float *p) {
+  const f32x4 *q = reinterpret_cast<const f32x4 *>(p);
+  if constexpr (NT)
+    return __builtin_nontemporal_load(q);
+  else
+    return *q;
+}
+static bool hist_nt(const HistView &h) { return double(2 * h.m) * double(h.ld) * 4.0 > 512.0 * 1024 * 1024; }
+
 static constexpr int GRAM_THREADS = 512;
-static constexpr long long GRAM_MAX_CHUNK = 4096; // 3 x 16 KB of LDS per workgroup
+// Largest chunk per workgroup (3 x chunk x 4 B of LDS); LBF_GRAM_CHUNK overrides (multiple of 1024).
+static long long gram_max_chunk() {
+  static const long long c = std::max(1024, std::min(8192, env_int("LBF_GRAM_CHUNK", 4096))) / 1024 * 1024;
+  return c;
+}
 
 int gram_ncols(int m) { return 6 * m + 6; }
 int gram_nwg(long long n) {
   long long w = cdiv(n, 1024);
   if (w > 2048) w = 2048;
-  long long need = cdiv(n, GRAM_MAX_CHUNK);
+  long long need = cdiv(n, gram_max_chunk());
   if (w < need) w = need;
   return int(w < 1 ? 1 : w);
 }
 static long long gram_chunk(long long n, int nwg) { return cdiv(cdiv(n, nwg), 4) * 4; }
 
 
+template <int U, bool NT>
 __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, long long chunk, double *partials) {
   if (a.h.abort && *a.h.abort) return;
   KT(16);
@@ -581,15 +599,15 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
     const float *V = (v < count ? h.S : h.Y) + (long long)slot * h.ld + e0;
     double ds = 0.0, dy = 0.0, dg = 0.0;
     const int full = len & ~3; // elements in whole 16-B quads
-    for (int i0 = lane * 4; i0 < full; i0 += 256 * 4) { // four independent 16-B loads in flight per lane
-      f32x4 xs[4];
+    for (int i0 = lane * 4; i0 < full; i0 += 256 * U) { // U independent 16-B loads in flight per lane
+      f32x4 xs[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int iu = i0 + 256 * u;
-        xs[u] = iu < full ? *reinterpret_cast<const f32x4 *>(V + iu) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        xs[u] = iu < full ? hist_load<NT>(V + iu) : (f32x4){0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int iu = i0 + 256 * u;
         if (iu < full) {
           const f32x4 s4 = *reinterpret_cast<const f32x4 *>(ls + iu);
@@ -630,7 +648,18 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
   const int nwg = gram_nwg(a.h.n);
   const long long chunk = gram_chunk(a.h.n, nwg);
   const size_t shmem = size_t(3 * chunk) * sizeof(float);
-  hipLaunchKernelGGL(gram_kernel, dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
+  static bool attr_set = false;
+  if (!attr_set && shmem > 64 * 1024) {
+    LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gram_kernel<4, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+    LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gram_kernel<4, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+    attr_set = true;
+  }
+  if (hist_nt(a.h))
+    hipLaunchKernelGGL((gram_kernel<4, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
+  else
+    hipLaunchKernelGGL((gram_kernel<4, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
   LBF_KERNEL_CHECK();
 }
 
@@ -730,6 +759,7 @@ void hist_coef(hipStream_t s, const CoefArgs &a) {
 // History: linear-combination sweep  dir = sum_i cs_i S_i + cy_i Y_i + cg g  (fp64 per element),
 // fused with the trial point x_out = x_in + alpha*dir (and an optional second copy).
 // ---------------------------------------------------------------------------------------------
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
   if (a.h.abort && *a.h.abort) return;
   __shared__ double cs[COEF_MAXK], cy[COEF_MAXK];
@@ -749,10 +779,25 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
   if (e >= h.n) return;
   if (e + 3 < h.n) {
     const f32x4 g4 = *reinterpret_cast<const f32x4 *>(a.g + e);
+    f32x4 x4 = {0.f, 0.f, 0.f, 0.f};
+    if (a.x_out) x4 = *reinterpret_cast<const f32x4 *>(a.x_in + e);
     double acc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = cg * double(g4[j]);
-    for (int i = 0; i < k; ++i) {
+    int i = 0;
+    for (; i + U <= k; i += U) { // 2U independent 16-B loads in flight per lane
+      f32x4 s4[U], y4[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        s4[u] = hist_load<NT>(h.S + (long long)L[i + u] * h.ld + e);
+        y4[u] = hist_load<NT>(h.Y + (long long)L[i + u] * h.ld + e);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += cs[i + u] * double(s4[u][j]) + cy[i + u] * double(y4[u][j]);
+    }
+    for (; i < k; ++i) {
       const f32x4 s4 = *reinterpret_cast<const f32x4 *>(h.S + (long long)L[i] * h.ld + e);
       const f32x4 y4 = *reinterpret_cast<const f32x4 *>(h.Y + (long long)L[i] * h.ld + e);
 #pragma unroll
@@ -763,7 +808,6 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
     for (int j = 0; j < 4; ++j) d4[j] = float(acc[j]);
     if (a.dir) *reinterpret_cast<f32x4 *>(a.dir + e) = d4;
     if (a.x_out) {
-      const f32x4 x4 = *reinterpret_cast<const f32x4 *>(a.x_in + e);
       const f32x4 o4 = x4 + float(alpha) * d4;
       *reinterpret_cast<f32x4 *>(a.x_out + e) = o4;
       if (a.x_out2) *reinterpret_cast<f32x4 *>(a.x_out2 + e) = o4;
@@ -786,7 +830,11 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
 
 void hist_combine(hipStream_t s, const CombineArgs &a) {
   LBF_REQUIRE(a.h.ld % 4 == 0, "history slot stride must be a multiple of 4");
-  hipLaunchKernelGGL(combine_kernel, dim3(unsigned(cdiv(cdiv(a.h.n, 4), 256))), dim3(256), 0, s, a);
+  const dim3 grid(unsigned(cdiv(cdiv(a.h.n, 4), 256)));
+  if (hist_nt(a.h))
+    hipLaunchKernelGGL((combine_kernel<8, true>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((combine_kernel<4, false>), grid, dim3(256), 0, s, a);
   LBF_KERNEL_CHECK();
 }
 

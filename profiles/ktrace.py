@@ -21,7 +21,7 @@ def main():
     from lbfgs_ffnn_amd import _lib  # noqa
     L = _lib.lib()
     ctx = pkg.Context(0)
-    Xh, Yh = pkg.synth_mnist(60000)
+    Xh, Yh = pkg.synth_mnist(int(os.environ.get("KT_N", "60000")))
     X, Y = torch.from_numpy(Xh).cuda(), torch.from_numpy(Yh).cuda()
     net = pkg.Mlp(ctx, [784, 128, 10], ["relu", "linear"])
     P = net.init_params(123, "cpu")
