@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--m", type=int, default=10)
     ap.add_argument("--line-search", type=str, default="wolfe")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--comm1", action="store_true",
+                    help="at N=1, route evaluations through a 1-rank RCCL communicator (the DP code path)")
     ap.add_argument("--cpu-iters", type=int, default=8)
     ap.add_argument("--pmc-json", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
@@ -84,6 +86,8 @@ def main():
         uid = [pkg.Context.unique_id() if rank == 0 else None]
         torch.distributed.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
+    elif a.comm1:
+        ctx.comm_init(1, 0, pkg.Context.unique_id())
     Xh, Yh = pkg.synth_mnist(N, dims[0], dims[-1], 123)
     lo, hi = N * rank // world, N * (rank + 1) // world
     X = torch.from_numpy(Xh[lo:hi]).cuda()
@@ -184,7 +188,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"{a.dims} MLP ({a.acts}), full-batch L-BFGS m={a.m} "
                                    f"({a.line_search} line search, CPU-reference semantics), N={N}",
-                       "global_batch": N, "parallelism": f"dp{world}"},
+                       "global_batch": N,
+                       "parallelism": f"dp{world}" + ("+rccl1" if a.comm1 and world == 1 else "")},
             "grad_eval_gflops": round(gflops, 1),
             "evals_per_iter": round(evals / max(iters_done, 1), 3),
             "roofline": roof,

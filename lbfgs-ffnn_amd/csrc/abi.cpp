@@ -109,11 +109,11 @@ int lbf_comm_init(lbf_ctx *ctx, int nranks, int rank, const char id[128]) {
       (void)ncclCommDestroy(ctx->c.comm);
       ctx->c.comm = nullptr;
     }
-    if (nranks > 1) {
-      ncclUniqueId uid;
-      std::memcpy(&uid, id, sizeof(uid));
-      check_comm(ncclCommInitRank(&ctx->c.comm, nranks, uid, rank), "ncclCommInitRank");
-    }
+    // a 1-rank communicator is created too: it routes evaluations through the data-parallel path
+    // (local reduce -> ncclAllReduce -> tail), the single-GPU test of that path
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    check_comm(ncclCommInitRank(&ctx->c.comm, nranks, uid, rank), "ncclCommInitRank");
     ctx->c.rank = rank;
     ctx->c.nranks = nranks;
   });

@@ -49,7 +49,7 @@ void Profiler::resolve() {
 void Ctx::set_device() const { LBF_HIP(hipSetDevice(device)); }
 
 void Ctx::allreduce(float *buf, size_t count) {
-  if (nranks <= 1 || !comm) return;
+  if (!comm) return;
   ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat, ncclSum, comm, stream);
   if (r != ncclSuccess) throw Error(3, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
 }
@@ -335,7 +335,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
   ra.w = P;
   ra.p = pdir;
   ra.lambda = lambda;
-  ra.dots = ctx_->nranks > 1 ? 0 : 1;
+  ra.dots = ctx_->dp() ? 0 : 1;
   ra.partials = dots_part_.get();
   ra.colpart = colpart_.get();
   ra.sse_part = loss_part_.get();
@@ -375,7 +375,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     // fused optimizer tail (tail.hip); data parallel: local reduce -> all-reduce -> tail over G
     TailArgs ta;
     const float *hilo = nullptr;
-    if (ctx_->nranks > 1) {
+    if (ctx_->dp()) {
       RedAllArgs loc = ra;
       loc.dots = 0;
       {
@@ -429,7 +429,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     return;
   }
   const float *hilo = nullptr;
-  if (ctx_->nranks > 1) {
+  if (ctx_->dp()) {
     {
       ProfScope ps(ctx_, PK_FINAL, 0);
       sse_pack(s, loss_part_.get(), nloss, G + nparams_, ctx_->abort);

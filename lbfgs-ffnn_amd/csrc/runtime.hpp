@@ -48,6 +48,9 @@ struct Ctx {
   PinnedBuf<double> host;
   ~Ctx();
   void set_device() const;
+  // data-parallel evaluation path: taken whenever a communicator exists, including a 1-rank one
+  // (lbf_comm_init(ctx, 1, 0, id)), which is how the RCCL path is exercised on a single GPU
+  bool dp() const { return comm != nullptr; }
   void allreduce(float *buf, size_t count);
 };
 

@@ -1,0 +1,104 @@
+"""The data-parallel evaluation path on ONE GPU, through a 1-rank RCCL communicator.
+
+`lbf_comm_init(ctx, 1, 0, id)` creates a real RCCL communicator, and every evaluation then takes the
+multi-rank route of runtime.cpp (per-rank reduce -> fp32 (hi, lo) loss words -> ncclAllReduce over
+[grad | hi | lo] -> tail / finalize over the reduced buffer) — the code the driver's 2/4/8-GPU bench
+runs, minus the cross-GPU hop. A 1-rank all-reduce is the identity, so the results must equal the
+single-GPU path: gradients bit for bit, losses to the (hi, lo) split's 2^-48, and whole L-BFGS /
+S-LBFGS trajectories with identical line-search decisions.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
+
+
+def host(t):
+    return t.double().cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def dp_ctx(pkg):
+    c = pkg.Context(0)
+    c.comm_init(1, 0, pkg.Context.unique_id())
+    return c
+
+
+def test_allreduce_one_rank_is_identity(dp_ctx):
+    t = torch.arange(1000, dtype=torch.float32, device="cuda") * 0.37
+    ref = t.clone()
+    dp_ctx.allreduce_(t)
+    torch.cuda.synchronize()
+    assert torch.equal(t, ref)
+
+
+@pytest.mark.parametrize("dims,acts", [([784, 128, 10], ["relu", "linear"]),
+                                       ([784, 128, 64, 10], ["relu", "relu", "linear"]),
+                                       ([784, 300, 20], ["relu", "linear"])])
+@pytest.mark.parametrize("N", [257, 7500])
+def test_dp_loss_grad_equals_single(ctx, dp_ctx, pkg, dims, acts, N):
+    Xh, Yh = pkg.synth_mnist(N)
+    X, Y = dev(Xh), dev(Yh)
+    net1 = pkg.Mlp(ctx, dims, acts)
+    netd = pkg.Mlp(dp_ctx, dims, acts)
+    P = net1.init_params(123, "cpu")
+    l1, g1 = net1.loss_grad(P, X, Y, inv_scale=1.0 / N)
+    ld, gd = netd.loss_grad(P, X, Y, inv_scale=1.0 / N)
+    assert torch.equal(g1, gd)
+    assert abs(l1 - ld) <= 1e-12 * abs(l1)
+
+
+@pytest.mark.parametrize("line_search", ["wolfe", "armijo"])
+def test_dp_lbfgs_trajectory_equals_single(ctx, dp_ctx, pkg, line_search):
+    """Speculative L-BFGS with the fused tail over the all-reduced buffer (runtime.cpp DP branch)."""
+    dims, acts = [784, 64, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(2048)
+    out = []
+    for c in (ctx, dp_ctx):
+        net = pkg.Mlp(c, dims, acts)
+        P = net.init_params(7, "cpu")
+        hist, info = pkg.lbfgs_solve(net, P, dev(Xh), dev(Yh), line_search=line_search, m=10, max_iters=30,
+                                     tol=0.0)
+        out.append((hist, info, host(P)))
+    (h1, i1, P1), (hd, idd, Pd) = out
+    assert np.array_equal(h1["ls_trials"], hd["ls_trials"])
+    assert np.array_equal(h1["accepted"], hd["accepted"])
+    r = np.abs(h1["loss"] - hd["loss"]) / np.abs(h1["loss"])
+    assert r.max() <= 1e-9, r
+    assert np.linalg.norm(P1 - Pd) <= 1e-6 * np.linalg.norm(P1)
+
+
+def test_dp_lbfgs_full_size(ctx, dp_ctx, pkg):
+    """cfg-2 shape at an 8-rank shard size (7500 rows), 10 iterations: DP route == single route."""
+    dims, acts = [784, 128, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(60000)
+    X, Y = dev(Xh[:7500]), dev(Yh[:7500])
+    out = []
+    for c in (ctx, dp_ctx):
+        net = pkg.Mlp(c, dims, acts)
+        P = net.init_params(123, "cpu")
+        hist, info = pkg.lbfgs_solve(net, P, X, Y, n_global=7500, m=10, max_iters=10, tol=0.0)
+        out.append(hist)
+    assert np.array_equal(out[0]["ls_trials"], out[1]["ls_trials"])
+    assert np.allclose(out[0]["loss"], out[1]["loss"], rtol=1e-9, atol=0)
+
+
+def test_dp_slbfgs_equals_single(ctx, dp_ctx, pkg):
+    dims, acts = [784, 16, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(512)
+    kw = dict(M=5, L=4, b=32, b_H=16, step=0.02, max_epochs=2, tol=0.0, lam=1e-4)
+    out = []
+    for c in (ctx, dp_ctx):
+        net = pkg.Mlp(c, dims, acts)
+        P = net.init_params(123, "cpu")
+        hist, info = pkg.slbfgs_solve(net, P, dev(Xh), dev(Yh), **kw)
+        out.append((hist, host(P)))
+    (h1, P1), (hd, Pd) = out
+    assert np.array_equal(h1["accepted"], hd["accepted"])
+    assert np.allclose(h1["loss"], hd["loss"], rtol=1e-9, atol=0)
+    assert np.linalg.norm(P1 - Pd) <= 1e-6 * np.linalg.norm(P1)
