@@ -31,7 +31,7 @@ struct HistSmem {
   double dots[6 * COEF_MAXK + 6];
   double gS_l[COEF_MAXK], gY_l[COEF_MAXK], rho_l[COEF_MAXK], alpha_l[COEF_MAXK], c_l[COEF_MAXK];
   int L0[COEF_MAXK + 1], L[COEF_MAXK + 1], inv0[COEF_MAXK + 1];
-  int count0, w, k;
+  int count0, w, k, acc, fslot;
   double rhow;
 };
 
@@ -41,6 +41,10 @@ struct HistStep {
   int want_dir = 1; // -1: force the push (explicit upload), 0: no direction, 1: direction (+ CUDA fallback)
   int iter = 1;
   double dsign = -1.0;
+  // hist_prologue<true> / hist_core<true>: copies of the ring header, rho, SY and YY already staged
+  // in LDS by the caller (the fused tail prefetches them with its first loads). Unused otherwise.
+  const int *ist = nullptr;
+  const double *rho = nullptr, *SY = nullptr, *YY = nullptr;
 };
 
 // Ring slot the next pair is written to.
@@ -54,56 +58,82 @@ __device__ __forceinline__ int hist_write_slot(const int *ist, int m, int policy
 
 __device__ __forceinline__ double hc_wave_sum(double v) { return wave_sum_f64(v); }
 
+// Loads from the step's sources. LDS = true: the HistStep pointers are LDS copies, read with ds_read
+// (a generic pointer would be a flat load, whose wait also drains every global store in flight).
+typedef const __attribute__((address_space(3))) double *hc_lds_dptr;
+typedef const __attribute__((address_space(3))) int *hc_lds_iptr;
+template <bool LDS> __device__ __forceinline__ double hc_ld(const double *p, long long i) {
+  if constexpr (LDS) return ((hc_lds_dptr)p)[i];
+  else return p[i];
+}
+template <bool LDS> __device__ __forceinline__ int hc_ldi(const int *p, int i) {
+  if constexpr (LDS) return ((hc_lds_iptr)p)[i];
+  else return p[i];
+}
+
+// Barriers here are LDS-only (wave.hpp lds_barrier): within a history step no thread reads global
+// memory another thread of the block wrote in the same step (fresh entries come from the dots in LDS).
+//
 // Live order before the step: sm.count0, sm.w (write slot), sm.L0[], sm.inv0[]. Block-wide; ends
-// with __syncthreads. w is the slot the pair was written to (ist[IST_WSLOT] or given).
-__device__ inline void hist_prologue(const HistStep &a, HistSmem &sm, int w) {
+// with a barrier. w is the slot the pair was written to (ist[IST_WSLOT] or given).
+template <bool LDS = false> __device__ inline void hist_prologue(const HistStep &a, HistSmem &sm, int w) {
   const HistView &h = a.h;
   const int t = threadIdx.x, nt = blockDim.x;
+  const int *ist = LDS ? a.ist : h.ist;
   if (t == 0) {
-    sm.count0 = a.reset ? 0 : h.ist[IST_COUNT];
+    sm.count0 = a.reset ? 0 : hc_ldi<LDS>(ist, IST_COUNT);
     sm.w = w;
   }
   for (int i = t; i < h.slots; i += nt) sm.inv0[i] = -1;
-  __syncthreads();
+  lds_barrier();
   for (int i = t; i < sm.count0; i += nt) {
-    const int j = h.ist[IST_ORDER + i];
+    const int j = hc_ldi<LDS>(ist, IST_ORDER + i);
     sm.L0[i] = j;
     sm.L[i] = j;
     sm.inv0[j] = i;
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // Steps B and C (see the file comment). Precondition: hist_prologue done and sm.dots filled, then a
-// __syncthreads. Must be the last phase of the kernel: waves other than 0 return early.
+// barrier. Must be the last phase of the kernel: waves other than 0 return early.
 // sy: sy_cap >= k*k doubles of LDS (SY, plus its transpose when 2*k*k fit); yyl: yy_cap doubles of
 // LDS (the YY block is staged when k*k <= yy_cap).
+//
+// FUSED (the fused tail: sources staged in LDS, want_dir == 1, reset == 0, >= 2 waves): step B only
+// decides, in LDS; the global writes of the new Gram rows, rho and the ring header are made by waves
+// 1.. while wave 0 runs the recurrences, and the live count by wave 0 with the coefficients. A store
+// in flight on wave 0 would stall it at its next vmcnt wait; other waves' stores do not.
+template <bool FUSED = false>
 __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, int sy_cap, double *yyl, int yy_cap) {
+  constexpr bool LDS = FUSED;
   const HistView &h = a.h;
   const int S_ = h.slots, t = threadIdx.x, nt = blockDim.x, lane = t & 63, wave = t >> 6;
   const int count0 = sm.count0, w = sm.w;
   const double *dots = sm.dots;
   const double *self = dots + 6 * h.m;
+  const double *SYsrc = LDS ? a.SY : h.SY, *YYsrc = LDS ? a.YY : h.YY, *rhosrc = LDS ? a.rho : h.rho;
   KT(56);
-  // ---- B: Gram rows of the new pair and the g-dots -> global (consumed by later steps) ----
-  for (int i = t; i < count0; i += nt) {
-    const int j = sm.L0[i];
-    if (a.has_pair && j == w) continue;
-    if (a.has_pair) {
-      h.SS[w * S_ + j] = dots[6 * i + 0];
-      h.SS[j * S_ + w] = dots[6 * i + 0];
-      h.SY[w * S_ + j] = dots[6 * i + 1]; // s_w . y_j
-      h.SY[j * S_ + w] = dots[6 * i + 2]; // s_j . y_w
-      h.YY[w * S_ + j] = dots[6 * i + 3];
-      h.YY[j * S_ + w] = dots[6 * i + 3];
+  // Gram rows of the new pair and the g-dots -> global (consumed by later steps); u / nu: this
+  // thread's index among the writers
+  auto write_rows = [&](int u, int nu) {
+    for (int i = u; i < count0; i += nu) {
+      const int j = sm.L0[i];
+      if (a.has_pair && j == w) continue;
+      if (a.has_pair) {
+        h.SS[w * S_ + j] = dots[6 * i + 0];
+        h.SS[j * S_ + w] = dots[6 * i + 0];
+        h.SY[w * S_ + j] = dots[6 * i + 1]; // s_w . y_j
+        h.SY[j * S_ + w] = dots[6 * i + 2]; // s_j . y_w
+        h.YY[w * S_ + j] = dots[6 * i + 3];
+        h.YY[j * S_ + w] = dots[6 * i + 3];
+      }
+      if (a.has_g) {
+        h.gS[j] = dots[6 * i + 4];
+        h.gY[j] = dots[6 * i + 5];
+      }
     }
-    if (a.has_g) {
-      h.gS[j] = dots[6 * i + 4];
-      h.gY[j] = dots[6 * i + 5];
-    }
-  }
-  if (t == 0) {
-    if (a.has_pair) {
+    if (u == 0 && a.has_pair) {
       h.SS[w * S_ + w] = self[0];
       h.SY[w * S_ + w] = self[1];
       h.YY[w * S_ + w] = self[2];
@@ -112,47 +142,57 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
         h.gY[w] = self[4];
       }
     }
-    if (a.has_g) h.scal[SC_GG] = self[5];
+  };
+  // ---- B ----
+  if constexpr (!FUSED) write_rows(t, nt);
+  if (t == 0) {
+    if (!FUSED && a.has_g) h.scal[SC_GG] = self[5];
     int count = count0;
-    sm.rhow = (a.has_pair && w < S_) ? h.rho[w] : 0.0;
-    if (a.reset) h.ist[IST_COUNT] = 0;
+    sm.rhow = (a.has_pair && w < S_) ? hc_ld<LDS>(rhosrc, w) : 0.0;
+    sm.acc = 0;
+    sm.fslot = -1;
+    if (!FUSED && a.reset) h.ist[IST_COUNT] = 0;
     if (a.has_pair) {
       const double ys = self[1];
-      h.scal[SC_YS] = ys;
       bool acc = (a.policy == POL_SLBFGS) ? fabs(ys) > 1e-10 : ys > 1e-10;
       if (a.want_dir < 0) acc = true; // explicit-history upload (lbf_two_loop): always push
-      h.scal[SC_ACCEPT] = acc ? 1.0 : 0.0;
+      if (!FUSED) {
+        h.scal[SC_YS] = ys;
+        h.scal[SC_ACCEPT] = acc ? 1.0 : 0.0;
+      }
+      sm.acc = acc ? 1 : 0;
       if (acc) {
         sm.rhow = 1.0 / ys;
-        h.rho[w] = sm.rhow;
+        if (!FUSED) h.rho[w] = sm.rhow;
+        int f = -1;
         if (count < h.m) {
           sm.L[count++] = w;
           if (a.policy != POL_CUDA || count < h.m) {
             unsigned long long live[3] = {0ull, 0ull, 0ull}; // next free slot: any of the m+1 not live
             for (int q = 0; q < count; ++q) live[sm.L[q] >> 6] |= 1ull << (sm.L[q] & 63);
-            int f = S_;
+            f = S_;
             for (int b = 0; b < 3 && f == S_; ++b)
               if (~live[b]) f = min(S_, b * 64 + __builtin_ctzll(~live[b]));
-            h.ist[IST_FREE] = f;
           }
         } else {
           const int evicted = sm.L[0];
           for (int q = 0; q + 1 < h.m; ++q) sm.L[q] = sm.L[q + 1];
           sm.L[h.m - 1] = w;
-          if (w != evicted) h.ist[IST_FREE] = evicted;
+          if (w != evicted) f = evicted;
         }
-        for (int q = 0; q < count; ++q) h.ist[IST_ORDER + q] = sm.L[q];
-        h.ist[IST_COUNT] = count;
+        sm.fslot = f;
+        if (!FUSED) {
+          if (f >= 0) h.ist[IST_FREE] = f;
+          for (int q = 0; q < count; ++q) h.ist[IST_ORDER + q] = sm.L[q];
+          h.ist[IST_COUNT] = count;
+        }
       }
     }
-    h.scal[SC_COUNT] = double(count);
+    if (!FUSED) h.scal[SC_COUNT] = double(count);
     sm.k = count;
     KT(57);
   }
-  __syncthreads();
-  KT(58);
-  if (a.want_dir <= 0) return;
-
+  lds_barrier();
   // ---- C1: stage the live quantities ----
   const int k = sm.k;
   const int *L = sm.L, *inv0 = sm.inv0;
@@ -162,7 +202,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
       if (p == w) return dots[6 * inv0[q] + 1];
       if (q == w) return dots[6 * inv0[p] + 2];
     }
-    return h.SY[p * S_ + q];
+    return hc_ld<LDS>(SYsrc, p * S_ + q);
   };
   auto YYv = [&](int p, int q) -> double {
     if (a.has_pair) {
@@ -170,7 +210,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
       if (p == w) return dots[6 * inv0[q] + 3];
       if (q == w) return dots[6 * inv0[p] + 3];
     }
-    return h.YY[p * S_ + q];
+    return hc_ld<LDS>(YYsrc, p * S_ + q);
   };
   const bool yy_lds = k * k <= yy_cap;
   const bool sy_t = 2 * k * k <= sy_cap;
@@ -206,11 +246,27 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
       sm.gS_l[i] = h.gS[j];
       sm.gY_l[i] = h.gY[j];
     }
-    sm.rho_l[i] = fresh ? sm.rhow : h.rho[j];
+    sm.rho_l[i] = fresh ? sm.rhow : hc_ld<LDS>(rhosrc, j);
   }
-  __syncthreads();
+  lds_barrier();
   KT(59);
-  if (wave != 0) return;
+  if (wave != 0) {
+    if constexpr (FUSED) { // the deferred writes of step B (the live count: wave 0, below)
+      const int u = t - 64, nu = nt - 64;
+      write_rows(u, nu);
+      if (u == 0) {
+        if (a.has_pair) {
+          h.scal[SC_YS] = self[1];
+          h.scal[SC_ACCEPT] = sm.acc ? 1.0 : 0.0;
+          if (sm.acc) h.rho[w] = sm.rhow;
+          if (sm.fslot >= 0) h.ist[IST_FREE] = sm.fslot;
+        }
+      }
+      if (sm.acc)
+        for (int q = u; q < sm.k; q += nu) h.ist[IST_ORDER + q] = sm.L[q];
+    }
+    return;
+  }
 
   // ---- C2: the recurrences (wave 0). Lane l owns indices l and l+64: alpha, c and the running
   // sums live in its registers; the step's scalar is broadcast with v_readlane. LDS reads are
@@ -342,7 +398,10 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
     h.coef[2 * S_] = fallback ? -1.0 : ds * gamma;
     h.scal[SC_RESET] = fallback ? 1.0 : 0.0;
     h.scal[SC_GTP] = fallback ? -gg : ds * gTz;
-    if (fallback) {
+    if (FUSED) {
+      h.ist[IST_COUNT] = fallback ? 0 : k;
+      h.scal[SC_COUNT] = fallback ? 0.0 : double(k);
+    } else if (fallback) {
       h.ist[IST_COUNT] = 0;
       h.scal[SC_COUNT] = 0.0;
     }

@@ -28,15 +28,22 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double t_wave_sum(double v) { return wave_sum_f64(v); }
 
+// Barriers are LDS-only (wave.hpp lds_barrier): no thread reads global memory that another thread of
+// its block wrote in the same launch.
+//
 // One 64-column group per block. Wave w owns split stripe w of the slab reduction and history vectors
 // v = w + 4j (v < count: S_{L[v]}, else Y_{L[v-count]}; VPW per wave). Every global load of the block
-// (history values, slabs, operands) is issued before the first use: one round trip, then LDS.
+// (history values, slabs, operands) is issued before the first use: one round trip, then LDS. The
+// block's dots are then reduced out of LDS with four lanes per dot column (16 products each, fp64,
+// then a quad DPP add): no per-vector 64-lane reductions. Rows are stored transposed, [nc][nb], so
+// tail_cols reads each column contiguously.
 template <int VPW>
 __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   const RedAllArgs &ra = a.ra;
   if (ra.abort && *ra.abort) return;
   __shared__ double part[4][RA_COLS];
-  __shared__ float lsv[RA_COLS], lyv[RA_COLS], lgv[RA_COLS];
+  __shared__ float xs[2 * TAIL_MAXM][RA_COLS]; // this group's values of the live history vectors
+  __shared__ float ops[5][RA_COLS];            // s, y, g, p, w
   __shared__ int ist[IST_ORDER + TAIL_MAXM];
   const HistView &h = a.h;
   const int t = threadIdx.x, lane = t & 63, stripe = t >> 6, wave = stripe;
@@ -47,7 +54,7 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
 #endif
   // the ring header in one round trip (count, free slot, order)
   if (t < IST_ORDER + h.m) ist[t] = h.ist[t];
-  __syncthreads();
+  lds_barrier();
   KTB(1);
   const int count0 = ist[IST_COUNT];
   const int w = hist_write_slot(ist, h.m, a.policy, 0);
@@ -98,13 +105,16 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   }
   KT(50);
   part[stripe][lane] = acc;
-  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < VPW; ++j) {
+    const int v = wave + 4 * j;
+    if (v < nvec) xs[v][lane] = vv[j];
+  }
+  lds_barrier();
   KT(51);
   KTB(2);
-  double *row = a.rows + (long long)blockIdx.x * a.nc;
   if (wave == 0) {
     float gv = 0.f, sv = 0.f, yv = 0.f;
-    double sf[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // s.s s.y y.y g.s g.y g.g g.p w.w
     if (live) {
       gv = S.splits > 0 ? float(((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]) : gw;
       if (ra.lambda != 0.0) gv = gv + float(ra.lambda) * wv; // finalize_kernel's update
@@ -115,44 +125,53 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
         h.S[(long long)w * h.ld + e] = sv;
         h.Y[(long long)w * h.ld + e] = yv;
       }
-      const double s = sv, y = yv, g = gv;
-      sf[0] = s * s;
-      sf[1] = s * y;
-      sf[2] = y * y;
-      sf[3] = g * s;
-      sf[4] = g * y;
-      sf[5] = g * g;
-      sf[6] = g * double(pv);
-      sf[7] = double(wv) * double(wv);
     }
-    lsv[lane] = sv;
-    lyv[lane] = yv;
-    lgv[lane] = gv;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const double x = t_wave_sum(sf[q]);
-      if (lane == 0) row[6 * h.m + q] = x;
-    }
+    ops[0][lane] = sv;
+    ops[1][lane] = yv;
+    ops[2][lane] = gv;
+    ops[3][lane] = pv;
+    ops[4][lane] = live ? wv : 0.f;
   }
+  lds_barrier();
   KT(52);
-  __syncthreads();
-  KT(53);
   KTB(3);
-  // ---- Gram sweep of this column group ----
-  const double s = lsv[lane], y = lyv[lane], g = lgv[lane];
+  // ---- dot columns: 4 lanes per column, 16 exact fp64 products each, fixed order ----
+  // history columns 6i + {0..5}: S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g ; then the 8 self columns
+  // s.s s.y y.y g.s g.y g.g g.p w.w at 6m + q.
+  const int nh = 6 * count0, ncu = nh + 8;
+  const int q = t & 3;
+  for (int base = 0; base < 4 * ncu; base += 256) {
+    const int u = (base + t) >> 2;
+    double d = 0.0;
+    int c = -1;
+    if (u < ncu) {
+      const float *A, *B;
+      if (u < nh) {
+        const int i = u / 6, r = u - 6 * i;
+        A = xs[(r & 1) ? count0 + i : i];
+        B = ops[r >> 1];
+        c = u;
+      } else {
+        const int z = u - nh; // (s,s) (s,y) (y,y) (g,s) (g,y) (g,g) (g,p) (w,w)
+        const int ia = (0x42222100 >> (4 * z)) & 0xF, ib = (0x43210110 >> (4 * z)) & 0xF;
+        A = ops[ia];
+        B = ops[ib];
+        c = 6 * h.m + z;
+      }
+      const f32x4 *A4 = reinterpret_cast<const f32x4 *>(A + 16 * q);
+      const f32x4 *B4 = reinterpret_cast<const f32x4 *>(B + 16 * q);
 #pragma unroll
-  for (int j = 0; j < VPW; ++j) {
-    const int v = wave + 4 * j;
-    if (v < nvec) { // wave-uniform
-      const double x = vv[j];
-      const double d0 = t_wave_sum(x * s), d1 = t_wave_sum(x * y), d2 = t_wave_sum(x * g);
-      if (lane == 0) {
-        const int i = v < count0 ? v : v - count0, c = v < count0 ? 0 : 1;
-        row[6 * i + c + 0] = d0; // S_i.s | Y_i.s
-        row[6 * i + c + 2] = d1; // S_i.y | Y_i.y
-        row[6 * i + c + 4] = d2; // S_i.g | Y_i.g
+      for (int k = 0; k < 4; ++k) {
+        const f32x4 x = A4[k], y = B4[k];
+        d += double(x[0]) * double(y[0]);
+        d += double(x[1]) * double(y[1]);
+        d += double(x[2]) * double(y[2]);
+        d += double(x[3]) * double(y[3]);
       }
     }
+    d += dpp_f64<0xB1, 0xF>(d); // quad_perm [1,0,3,2]
+    d += dpp_f64<0x4E, 0xF>(d); // quad_perm [2,3,0,1]: every lane of the quad holds the same sum
+    if (c >= 0 && q == 0) a.rows[(long long)c * a.nb + blockIdx.x] = d;
   }
   KT(54);
   KTB(4);
@@ -161,7 +180,8 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
 #endif
 }
 
-// dots[c] = sum over rows in row order (per-thread strided rows, then a fixed tree).
+// dots[c] = sum over rows in row order (per-thread strided rows, then a fixed tree); rows are stored
+// transposed ([nc][nb]), so each block reads one contiguous column.
 __global__ __launch_bounds__(256) void tail_cols_kernel(const TailArgs a) {
   if (a.ra.abort && *a.ra.abort) return;
   __shared__ double ws[4];
@@ -169,91 +189,131 @@ __global__ __launch_bounds__(256) void tail_cols_kernel(const TailArgs a) {
   const int count0 = a.h.ist[IST_COUNT];
   // only the columns in use (live pairs and the self block)
   if (c < 6 * a.h.m && c >= 6 * count0) return;
+  const double *colp = a.rows + (long long)c * a.nb;
   double v[8];
   double s = 0.0;
   for (int r0 = t; r0 < a.nb; r0 += 256 * 8) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int r = r0 + 256 * u;
-      v[u] = r < a.nb ? a.rows[(long long)r * a.nc + c] : 0.0;
+      v[u] = r < a.nb ? colp[r] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += v[u];
   }
   s = t_wave_sum(s);
   if ((t & 63) == 0) ws[t >> 6] = s;
-  __syncthreads();
+  lds_barrier();
   if (t == 0) a.dots[c] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
 }
 
 constexpr int TF_THREADS = 256;
 
+// One block. Every global value it needs (dot columns, SSE partials, status words, ring header, rho,
+// SY, YY) is requested up front in one round trip and staged in LDS; hist_core then runs from LDS.
+// Wave 0 (decision, then the recurrences) issues no global store until the coefficients: the status
+// block, the host record (system-scope stores to host-mapped memory, whose acknowledgement the
+// sequence word must wait for) and the history step's ring/Gram writes are made by waves 1..3.
 __global__ __launch_bounds__(TF_THREADS) void tail_fin_kernel(const TailArgs a) {
   const RedAllArgs &ra = a.ra;
   if (ra.abort && *ra.abort) return;
-  extern __shared__ double dyn[]; // sy [2*m*m] (SY and its transpose) | yy [m*m]
+  extern __shared__ double dyn[]; // sy [2*m*m] (SY and its transpose) | yy [m*m] | SY, YY [S*S] | rho [S]
   __shared__ HistSmem sm;
   __shared__ double v[4];
-  __shared__ int s_status;
+  __shared__ double s_rec[4]; // loss, tgg, alpha0, accept_prev
+  __shared__ double s_sc[6];  // tgg, tgp, ww, sse, loss, the new f_old
+  __shared__ int s_status, s_ok;
+  __shared__ int ist_l[IST_ORDER + TAIL_MAXM + 4];
   const HistView &h = a.h;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  // ---- status: dots and the SSE (partials on one rank, the all-reduced pair otherwise) ----
-  KT(40);
-  const double *D = a.dots;
-  const int m = h.m;
-  {
-    double sse = 0.0;
-    if (!a.hilo)
-      for (int r = t; r < ra.nsse; r += TF_THREADS) sse += ra.sse_part[r];
-    sse = t_wave_sum(sse);
-    if (lane == 0) v[wave] = sse;
-  }
-  __syncthreads();
+  const int m = h.m, S_ = h.slots;
+  double *SYp = dyn + 3 * m * m, *YYp = SYp + S_ * S_, *rhop = YYp + S_ * S_;
   double *sc = h.scal;
+  KT(40);
+  // ---- prefetch (one round trip) ----
+  double sse = 0.0;
+  if (!a.hilo)
+    for (int r = t; r < ra.nsse; r += TF_THREADS) sse += ra.sse_part[r];
+  for (int q = t; q < a.nc; q += TF_THREADS) sm.dots[q] = a.dots[q];
+  for (int i = t; i < S_ * S_; i += TF_THREADS) {
+    SYp[i] = h.SY[i];
+    YYp[i] = h.YY[i];
+  }
+  if (t < S_) rhop[t] = h.rho[t];
+  if (t < IST_ORDER + m) ist_l[t] = h.ist[t];
+  double gfo = 0.0, fold = 0.0, alpha0 = 0.0, accept_prev = 0.0;
   if (t == 0) {
-    const double sse = a.hilo ? (double(a.hilo[0]) + double(a.hilo[1])) : ((v[0] + v[1]) + v[2]) + v[3];
+    gfo = sc[SC_GTP];
+    fold = a.ls.armijo ? sc[SC_FOLDF] : sc[SC_FOLD];
+    alpha0 = sc[SC_ALPHA0];
+    accept_prev = sc[SC_ACCEPT];
+  }
+  sse = t_wave_sum(sse);
+  if (lane == 0) v[wave] = sse;
+  KT(45);
+  lds_barrier();
+  KT(46);
+  if (t == 0) { // decide (LDS only: wave 0 issues no global store before the recurrences)
+    const double *D = sm.dots;
+    const double sse_t = a.hilo ? (double(a.hilo[0]) + double(a.hilo[1])) : ((v[0] + v[1]) + v[2]) + v[3];
     const double tgg = D[6 * m + 5], tgp = D[6 * m + 6], ww = D[6 * m + 7];
-    double loss = 0.5 * sse * ra.inv_scale;
+    double loss = 0.5 * sse_t * ra.inv_scale;
     if (ra.lambda != 0.0) loss += 0.5 * ra.lambda * ww;
-    sc[SC_TGG] = tgg;
-    sc[SC_TGP] = tgp;
-    sc[SC_WW] = ww;
-    sc[SC_SSE] = sse;
-    sc[SC_LOSS] = loss;
+    s_sc[0] = tgg;
+    s_sc[1] = tgp;
+    s_sc[2] = ww;
+    s_sc[3] = sse_t;
+    s_sc[4] = loss;
     // ---- the line-search decision (ls_ctl_kernel's rule, vec_kernels.hip) ----
     const LsCtlArgs &L = a.ls;
-    const double fn = loss, gfo = sc[SC_GTP];
+    const double fn = loss;
     bool ok, conv;
     if (!L.armijo) {
-      const double fold = L.host_fold ? L.fold : sc[SC_FOLD];
-      ok = L.first || (!(fn > __dadd_rn(fold, __dmul_rn(__dmul_rn(L.c1, 1.0), gfo))) && !(tgp < __dmul_rn(L.c2, gfo)));
+      const double fo = L.host_fold ? L.fold : fold;
+      ok = L.first || (!(fn > __dadd_rn(fo, __dmul_rn(__dmul_rn(L.c1, 1.0), gfo))) && !(tgp < __dmul_rn(L.c2, gfo)));
       conv = sqrt(tgg) < L.tol;
-      if (ok) sc[SC_FOLD] = fn;
+      s_sc[5] = fn;
     } else {
-      const float foldf = L.host_fold ? L.foldf : float(sc[SC_FOLDF]);
+      const float foldf = L.host_fold ? L.foldf : float(fold);
       const float lnew = float(fn), gdp = float(gfo);
       ok = lnew <= __fadd_rn(foldf, __fmul_rn(__fmul_rn(float(L.c1), L.alphaf), gdp));
       conv = float(sqrt(tgg)) < float(L.tol);
-      if (ok) sc[SC_FOLDF] = double(lnew);
+      s_sc[5] = double(lnew);
     }
-    const int status = !ok ? SPEC_REJECT : (conv ? SPEC_CONVERGED : SPEC_ACCEPT);
-    if (status != SPEC_ACCEPT) *L.abort = 1;
-    SpecRecord *r = L.rec;
-    const double alpha0 = sc[SC_ALPHA0], accept_prev = sc[SC_ACCEPT];
-    __hip_atomic_store(&r->loss, fn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&r->tgg, tgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&r->alpha0, alpha0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&r->accept_prev, accept_prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&r->status, status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(&r->seq, L.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    s_status = status;
+    s_ok = ok ? 1 : 0;
+    s_rec[0] = fn;
+    s_rec[1] = tgg;
+    s_rec[2] = alpha0;
+    s_rec[3] = accept_prev;
+    s_status = !ok ? SPEC_REJECT : (conv ? SPEC_CONVERGED : SPEC_ACCEPT);
   }
-  __syncthreads();
+  lds_barrier();
   KT(41);
+  // status block, abort flag and host record: payload, then (after its acknowledgement) the
+  // sequence word. Written by wave 1 after its last barrier (see hist_core<true>).
+  auto publish = [&]() {
+    sc[SC_TGG] = s_sc[0];
+    sc[SC_TGP] = s_sc[1];
+    sc[SC_WW] = s_sc[2];
+    sc[SC_SSE] = s_sc[3];
+    sc[SC_LOSS] = s_sc[4];
+    if (s_ok) sc[a.ls.armijo ? SC_FOLDF : SC_FOLD] = s_sc[5];
+    if (s_status != SPEC_ACCEPT) *a.ls.abort = 1;
+    SpecRecord *r = a.ls.rec;
+    __hip_atomic_store(&r->loss, s_rec[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->tgg, s_rec[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->alpha0, s_rec[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->accept_prev, s_rec[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->status, s_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&r->seq, a.ls.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  };
   // Rejected: history untouched (the host finishes the line search). Converged: the solver stops
   // before the next history update, exactly like the host-driven loop.
-  if (s_status != SPEC_ACCEPT) return;
+  if (s_status != SPEC_ACCEPT) {
+    if (t == 64) publish();
+    return;
+  }
   // ---- accepted: push the pair, coefficients of the next direction ----
   HistStep st;
   st.h = h;
@@ -264,14 +324,16 @@ __global__ __launch_bounds__(TF_THREADS) void tail_fin_kernel(const TailArgs a) 
   st.want_dir = 1;
   st.iter = a.iter_next;
   st.dsign = -1.0;
-  hist_prologue(st, sm, h.ist[IST_WSLOT]);
+  st.ist = ist_l;
+  st.rho = rhop;
+  st.SY = SYp;
+  st.YY = YYp;
+  hist_prologue<true>(st, sm, ist_l[IST_WSLOT]);
   KT(42);
-  const int count0 = sm.count0;
-  for (int q = t; q < 6 * count0; q += TF_THREADS) sm.dots[q] = D[q];
-  if (t < 6) sm.dots[6 * m + t] = D[6 * m + t];
-  __syncthreads();
   KT(43);
-  hist_core(st, sm, dyn, 2 * m * m, dyn + 2 * m * m, m * m);
+  hist_core<true>(st, sm, dyn, 2 * m * m, dyn + 2 * m * m, m * m);
+  // waves 1..3 leave hist_core after its deferred stores; wave 1 then publishes
+  if (t == 64) publish();
   KT(44);
 }
 
@@ -298,7 +360,7 @@ void tail_reduce(hipStream_t s, const TailArgs &a) {
 }
 
 void tail_fin(hipStream_t s, const TailArgs &a) {
-  const size_t shmem = size_t(3) * a.h.m * a.h.m * sizeof(double);
+  const size_t shmem = (size_t(3) * a.h.m * a.h.m + 2 * size_t(a.h.slots) * a.h.slots + a.h.slots) * sizeof(double);
   hipLaunchKernelGGL(tail_fin_kernel, dim3(1), dim3(TF_THREADS), shmem, s, a);
   LBF_KERNEL_CHECK();
 }

@@ -34,4 +34,10 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return lane_f64(v, 63);
 }
 
+// Workgroup barrier that orders LDS only. __syncthreads() carries a workgroup-scope release, which on
+// gfx950 means s_waitcnt vmcnt(0): every global store the wave has in flight must be acknowledged
+// (~1 us) before the barrier. Where no thread reads, after the barrier, global memory written before
+// it by another thread of the block, the LDS wait is all the barrier has to order.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 } // namespace lbf

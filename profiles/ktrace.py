@@ -12,7 +12,7 @@ import torch  # noqa: E402,F401
 import __graft_entry__  # noqa: E402
 
 GROUPS = {"hist_step": range(0, 9), "gram(block0)": range(16, 20), "reduce_fin": range(32, 36),
-          "tail_fin": range(40, 45), "tail_reduce(block0)": range(48, 55),
+          "tail_fin": [40, 45, 46, 41, 42, 43, 44], "tail_reduce(block0)": range(48, 55),
           "hist_core(in tail_fin)": range(56, 63)}
 
 
