@@ -280,6 +280,7 @@ void hist_coef(hipStream_t s, const CoefArgs &a);
 // direction's coefficients (hist_core.hpp). Row layout (nc = 6m + 8 doubles): the Gram sweep's
 // columns (see hist_core.hpp), then g.p and w.w.
 constexpr int TAIL_MAXM = 32;
+constexpr int TAIL_COLS = 128; // columns per tail_reduce block
 struct TailArgs {
   RedAllArgs ra;                // every segment with parts == 1; ra.w = x_t, ra.p = direction
   const float *hilo = nullptr;  // data parallel: all-reduced SSE (hi, lo) behind the gradient
@@ -291,7 +292,8 @@ struct TailArgs {
   LsCtlArgs ls;
   double *rows = nullptr; // [nb][nc]
   double *dots = nullptr; // [nc]
-  int nb = 0, nc = 0; // nb = ra.ncg blocks (one 64-column group each)
+  int tcg0[RA_MAXSEG] = {}; // first TAIL_COLS column group of each segment
+  int nb = 0, nc = 0;       // nb: TAIL_COLS column groups over all segments (one block each)
 };
 void tail_reduce(hipStream_t s, const TailArgs &a); // tail_reduce + tail_cols launches
 void tail_fin(hipStream_t s, const TailArgs &a);    // one block

@@ -404,7 +404,11 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     ta.iter_next = tf->iter_next;
     ta.ls = tf->ls;
     ta.nc = 6 * tf->h.m + 8;
-    ta.nb = ra.ncg; // one 64-column group per block: latency-bound work wants every CU busy
+    ta.nb = 0; // one TAIL_COLS column group per block: latency-bound work wants every CU busy
+    for (int l = 0; l < nl; ++l) {
+      ta.tcg0[l] = ta.nb;
+      ta.nb += int(cdiv(ra.seg[l].count, (long long)TAIL_COLS));
+    }
     trows_.ensure(size_t(ta.nb) * ta.nc);
     tdots_.ensure(size_t(ta.nc));
     ta.rows = trows_.get();

@@ -31,22 +31,26 @@ __device__ __forceinline__ double t_wave_sum(double v) { return wave_sum_f64(v);
 // Barriers are LDS-only (wave.hpp lds_barrier): no thread reads global memory that another thread of
 // its block wrote in the same launch.
 //
-// One 64-column group per block. Wave w owns split stripe w of the slab reduction and history vectors
-// v = w + 4j (v < count: S_{L[v]}, else Y_{L[v-count]}; VPW per wave). Every global load of the block
-// (history values, slabs, operands) is issued before the first use: one round trip, then LDS. The
-// block's dots are then reduced out of LDS with four lanes per dot column (16 products each, fp64,
-// then a quad DPP add): no per-vector 64-lane reductions. Rows are stored transposed, [nc][nb], so
-// tail_cols reads each column contiguously.
+// One TAIL_COLS (128) column group per block, lane l owning columns l and l + 64 of it. Wave w owns
+// split stripe w of the slab reduction and history vectors v = w + 4j (v < count: S_{L[v]}, else
+// Y_{L[v-count]}; VPW per wave). Every global load of the block (history values, slabs, operands)
+// is issued before the first use: one round trip, then LDS. The block's dots are then reduced out of
+// LDS with four lanes per dot column (32 exact fp64 products each, then a quad DPP add): no
+// per-vector 64-lane reductions. Rows are stored transposed, [nc][nb], so tail_cols reads each
+// column contiguously. 128-column groups halve the grid (n = 101,770: 796 blocks), which keeps every
+// block resident at once (this kernel's SGPR count admits 6 blocks per CU).
 template <int VPW>
 __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
+  constexpr int TC = TAIL_COLS, C = TAIL_COLS / 64;
   const RedAllArgs &ra = a.ra;
   if (ra.abort && *ra.abort) return;
-  __shared__ double part[4][RA_COLS];
-  __shared__ float xs[2 * TAIL_MAXM][RA_COLS]; // this group's values of the live history vectors
-  __shared__ float ops[5][RA_COLS];            // s, y, g, p, w
+  __shared__ double part[4][TC];
+  __shared__ float xs[2 * TAIL_MAXM][TC]; // this group's values of the live history vectors
+  __shared__ float ops[5][TC];            // s, y, g, p, w
   __shared__ int ist[IST_ORDER + TAIL_MAXM];
   const HistView &h = a.h;
-  const int t = threadIdx.x, lane = t & 63, stripe = t >> 6, wave = stripe;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6), stripe = wave; // uniform: scalar branches
   KT(48);
   KTB(0);
 #ifdef LBF_KTRACE
@@ -56,86 +60,115 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   if (t < IST_ORDER + h.m) ist[t] = h.ist[t];
   lds_barrier();
   KTB(1);
-  const int count0 = ist[IST_COUNT];
-  const int w = hist_write_slot(ist, h.m, a.policy, 0);
+  // wave-uniform scalars (SGPRs): the loads below then need no per-lane select or branch
+  const int count0 = __builtin_amdgcn_readfirstlane(ist[IST_COUNT]);
+  const int w = __builtin_amdgcn_readfirstlane(hist_write_slot(ist, h.m, a.policy, 0));
   if (blockIdx.x == 0 && t == 0) h.ist[IST_WSLOT] = w;
   const int nvec = 2 * count0;
   const int cg = blockIdx.x;
   int si = 0;
-  while (si + 1 < ra.nseg && ra.seg[si + 1].cg0 <= cg) ++si;
+  while (si + 1 < ra.nseg && a.tcg0[si + 1] <= cg) ++si;
   const RedSeg &S = ra.seg[si];
-  const long long col = (long long)(cg - S.cg0) * RA_COLS + lane;
-  const bool live = col < S.count;
-  const long long e = S.goff + col;
+  // Every load below is unconditional, from an address clamped into the arrays, and masked after:
+  // a per-element "load or zero" select makes the compiler branch around each load and wait for it
+  // (one dependent round trip per element).
+  long long col[C], colc[C], e[C];
+  bool live[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    col[c] = (long long)(cg - a.tcg0[si]) * TC + lane + 64 * c;
+    live[c] = col[c] < S.count;
+    colc[c] = live[c] ? col[c] : S.count - 1;
+    e[c] = S.goff + colc[c];
+  }
   // ---- history values of this wave's vectors (in flight while the slabs load) ----
-  float vv[VPW];
+  const float *Sb = h.S, *Yb = h.Y;
+  float vv[VPW][C];
+  unsigned zero_mask = 0; // bit j: vector j of this wave is the slot being overwritten (not live)
 #pragma unroll
   for (int j = 0; j < VPW; ++j) {
-    const int v = wave + 4 * j;
-    vv[j] = 0.0f;
-    if (v < nvec && live) {
-      const int slot = ist[IST_ORDER + (v < count0 ? v : v - count0)];
-      if (!(a.has_pair && slot == w)) vv[j] = (v < count0 ? h.S : h.Y)[(long long)slot * h.ld + e];
-    }
+    const int v = wave + 4 * j; // wave-uniform
+    const int vi = v < nvec ? v : 0;
+    const int slot = __builtin_amdgcn_readfirstlane(ist[IST_ORDER + (vi < count0 ? vi : vi - count0)]);
+    const float *base = (vi < count0 ? Sb : Yb) + (long long)slot * h.ld;
+#pragma unroll
+    for (int c = 0; c < C; ++c) vv[j][c] = base[e[c]];
+    if (v >= nvec || (a.has_pair && slot == w)) zero_mask |= 1u << j;
   }
-  // ---- operands (wave 0) ----
-  float wv = 0.f, xp = 0.f, gp = 0.f, pv = 0.f, gw = 0.f;
-  if (wave == 0 && live) {
-    wv = ra.w[e];
-    if (a.has_pair) {
-      xp = a.x_prev[e];
-      gp = a.g_prev[e];
-    }
-    if (ra.p) pv = ra.p[e];
-    if (S.splits == 0) gw = ra.G[e];
+  // ---- operands ----
+  // every wave loads them (same lines as wave 0's: L1 hits) so no branch merge forces an early wait;
+  // null operands read w instead and are masked where used
+  float wv[C], xp[C], gp[C], pv[C], gw[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    wv[c] = ra.w[e[c]];
+    xp[c] = (a.x_prev ? a.x_prev : ra.w)[e[c]];
+    gp[c] = (a.g_prev ? a.g_prev : ra.w)[e[c]];
+    pv[c] = (ra.p ? ra.p : ra.w)[e[c]];
+    gw[c] = ra.G[e[c]];
   }
   KT(49);
-  // ---- gradient column: split-K slabs in split order (4 stripes) ----
-  double acc = 0.0;
-  if (live && S.splits > 0) {
-    const float *src = S.slab + col;
-    for (int k = stripe; k < S.splits; k += 4 * 16) { // sixteen independent loads in flight
-      float x[16];
+  // ---- gradient columns: split-K slabs in split order (4 stripes) ----
+  double acc[C];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) x[u] = k + 4 * u < S.splits ? src[(long long)(k + 4 * u) * S.stride] : 0.0f;
+  for (int c = 0; c < C; ++c) acc[c] = 0.0;
+  if (S.splits > 0) {
+    constexpr int U = 8; // loads per column in flight per round (clamped duplicates past the end)
+    for (int k = stripe; k < S.splits; k += 4 * U) {
+      float x[U][C];
 #pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (k + 4 * u < S.splits) acc += double(x[u]);
+      for (int u = 0; u < U; ++u) {
+        const long long sp = min(k + 4 * u, S.splits - 1);
+#pragma unroll
+        for (int c = 0; c < C; ++c) x[u][c] = S.slab[colc[c] + sp * S.stride];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          if (k + 4 * u < S.splits) acc[c] += double(x[u][c]);
     }
   }
   KT(50);
-  part[stripe][lane] = acc;
+#pragma unroll
+  for (int c = 0; c < C; ++c) part[stripe][lane + 64 * c] = acc[c];
 #pragma unroll
   for (int j = 0; j < VPW; ++j) {
     const int v = wave + 4 * j;
-    if (v < nvec) xs[v][lane] = vv[j];
+    if (v < nvec)
+#pragma unroll
+      for (int c = 0; c < C; ++c) xs[v][lane + 64 * c] = ((zero_mask >> j) & 1u) || !live[c] ? 0.0f : vv[j][c];
   }
   lds_barrier();
   KT(51);
   KTB(2);
   if (wave == 0) {
-    float gv = 0.f, sv = 0.f, yv = 0.f;
-    if (live) {
-      gv = S.splits > 0 ? float(((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]) : gw;
-      if (ra.lambda != 0.0) gv = gv + float(ra.lambda) * wv; // finalize_kernel's update
-      if (S.splits > 0 || ra.lambda != 0.0) ra.G[e] = gv;
-      if (a.has_pair) {
-        sv = wv - xp;
-        yv = gv - gp;
-        h.S[(long long)w * h.ld + e] = sv;
-        h.Y[(long long)w * h.ld + e] = yv;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int q = lane + 64 * c;
+      float gv = 0.f, sv = 0.f, yv = 0.f;
+      if (live[c]) {
+        gv = S.splits > 0 ? float(((part[0][q] + part[1][q]) + part[2][q]) + part[3][q]) : gw[c];
+        if (ra.lambda != 0.0) gv = gv + float(ra.lambda) * wv[c]; // finalize_kernel's update
+        if (S.splits > 0 || ra.lambda != 0.0) ra.G[e[c]] = gv;
+        if (a.has_pair) {
+          sv = wv[c] - xp[c];
+          yv = gv - gp[c];
+          h.S[(long long)w * h.ld + e[c]] = sv;
+          h.Y[(long long)w * h.ld + e[c]] = yv;
+        }
       }
+      ops[0][q] = sv;
+      ops[1][q] = yv;
+      ops[2][q] = gv;
+      ops[3][q] = ra.p ? pv[c] : 0.f;
+      ops[4][q] = live[c] ? wv[c] : 0.f;
     }
-    ops[0][lane] = sv;
-    ops[1][lane] = yv;
-    ops[2][lane] = gv;
-    ops[3][lane] = pv;
-    ops[4][lane] = live ? wv : 0.f;
   }
   lds_barrier();
   KT(52);
   KTB(3);
-  // ---- dot columns: 4 lanes per column, 16 exact fp64 products each, fixed order ----
+  // ---- dot columns: 4 lanes per column, 32 exact fp64 products each, fixed order ----
   // history columns 6i + {0..5}: S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g ; then the 8 self columns
   // s.s s.y y.y g.s g.y g.g g.p w.w at 6m + q.
   const int nh = 6 * count0, ncu = nh + 8;
@@ -158,10 +191,10 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
         B = ops[ib];
         c = 6 * h.m + z;
       }
-      const f32x4 *A4 = reinterpret_cast<const f32x4 *>(A + 16 * q);
-      const f32x4 *B4 = reinterpret_cast<const f32x4 *>(B + 16 * q);
+      const f32x4 *A4 = reinterpret_cast<const f32x4 *>(A + (TC / 4) * q);
+      const f32x4 *B4 = reinterpret_cast<const f32x4 *>(B + (TC / 4) * q);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < TC / 16; ++k) {
         const f32x4 x = A4[k], y = B4[k];
         d += double(x[0]) * double(y[0]);
         d += double(x[1]) * double(y[1]);

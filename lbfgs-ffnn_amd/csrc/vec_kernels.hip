@@ -828,8 +828,68 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
   }
 }
 
+// Small-n form (the latency-bound regime: n up to a few million, k <= 32): one element per lane so
+// the grid covers every CU, the ring header and coefficients read lane-distributed (no LDS, no
+// barrier) and broadcast with v_readlane, and every history load of the lane issued at once: one
+// round trip for the header, one for the data.
+template <int KMAX>
+__global__ __launch_bounds__(256) void combine_small_kernel(const CombineArgs a) {
+  if (a.h.abort && *a.h.abort) return;
+  const HistView &h = a.h;
+  const int S_ = h.slots, lane = threadIdx.x & 63;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = e < h.n;
+  // independent of the header: in flight with it
+  const float gv = in ? a.g[e] : 0.f;
+  const float xv = (in && a.x_out) ? a.x_in[e] : 0.f;
+  const int k = h.ist[IST_COUNT];
+  int Lr = 0;
+  double csr = 0.0, cyr = 0.0;
+  if (lane < k) {
+    Lr = h.ist[IST_ORDER + lane];
+    csr = h.coef[lane];
+    cyr = h.coef[S_ + lane];
+  }
+  const double cg = h.coef[2 * S_];
+  const double alpha = a.alpha_from_state ? h.scal[SC_ALPHA0] : a.alpha;
+  float sv[KMAX], yv[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    sv[i] = yv[i] = 0.f;
+    if (i < k) { // wave-uniform
+      const long long off = (long long)__builtin_amdgcn_readlane(Lr, i) * h.ld + e;
+      if (in) {
+        sv[i] = h.S[off];
+        yv[i] = h.Y[off];
+      }
+    }
+  }
+  double acc = cg * double(gv);
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i)
+    if (i < k) acc += lane_f64(csr, i) * double(sv[i]) + lane_f64(cyr, i) * double(yv[i]);
+  if (!in) return;
+  const float d = float(acc);
+  if (a.dir) a.dir[e] = d;
+  if (a.x_out) {
+    const float o = xv + float(alpha) * d;
+    a.x_out[e] = o;
+    if (a.x_out2) a.x_out2[e] = o;
+  }
+}
+
 void hist_combine(hipStream_t s, const CombineArgs &a) {
   LBF_REQUIRE(a.h.ld % 4 == 0, "history slot stride must be a multiple of 4");
+  static const int small_max = env_int("LBF_COMBINE_SMALL_N", 1 << 21);
+  if (a.h.n <= small_max && a.h.m <= 32) {
+    const dim3 g1(unsigned(cdiv(a.h.n, 256)));
+    if (a.h.m <= 16)
+      hipLaunchKernelGGL(combine_small_kernel<16>, g1, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(combine_small_kernel<32>, g1, dim3(256), 0, s, a);
+    LBF_KERNEL_CHECK();
+    return;
+  }
   const dim3 grid(unsigned(cdiv(cdiv(a.h.n, 4), 256)));
   if (hist_nt(a.h))
     hipLaunchKernelGGL((combine_kernel<8, true>), grid, dim3(256), 0, s, a);
