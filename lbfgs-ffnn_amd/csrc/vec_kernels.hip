@@ -837,31 +837,25 @@ __global__ __launch_bounds__(256) void combine_small_kernel(const CombineArgs a)
   if (a.h.abort && *a.h.abort) return;
   const HistView &h = a.h;
   const int S_ = h.slots, lane = threadIdx.x & 63;
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = e < h.n;
+  const long long e0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = e0 < h.n;
+  const long long e = in ? e0 : h.n - 1; // loads are unconditional (clamped), results masked
   // independent of the header: in flight with it
-  const float gv = in ? a.g[e] : 0.f;
-  const float xv = (in && a.x_out) ? a.x_in[e] : 0.f;
-  const int k = h.ist[IST_COUNT];
-  int Lr = 0;
-  double csr = 0.0, cyr = 0.0;
-  if (lane < k) {
-    Lr = h.ist[IST_ORDER + lane];
-    csr = h.coef[lane];
-    cyr = h.coef[S_ + lane];
-  }
+  const float gv = a.g[e];
+  const float xv = (a.x_out ? a.x_in : a.g)[e];
+  const int lk = lane < h.m ? lane : 0; // header entries read without waiting for the count
+  const int k = __builtin_amdgcn_readfirstlane(h.ist[IST_COUNT]);
+  const int Lr = h.ist[IST_ORDER + lk];
+  const double csr = h.coef[lk], cyr = h.coef[S_ + lk];
   const double cg = h.coef[2 * S_];
   const double alpha = a.alpha_from_state ? h.scal[SC_ALPHA0] : a.alpha;
   float sv[KMAX], yv[KMAX];
+  if (k > 0) {
 #pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    sv[i] = yv[i] = 0.f;
-    if (i < k) { // wave-uniform
-      const long long off = (long long)__builtin_amdgcn_readlane(Lr, i) * h.ld + e;
-      if (in) {
-        sv[i] = h.S[off];
-        yv[i] = h.Y[off];
-      }
+    for (int i = 0; i < KMAX; ++i) { // every load issued before the first use
+      const long long off = (long long)__builtin_amdgcn_readlane(Lr, i < k ? i : k - 1) * h.ld + e;
+      sv[i] = h.S[off];
+      yv[i] = h.Y[off];
     }
   }
   double acc = cg * double(gv);
