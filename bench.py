@@ -47,23 +47,31 @@ def parse():
     ap.add_argument("--comm1", action="store_true",
                     help="at N=1, route evaluations through a 1-rank RCCL communicator (the DP code path)")
     ap.add_argument("--cpu-iters", type=int, default=8)
+    ap.add_argument("--cpu-samples", type=int, default=0,
+                    help="rows of the CPU-baseline sample (0: all rows up to 60000, else 2000; scaled to N)")
+    ap.add_argument("--data", choices=["mnist", "regression"], default="mnist",
+                    help="mnist: SURVEY §8(d) MNIST-shaped classes (configs 1-4); regression: config 5's "
+                         "device-generated X ~ N(0,1), y = tanh(v.x/64) + 0.01 e")
     ap.add_argument("--pmc-json", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
 
-def cpu_baseline(dims, acts, N, m, iters):
+def cpu_baseline(dims, acts, N, m, iters, data, rows):
     """The oracle (fp64 C++/OpenMP restatement of the reference CPU path, literal call pattern incl. its
-    redundant f/grad re-evaluations) timed on this host; bounded sample of the same workload."""
+    redundant f/grad re-evaluations) timed on this host; bounded sample of the same workload: `rows` of
+    the N samples (the full-batch cost is linear in N, so the rate is scaled by rows / N)."""
     O = __graft_entry__.load_oracle()
     O.lib()
-    X, Y = O.synth_mnist(N)
+    X, Y = O.synth_mnist(rows, dims[0], dims[-1]) if data == "mnist" else O.synth_regression(rows, dims[0])
     net = O.Net(dims, acts)
     P = net.init_cpu(123)
     _, rec, info = net.lbfgs_wolfe(P, X, Y, m=m, max_iters=iters)
     ms = info["ms"]
-    return dict(value=round(iters / (ms / 1e3), 4), unit="iters/s", cores=O.num_threads(), kind="port",
-                sample=f"{iters} L-BFGS iterations (Wolfe, m={m}) of the {'-'.join(map(str, dims))} MLP at "
-                       f"N={N}, fp64 oracle (oracle/oracle.hpp) with the reference's f/grad call pattern "
+    scale = rows / N
+    return dict(value=round(iters / (ms / 1e3) * scale, 6), unit="iters/s", cores=O.num_threads(), kind="port",
+                sample=f"{iters} L-BFGS iterations (Wolfe, m={m}) of the {'-'.join(map(str, dims))} MLP on "
+                       f"{rows} of the N={N} rows{f' (rate scaled by {rows}/{N})' if rows != N else ''}, fp64 "
+                       f"oracle (oracle/oracle.hpp) with the reference's f/grad call pattern "
                        f"({info['n_fwd']} forward, {info['n_bwd']} backward passes), "
                        f"{O.num_threads()} OpenMP threads, {ms / 1e3:.1f} s")
 
@@ -88,10 +96,14 @@ def main():
         ctx.comm_init(world, rank, uid[0])
     elif a.comm1:
         ctx.comm_init(1, 0, pkg.Context.unique_id())
-    Xh, Yh = pkg.synth_mnist(N, dims[0], dims[-1], 123)
     lo, hi = N * rank // world, N * (rank + 1) // world
-    X = torch.from_numpy(Xh[lo:hi]).cuda()
-    Y = torch.from_numpy(Yh[lo:hi]).cuda()
+    if a.data == "mnist":
+        Xh, Yh = pkg.synth_mnist(N, dims[0], dims[-1], 123)
+        X = torch.from_numpy(Xh[lo:hi]).cuda()
+        Y = torch.from_numpy(Yh[lo:hi]).cuda()
+        del Xh, Yh
+    else:  # this rank's shard generated in place
+        X, Y = pkg.synth_regression(ctx, hi - lo, dims[0], row0=lo)
     net = pkg.Mlp(ctx, dims, acts)
     P = net.init_params(123, "cpu")
     torch.cuda.synchronize()
@@ -185,7 +197,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": round(value / REF_GPU_ITERS_PER_S, 3),
             "dtype": "fp32",
-            "data": "synthetic",
+            "data": "synthetic" if a.data == "mnist" else "synthetic (config-5 regression stream, device-generated)",
             "config": {"workload": f"{a.dims} MLP ({a.acts}), full-batch L-BFGS m={a.m} "
                                    f"({a.line_search} line search, CPU-reference semantics), N={N}",
                        "global_batch": N,
@@ -196,7 +208,8 @@ def main():
             "kernel_ms_per_step": {k: round(v[0] / bd_steps, 4) for k, v in sorted(breakdown.items())},
         }
         if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(dims, acts, N, a.m, a.cpu_iters)
+            rows = a.cpu_samples or (N if N <= 60000 else 2000)
+            out["cpu_baseline"] = cpu_baseline(dims, acts, N, a.m, a.cpu_iters, a.data, min(rows, N))
         print(json.dumps(out), flush=True)
     run.close()
     if world > 1:

@@ -189,6 +189,12 @@ int lbf_memcpy(lbf_ctx *ctx, void *dst, const void *src, size_t bytes, int kind)
 int lbf_synth_mnist(long long N, int In, int classes, unsigned seed, float *h_X, float *h_Y);
 /* Partial Fisher-Yates minibatch draws from one mt19937(seed) (s_lbfgs.hpp:141-160). */
 int lbf_sample_indices(long long N, int b, unsigned seed, int calls, long long *h_out);
+/* BASELINE config 5's synthetic regression data, generated on the device (no reference counterpart:
+ * the reference reads MNIST files): X ~ N(0,1) [N][In], y = tanh(v.x / 64) + 0.01 e [N][1]; stream
+ * defined in lbfgs-ffnn_amd/csrc/synth.hip, restated in oracle/oracle.py. Writes rows [row0, row0+N)
+ * of the stream (a data-parallel shard). Synchronises. */
+int lbf_synth_regression(lbf_ctx *ctx, long long row0, long long N, int In, unsigned seed_x, unsigned seed_t,
+                         float *d_X, float *d_Y);
 
 #ifdef __cplusplus
 }

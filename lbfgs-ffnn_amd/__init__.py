@@ -7,6 +7,6 @@ The directory name contains a hyphen, so load it with :func:`load` from the repo
 """
 from ._lib import LIB_PATH, LbfError, lib  # noqa: F401
 from .engine import (Context, History, LbfgsRun, Mlp, grad_flops_per_sample, init_params_host, lbfgs_solve,  # noqa: F401
-                     sample_indices, slbfgs_solve, synth_mnist)
+                     sample_indices, slbfgs_solve, synth_mnist, synth_regression)
 from .unified import (IterationRecorder, UnifiedConfig, UnifiedDataset, UnifiedLauncher, UnifiedLBFGS,  # noqa: F401
                       UnifiedSLBFGS, write_history_csv)

@@ -105,6 +105,7 @@ def lib():
         "lbf_prof_read": (C.c_int, [_vp, C.c_int, _ip, _dp, C.POINTER(C.c_longlong), _ip]),
         "lbf_synth_mnist": (C.c_int, [C.c_longlong, C.c_int, C.c_int, C.c_uint, _vp, _vp]),
         "lbf_sample_indices": (C.c_int, [C.c_longlong, C.c_int, C.c_uint, C.c_int, _vp]),
+        "lbf_synth_regression": (C.c_int, [_vp, C.c_longlong, C.c_longlong, C.c_int, C.c_uint, C.c_uint, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -119,7 +120,7 @@ EXPORTS = ("lbf_last_error lbf_version lbf_ctx_create lbf_ctx_destroy lbf_ctx_sy
            "lbf_mlp_param_count lbf_mlp_init_params lbf_init_params_host lbf_mlp_forward lbf_mlp_loss_grad lbf_two_loop lbf_dot "
            "lbf_nrm2 lbf_axpy lbf_scal lbf_lbfgs_default_params lbf_slbfgs_default_params lbf_lbfgs_solve "
            "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_prof_enable lbf_prof_select lbf_prof_sample lbf_prof_read lbf_synth_mnist "
-           "lbf_sample_indices").split()
+           "lbf_sample_indices lbf_synth_regression").split()
 
 
 def check(rc: int, what: str) -> None:

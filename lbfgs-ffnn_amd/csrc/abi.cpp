@@ -62,6 +62,9 @@ int lbf_ctx_create(int device, void *stream, lbf_ctx **out) {
     c->c.device = device;
     try {
       c->c.set_device();
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        c->c.cus = cus;
       if (stream) {
         c->c.stream = static_cast<hipStream_t>(stream);
       } else {
@@ -486,6 +489,16 @@ int lbf_synth_mnist(long long N, int In, int classes, unsigned seed, float *h_X,
   return guard([&] {
     LBF_REQUIRE(N >= 0 && In > 0 && classes > 0 && h_X && h_Y, "bad argument");
     synth_mnist_host(N, In, classes, seed, h_X, h_Y);
+  });
+}
+
+int lbf_synth_regression(lbf_ctx *ctx, long long row0, long long N, int In, unsigned seed_x, unsigned seed_t,
+                         float *d_X, float *d_Y) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && row0 >= 0 && N >= 0 && In > 0 && d_X && d_Y, "bad argument");
+    ctx->c.set_device();
+    synth_regression(ctx->c.stream, row0, N, In, seed_x, seed_t, d_X, d_Y);
+    LBF_HIP(hipStreamSynchronize(ctx->c.stream));
   });
 }
 

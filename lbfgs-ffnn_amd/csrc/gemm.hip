@@ -700,6 +700,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
     }
   };
 
+  if (EPI == EPI_HEAD) KT(0);
   if (EPI == EPI_HEAD) KTB(0);
   headc::EpiPrefetch<BN, BM, 256> hpre;
   if constexpr (EPI == EPI_HEAD) hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
@@ -711,9 +712,11 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
     vm_wait_tiles<P, NS>(min(NS - 2, nk - 1 - i)); // this wave's pieces of k-tile i landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier(); // everyone's pieces landed; buffer (i - 1) % NS no longer read
+    if (EPI == EPI_HEAD && i < 24) KT(1 + i);
     if (i + NS - 1 < nk) issue(i + NS - 1);
     compute(i % NS);
   }
+  if (EPI == EPI_HEAD) KT(25);
   __syncthreads(); // the LDS is the epilogue's now
   gemm_epilogue<WM, WN, TM, TN, EPI, 1>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, 0);
 }

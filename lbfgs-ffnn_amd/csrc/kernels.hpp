@@ -145,6 +145,10 @@ constexpr int RA_SPLITS_PER_PART = 64; // 4 stripes x 16 loads per thread
 constexpr int RA_MAXFIN = 128;         // column groups the one-block finishing launch combines
 void reduce_all(hipStream_t s, const RedAllArgs &a);
 
+// BASELINE config 5's synthetic regression data on the device (synth.hip).
+void synth_regression(hipStream_t s, long long row0, long long N, int In, unsigned seed_x, unsigned seed_t, float *X,
+                      float *Y);
+
 void finalize_grad_dots(hipStream_t s, long long n, float *g, const float *w, double lambda, const float *p,
                         double *partials, const int *abort = nullptr);
 // generic: per-WG partials of x.y -> partials[wg]

@@ -80,8 +80,31 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
   if (const char *e = std::getenv("LBF_DW_TILE64")) dw64_ = e[0] != '0';
 }
 
-// Split-K plan of every dW GEMM for batch B: aim for ~512 workgroups (2 per CU) per GEMM, k chunks
-// a multiple of the 32-deep LDS tile.
+// Split-K factor for `tiles` output tiles over a K of `K` rows: the GEMM tiles run two workgroups per
+// CU, so a launch is ceil(tiles * s / slots) waves of equal-length workgroups; choose s (chunks of at
+// least min_chunk rows, slabs within a memory cap) to maximise tiles * s / (waves * slots), the
+// smallest s within half a percent of the best. A count just past a multiple of the slots (e.g. 520
+// workgroups on 512 slots) would otherwise cost a whole extra wave.
+static long long split_factor(long long tiles, long long K, long long min_chunk, long long slots,
+                              long long slab_elems_per_split) {
+  const long long cap_elems = 1LL << 29; // 2 GiB of fp32 slabs
+  long long smax = std::max(1LL, std::min(cdiv(K, min_chunk), 4 * slots));
+  if (slab_elems_per_split > 0) smax = std::max(1LL, std::min(smax, cap_elems / slab_elems_per_split));
+  long long best = 1;
+  double best_eff = 0.0;
+  for (long long s = 1; s <= smax; ++s) {
+    const long long wg = tiles * s, waves = cdiv(wg, slots);
+    const double eff = double(wg) / double(waves * slots);
+    if (eff > best_eff + 0.005) {
+      best_eff = eff;
+      best = s;
+    }
+  }
+  return best;
+}
+
+// Split-K plan of every dW GEMM for batch B (workgroup-slot aware, split_factor), k chunks a multiple
+// of the 32-deep LDS tile.
 void Mlp::plan(long long B) {
   if (planned_ == B) return;
   size_t slab = 0, fslab = 0;
@@ -94,7 +117,9 @@ void Mlp::plan(long long B) {
     gemm_tile_for(L.out, L.dtile, &BM, &BN);
     const long long tiles = cdiv(M, BM) * cdiv(L.out, BN);
     const long long min_chunk = L.dtile == TILE_64x64 ? 256 : 128;
-    long long splits = std::max(1LL, std::min(cdiv(512, tiles), cdiv(B, min_chunk)));
+    static const int legacy = env_int("LBF_SPLIT_LEGACY", 0);
+    long long splits = legacy ? std::max(1LL, std::min(cdiv(512, tiles), cdiv(B, min_chunk)))
+                              : split_factor(tiles, B, min_chunk, 2LL * ctx_->cus, M * L.out);
     long long kc = cdiv(cdiv(B, splits), 32) * 32;
     if (kc <= 0) kc = 32;
     splits = std::max(1LL, cdiv(B, kc));

@@ -37,6 +37,7 @@ struct Profiler {
 
 struct Ctx {
   int device = 0;
+  int cus = 256; // compute units (workgroup slots = 2 per CU for the GEMM tiles, see Mlp::plan)
   Profiler prof;
   hipStream_t stream = nullptr;
   bool own_stream = false;

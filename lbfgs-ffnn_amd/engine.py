@@ -288,6 +288,15 @@ def synth_mnist(N: int, In: int = 784, classes: int = 10, seed: int = 123):
     return X, Y
 
 
+def synth_regression(ctx: Context, N: int, In: int = 4096, seed_x: int = 123, seed_t: int = 124, row0: int = 0):
+    """BASELINE config 5 data on the device: rows [row0, row0+N) of X ~ N(0,1) [.][In] and
+    y = tanh(v.x/64) + 0.01 e [.][1]."""
+    X = torch.empty((N, In), dtype=torch.float32, device=f"cuda:{ctx.device}")
+    Y = torch.empty((N, 1), dtype=torch.float32, device=f"cuda:{ctx.device}")
+    check(lib().lbf_synth_regression(ctx.h, row0, N, In, seed_x, seed_t, ptr(X), ptr(Y)), "lbf_synth_regression")
+    return X, Y
+
+
 def sample_indices(N: int, b: int, seed: int = 123, calls: int = 1) -> np.ndarray:
     out = np.empty(calls * b, np.int64)
     check(lib().lbf_sample_indices(N, b, seed, calls, out.ctypes.data_as(C.c_void_p)), "lbf_sample_indices")

@@ -201,3 +201,37 @@ def ring_trace(cap: int, npush: int):
 
 def num_threads() -> int:
     return int(lib().oracle_num_threads())
+
+
+# ---- BASELINE config 5 data (test infrastructure; restates lbfgs-ffnn_amd/csrc/synth.hip) ----------
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix64(x):
+    x = (x + np.uint64(0x9E3779B97F4A7C15)) & _M64
+    x = ((x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & _M64
+    x = ((x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & _M64
+    return x ^ (x >> np.uint64(31))
+
+
+def synth_normal(seed: int, idx: np.ndarray) -> np.ndarray:
+    """Normal number idx of stream `seed` (fp64): Box-Muller on splitmix64 uniform pairs."""
+    idx = np.asarray(idx, np.uint64)
+    j = idx >> np.uint64(1)
+    base = np.uint64(seed) << np.uint64(32)
+    with np.errstate(over="ignore"):
+        a = _splitmix64(base + np.uint64(2) * j)
+        b = _splitmix64(base + np.uint64(2) * j + np.uint64(1))
+    u1 = ((a >> np.uint64(11)) + np.uint64(1)).astype(np.float64) * 2.0 ** -53
+    u2 = (b >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    r, th = np.sqrt(-2.0 * np.log(u1)), 6.283185307179586 * u2
+    return np.where((idx & np.uint64(1)) == 1, r * np.sin(th), r * np.cos(th))
+
+
+def synth_regression(N: int, In: int = 4096, seed_x: int = 123, seed_t: int = 124):
+    """X ~ N(0,1) [N][In] fp32, y = tanh(v.x / 64) + 0.01 e [N][1] fp32 (config 5 recipe)."""
+    X = synth_normal(seed_x, np.arange(N * In, dtype=np.uint64)).astype(np.float32).reshape(N, In)
+    v = synth_normal(seed_t, np.arange(In, dtype=np.uint64))
+    e = synth_normal(seed_t, In + np.arange(N, dtype=np.uint64))
+    y = np.tanh((X.astype(np.float64) @ v) / 64.0) + 0.01 * e
+    return X, y.astype(np.float32).reshape(N, 1)
