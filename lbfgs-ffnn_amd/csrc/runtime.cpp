@@ -108,7 +108,13 @@ static long long split_factor(long long tiles, long long K, long long min_chunk,
 void Mlp::plan(long long B) {
   if (planned_ == B) return;
   size_t slab = 0, fslab = 0;
-  for (auto &L : layers_) {
+  const int nl = int(layers_.size());
+  const bool fused = use_head_ && nl >= 2 && head_supported(layers_[nl - 1].in, layers_[nl - 1].out);
+  const long long slots = 2LL * ctx_->cus;
+  // dW tiles and split-K, last layer first: layer l's launch also carries the side blocks that finish
+  // layer l+1's slabs (side_reduced), and those take workgroup slots too
+  for (int l = nl - 1; l >= 0; --l) {
+    Layer &L = layers_[l];
     int BM, BN;
     const long long M = L.in + 1;
     // dW: 64x64 tiles over narrow outputs -> fewer, longer K splits (a third of the slab traffic)
@@ -117,14 +123,23 @@ void Mlp::plan(long long B) {
     gemm_tile_for(L.out, L.dtile, &BM, &BN);
     const long long tiles = cdiv(M, BM) * cdiv(L.out, BN);
     const long long min_chunk = L.dtile == TILE_64x64 ? 256 : 128;
+    long long side = 0;
+    if (side_reduced(l + 1, fused, 0)) {
+      const Layer &N1 = layers_[l + 1];
+      side = cdiv(cdiv((long long)(N1.in + 1) * N1.out, 64), tiles) * tiles;
+    }
     static const int legacy = env_int("LBF_SPLIT_LEGACY", 0);
     long long splits = legacy ? std::max(1LL, std::min(cdiv(512, tiles), cdiv(B, min_chunk)))
-                              : split_factor(tiles, B, min_chunk, 2LL * ctx_->cus, M * L.out);
+                              : split_factor(tiles, B, min_chunk, std::max(slots - side, tiles), M * L.out);
     long long kc = cdiv(cdiv(B, splits), 32) * 32;
     if (kc <= 0) kc = 32;
     splits = std::max(1LL, cdiv(B, kc));
     L.splits = int(splits);
     L.k_chunk = int(kc);
+  }
+  for (auto &L : layers_) {
+    const long long M = L.in + 1;
+    const long long splits = L.splits;
     L.slab_off = slab;
     if (splits > 1) slab += size_t(splits) * size_t(M) * L.out; // every layer keeps its own slabs until reduce_all
     // forward GEMM: with fewer row tiles than CUs (a data-parallel rank's shard), split K so the chip
