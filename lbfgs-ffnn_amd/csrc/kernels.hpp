@@ -273,6 +273,7 @@ struct CoefArgs {
   int iter = 1;
   int stage = 0;  // LDS doubles for staging partial rows (set by hist_coef)
   int sy_cap = 0; // LDS doubles for SY (and its transpose) (set by hist_coef)
+  int fused = 0;  // hist_core<true>: SY, YY, rho prefetched into LDS, stores off wave 0 (set by hist_coef)
   double dsign = -1.0;
 };
 void hist_coef(hipStream_t s, const CoefArgs &a);

@@ -81,9 +81,10 @@ __global__ __launch_bounds__(256) void fold_rows_kernel(const double *P, int nro
     for (int r = r0 + wave; r < r1; r += 4 * 8) { // eight independent loads in flight per lane
       double v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = r + 4 * u < r1 ? P[(long long)(r + 4 * u) * ncols + c] : 0.0;
+      for (int u = 0; u < 8; ++u) v[u] = P[(long long)min(r + 4 * u, r1 - 1) * ncols + c]; // clamped: no per-load branch
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+      for (int u = 0; u < 8; ++u)
+        if (r + 4 * u < r1) s += v[u];
     }
   }
   part[wave][lane] = s;
@@ -604,7 +605,7 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int iu = i0 + 256 * u;
-        xs[u] = iu < full ? hist_load<NT>(V + iu) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        xs[u] = hist_load<NT>(V + (iu < full ? iu : 0)); // clamped, masked below: no per-load branch
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -669,6 +670,7 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
 // ---------------------------------------------------------------------------------------------
 static constexpr int HIST_STAGE_DOUBLES = 4096;   // up to 32 KB of partial rows staged per round
 static constexpr int HIST_STATIC_LDS = 16 * 1024; // bound on the kernel's static LDS
+static constexpr int HIST_PRE_UNROLL = 11;        // fused path: (m+1)^2 <= 256 * 11, i.e. m <= 52
 
 __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
   if (a.h.abort && *a.h.abort) return;
@@ -686,7 +688,33 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
   st.want_dir = a.want_dir;
   st.iter = a.iter;
   st.dsign = a.dsign;
+  // fused: SY, YY and rho go to LDS (after the SY block and the staging area) with the prologue's
+  // loads, one round trip for all of them; the recurrences then read LDS only
+  constexpr int PU = HIST_PRE_UNROLL;
+  const int S_ = h.slots, SS = S_ * S_;
+  double *pre = sy + a.sy_cap + a.stage;
+  double psy[PU], pyy[PU], prho = 0.0;
+  if (a.fused) {
+#pragma unroll
+    for (int u = 0; u < PU; ++u) { // clamped, unconditional: no branch and wait per load
+      const int i = min(t + 256 * u, SS - 1);
+      psy[u] = h.SY[i];
+      pyy[u] = h.YY[i];
+    }
+    prho = h.rho[min(t, S_ - 1)];
+  }
   hist_prologue(st, sm, h.ist[IST_WSLOT]);
+  if (a.fused) {
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const int i = t + 256 * u;
+      if (i < SS) {
+        pre[i] = psy[u];
+        pre[SS + i] = pyy[u];
+      }
+    }
+    if (t < S_) pre[2 * SS + t] = prho;
+  }
   KT(1);
   const int count0 = sm.count0;
   // ---- A: reduce the columns in use. Tiles of partial rows are staged into LDS with every load in
@@ -704,14 +732,11 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
     for (int e0 = t; e0 < tot; e0 += 256 * 8) { // 8 independent loads in flight per thread
       double v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + 256 * u;
-        v[u] = 0.0;
-        if (e < tot) {
-          const int r = e / nneed, q = e - r * nneed;
-          const int col = q < 6 * count0 ? q : 6 * h.m + (q - 6 * count0);
-          v[u] = a.partials[(long long)(r0 + r) * ncols + col];
-        }
+      for (int u = 0; u < 8; ++u) { // unconditional (clamped) loads: no branch and wait per load
+        const int e = min(e0 + 256 * u, tot - 1);
+        const int r = e / nneed, q = e - r * nneed;
+        const int col = q < 6 * count0 ? q : 6 * h.m + (q - 6 * count0);
+        v[u] = a.partials[(long long)(r0 + r) * ncols + col];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u)
@@ -733,7 +758,14 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
   }
   __syncthreads();
   KT(2);
-  hist_core(st, sm, sy, a.sy_cap, stage, a.stage);
+  if (a.fused) {
+    st.SY = pre;
+    st.YY = pre + SS;
+    st.rho = pre + 2 * SS;
+    hist_core<true>(st, sm, sy, a.sy_cap, stage, a.stage);
+  } else {
+    hist_core<false>(st, sm, sy, a.sy_cap, stage, a.stage);
+  }
 }
 
 void hist_coef(hipStream_t s, const CoefArgs &a) {
@@ -748,10 +780,17 @@ void hist_coef(hipStream_t s, const CoefArgs &a) {
   CoefArgs c = a;
   const long long total = (160 * 1024 - HIST_STATIC_LDS) / 8, m2 = (long long)a.h.m * a.h.m;
   const long long need_stage = 6LL * a.h.m + 6;
-  c.sy_cap = int(std::min(2 * m2, total - need_stage)); // SY, and its transpose when it fits
+  const long long S = a.h.slots, pre = 2 * S * S + S;
+  // fused history step (LDS-prefetched sources, stores off wave 0) when the direction is wanted and
+  // SY (with its transpose), a full staging area and the prefetch all fit
+  static const int fused_on = env_int("LBF_HIST_FUSED", 1);
+  c.fused = (fused_on && a.want_dir == 1 && S * S <= 256LL * HIST_PRE_UNROLL &&
+             2 * m2 + HIST_STAGE_DOUBLES + pre <= total) ? 1 : 0;
+  const long long avail = total - (c.fused ? pre : 0);
+  c.sy_cap = int(std::min(2 * m2, avail - need_stage)); // SY, and its transpose when it fits
   LBF_REQUIRE(c.sy_cap >= m2, "hist_step: LDS too small for the SY block");
-  c.stage = int(std::min<long long>(HIST_STAGE_DOUBLES, total - c.sy_cap));
-  const size_t shmem = (size_t(c.sy_cap) + size_t(c.stage)) * sizeof(double);
+  c.stage = int(std::min<long long>(HIST_STAGE_DOUBLES, avail - c.sy_cap));
+  const size_t shmem = (size_t(c.sy_cap) + size_t(c.stage) + (c.fused ? size_t(pre) : 0)) * sizeof(double);
   hipLaunchKernelGGL(hist_step_kernel, dim3(1), dim3(256), shmem, s, c);
   LBF_KERNEL_CHECK();
 }
@@ -779,8 +818,7 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
   if (e >= h.n) return;
   if (e + 3 < h.n) {
     const f32x4 g4 = *reinterpret_cast<const f32x4 *>(a.g + e);
-    f32x4 x4 = {0.f, 0.f, 0.f, 0.f};
-    if (a.x_out) x4 = *reinterpret_cast<const f32x4 *>(a.x_in + e);
+    const f32x4 x4 = *reinterpret_cast<const f32x4 *>((a.x_out ? a.x_in : a.g) + e); // unconditional: no early wait
     double acc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = cg * double(g4[j]);

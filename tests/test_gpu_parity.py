@@ -130,6 +130,18 @@ def test_two_loop_matches_oracle(ctx, O, mode, k, n):
     assert rel(host(out), ref) <= DIR_RTOL
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("k", [5, 48])
+def test_two_loop_large_n(ctx, O, mode, k):
+    """n past 2M: the Gram sweep's chunks are longer than one pass of its loads (4096 elements per
+    workgroup at cfg 5's n), and the history loads switch to nontemporal past the Infinity Cache."""
+    n = 3_000_001
+    S, Yv, rho, g = make_history(n, k, seed=k + 7)
+    ref = O.two_loop(mode, S, Yv, rho, g)
+    out = ctx.two_loop(dev(S), dev(Yv), rho, dev(g), mode=mode)
+    assert rel(host(out), ref) <= DIR_RTOL
+
+
 def test_blas1(ctx):
     rng = np.random.default_rng(1)
     x = rng.standard_normal(123457).astype(np.float32)
