@@ -119,6 +119,25 @@ typedef struct lbf_slbfgs_params {
   double fd_eps;      /* finite-difference HVP epsilon, 1e-4 (s_lbfgs.hpp:90)        */
 } lbf_slbfgs_params;
 
+/* Gradient descent with momentum == cuda_mlp::CudaGD (src/cuda/gd.cuh:38-106; setters :22-25). */
+typedef struct lbf_gd_params {
+  double lr;          /* setLearningRate, 0.01                                               */
+  double momentum;    /* setMomentum, 0.9 (0: plain x -= lr g)                               */
+  int max_iters;      /* setMaxIterations, 200 (minimizer_base.cuh:62)                       */
+  double tol;         /* setTolerance: stop when ||g|| < tol, 1e-6 (minimizer_base.cuh:63)   */
+} lbf_gd_params;
+
+/* Minibatch SGD with momentum and step decay == cuda_mlp::CudaSGD (src/cuda/sgd.cuh:50-153).
+ * Contiguous, unshuffled batches as in the reference; single rank. */
+typedef struct lbf_sgd_params {
+  double lr, momentum; /* 0.01, 0.9                                                         */
+  int batch;           /* setBatchSize                                                      */
+  double decay_rate;   /* setLearningRateDecay(rate, step): lr *= rate every step epochs (1.0) */
+  int decay_step;      /* 0: no decay                                                       */
+  int max_epochs;      /* setMaxIterations (epochs), 200                                    */
+  double tol;          /* relative epoch-loss improvement stop when > 0, 1e-6               */
+} lbf_sgd_params;
+
 /* Per-iteration history == IterationRecorder (src/iteration_recorder.hpp:13-146) plus extras.
  * Host arrays of capacity cap; any pointer may be NULL. */
 typedef struct lbf_record {
@@ -161,6 +180,17 @@ int lbf_lbfgs_solve_fn(lbf_ctx *ctx, const lbf_lbfgs_params *prm, long long n, f
 /* S-LBFGS (SLBFGS::stochastic_solve s_lbfgs.hpp:165-290 via UnifiedSLBFGS_CPU,
  * unified_optimization.hpp:306-408). X/Y hold all N rows on every rank; minibatches are sampled on
  * the host with the reference's libstdc++ stream and sliced across ranks. */
+/* CudaGD::solve / CudaSGD::solve (the reference's CudaMinimizerBase::solve, minimizer_base.cuh:54-59) on
+ * the MLP. GD: full batch over the n_local rows of this rank (n_global = sum over ranks, as for
+ * lbf_lbfgs_solve). rec: one record per iteration (GD) / the initial full-batch record then one per
+ * epoch (SGD, only when rec is non-NULL, like the reference's recorder_ branch). */
+void lbf_gd_default_params(lbf_gd_params *p);
+void lbf_sgd_default_params(lbf_sgd_params *p);
+int lbf_gd_solve(lbf_mlp *net, const lbf_gd_params *prm, float *d_params, const float *d_X, const float *d_Y,
+                 long long n_local, long long n_global, lbf_record *rec, lbf_solve_info *info);
+int lbf_sgd_solve(lbf_mlp *net, const lbf_sgd_params *prm, float *d_params, const float *d_X, const float *d_Y,
+                  long long N, lbf_record *rec, lbf_solve_info *info);
+
 int lbf_slbfgs_solve(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params, const float *d_X,
                      const float *d_Y, long long N, lbf_record *rec, lbf_solve_info *info);
 
@@ -189,6 +219,13 @@ int lbf_memcpy(lbf_ctx *ctx, void *dst, const void *src, size_t bytes, int kind)
 int lbf_synth_mnist(long long N, int In, int classes, unsigned seed, float *h_X, float *h_Y);
 /* Partial Fisher-Yates minibatch draws from one mt19937(seed) (s_lbfgs.hpp:141-160). */
 int lbf_sample_indices(long long N, int b, unsigned seed, int calls, long long *h_out);
+/* IDX datasets (MNIST / Fashion-MNIST files) == the reference's MNISTLoader (tests/mnist/mnist_loader.hpp:
+ * 8-100): images (magic 2051) scaled by 1/255 into row-major [N][rows*cols] fp32, labels (magic 2049)
+ * one-hot into [N][classes] (labels >= classes stay all-zero); max_* > 0 caps the count. Call with a
+ * NULL output first to read the header (count, rows, cols), then with a buffer of that size. */
+int lbf_idx_read_images(const char *path, long long max_images, float *h_out, long long *count, int *rows,
+                        int *cols);
+int lbf_idx_read_labels(const char *path, long long max_labels, int classes, float *h_onehot, long long *count);
 /* BASELINE config 5's synthetic regression data, generated on the device (no reference counterpart:
  * the reference reads MNIST files): X ~ N(0,1) [N][In], y = tanh(v.x / 64) + 0.01 e [N][1]; stream
  * defined in lbfgs-ffnn_amd/csrc/synth.hip, restated in oracle/oracle.py. Writes rows [row0, row0+N)

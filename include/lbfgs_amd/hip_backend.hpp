@@ -318,6 +318,30 @@ private:
   std::vector<double> d_;
 };
 
+/// The reference's MNISTLoader (tests/mnist/mnist_loader.hpp:8-100) over lbf_idx_read_*: images as a
+/// (rows*cols) x N matrix scaled to [0, 1], labels one-hot 10 x N, column-major like the Eigen version.
+struct MNISTLoader {
+  static HostMatrix loadImages(const std::string &path, int max_images = 0) {
+    long long n = 0;
+    int r = 0, c = 0;
+    hip_check(lbf_idx_read_images(path.c_str(), max_images, nullptr, &n, &r, &c), "lbf_idx_read_images");
+    std::vector<float> buf(size_t(n) * size_t(r) * size_t(c));
+    hip_check(lbf_idx_read_images(path.c_str(), max_images, buf.data(), &n, &r, &c), "lbf_idx_read_images");
+    HostMatrix m(long(r) * c, long(n));
+    for (size_t i = 0; i < buf.size(); ++i) m.data()[i] = double(buf[i]);
+    return m;
+  }
+  static HostMatrix loadLabels(const std::string &path, int max_images = 0) {
+    long long n = 0;
+    hip_check(lbf_idx_read_labels(path.c_str(), max_images, 10, nullptr, &n), "lbf_idx_read_labels");
+    std::vector<float> buf(size_t(n) * 10);
+    hip_check(lbf_idx_read_labels(path.c_str(), max_images, 10, buf.data(), &n), "lbf_idx_read_labels");
+    HostMatrix m(10, long(n));
+    for (size_t i = 0; i < buf.size(); ++i) m.data()[i] = double(buf[i]);
+    return m;
+  }
+};
+
 } // namespace hip_mlp
 
 #ifndef LBF_USE_REFERENCE_UNIFIED_TYPES
@@ -437,6 +461,58 @@ public:
     lbf_solve_info info{};
     hip_mlp::hip_check(lbf_slbfgs_solve(nw.raw(), &prm, nw.params_data(), dx.data(), dy.data(), n_train, &rec, &info),
                        "lbf_slbfgs_solve");
+    recorder.set_size(rec.size);
+    write_hip_history_csv(hip_log_filename(c), recorder, c.log_interval);
+  }
+};
+
+/// UnifiedGD_CUDA counterpart (unified_optimization.hpp:518-554): CudaGD with lr, momentum,
+/// max_iters, tolerance from the config (gd.cuh:38-106), on the device.
+class UnifiedGD_HIP : public UnifiedOptimizer<HipBackend> {
+public:
+  void optimize(hip_mlp::HipHandle &, NetworkWrapper<HipBackend> &net, long n_train,
+                hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dx, hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dy,
+                const UnifiedConfig &c) override {
+    auto &nw = net.getInternal();
+    lbf_gd_params prm;
+    lbf_gd_default_params(&prm);
+    prm.lr = c.learning_rate;
+    prm.momentum = c.momentum;
+    prm.max_iters = c.max_iters;
+    prm.tol = c.tolerance;
+    recorder.init(c.max_iters);
+    lbf_record rec = recorder.view();
+    lbf_solve_info info{};
+    hip_mlp::hip_check(lbf_gd_solve(nw.raw(), &prm, nw.params_data(), dx.data(), dy.data(), n_train, n_train, &rec,
+                                    &info),
+                       "lbf_gd_solve");
+    recorder.set_size(rec.size);
+    write_hip_history_csv(hip_log_filename(c), recorder, c.log_interval);
+  }
+};
+
+/// UnifiedSGD_CUDA counterpart (unified_optimization.hpp:595-632): CudaSGD with the config's lr,
+/// momentum, batch size, max_iters (epochs) and setLearningRateDecay(lr_decay, lr_decay_rate)
+/// (sgd.cuh:50-153; the reference does not pass the tolerance, so CudaSGD keeps its 1e-6).
+class UnifiedSGD_HIP : public UnifiedOptimizer<HipBackend> {
+public:
+  void optimize(hip_mlp::HipHandle &, NetworkWrapper<HipBackend> &net, long n_train,
+                hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dx, hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dy,
+                const UnifiedConfig &c) override {
+    auto &nw = net.getInternal();
+    lbf_sgd_params prm;
+    lbf_sgd_default_params(&prm);
+    prm.lr = c.learning_rate;
+    prm.momentum = c.momentum;
+    prm.batch = c.batch_size;
+    prm.max_epochs = c.max_iters;
+    prm.decay_rate = c.lr_decay;
+    prm.decay_step = c.lr_decay_rate;
+    recorder.init(c.max_iters + 1);
+    lbf_record rec = recorder.view();
+    lbf_solve_info info{};
+    hip_mlp::hip_check(lbf_sgd_solve(nw.raw(), &prm, nw.params_data(), dx.data(), dy.data(), n_train, &rec, &info),
+                       "lbf_sgd_solve");
     recorder.set_size(rec.size);
     write_hip_history_csv(hip_log_filename(c), recorder, c.log_interval);
   }

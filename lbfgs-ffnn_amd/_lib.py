@@ -36,6 +36,15 @@ class SlbfgsParams(C.Structure):
                 ("fd_eps", C.c_double)]
 
 
+class GdParams(C.Structure):
+    _fields_ = [("lr", C.c_double), ("momentum", C.c_double), ("max_iters", C.c_int), ("tol", C.c_double)]
+
+
+class SgdParams(C.Structure):
+    _fields_ = [("lr", C.c_double), ("momentum", C.c_double), ("batch", C.c_int), ("decay_rate", C.c_double),
+                ("decay_step", C.c_int), ("max_epochs", C.c_int), ("tol", C.c_double)]
+
+
 class Record(C.Structure):
     _fields_ = [("loss", C.POINTER(C.c_double)), ("grad_norm", C.POINTER(C.c_double)),
                 ("time_ms", C.POINTER(C.c_double)), ("alpha", C.POINTER(C.c_double)),
@@ -105,6 +114,14 @@ def lib():
         "lbf_prof_read": (C.c_int, [_vp, C.c_int, _ip, _dp, C.POINTER(C.c_longlong), _ip]),
         "lbf_synth_mnist": (C.c_int, [C.c_longlong, C.c_int, C.c_int, C.c_uint, _vp, _vp]),
         "lbf_sample_indices": (C.c_int, [C.c_longlong, C.c_int, C.c_uint, C.c_int, _vp]),
+        "lbf_idx_read_images": (C.c_int, [C.c_char_p, C.c_longlong, _vp, C.POINTER(C.c_longlong), _ip, _ip]),
+        "lbf_idx_read_labels": (C.c_int, [C.c_char_p, C.c_longlong, C.c_int, _vp, C.POINTER(C.c_longlong)]),
+        "lbf_gd_default_params": (None, [C.POINTER(GdParams)]),
+        "lbf_sgd_default_params": (None, [C.POINTER(SgdParams)]),
+        "lbf_gd_solve": (C.c_int, [_vp, C.POINTER(GdParams), _vp, _vp, _vp, C.c_longlong, C.c_longlong,
+                                   C.POINTER(Record), C.POINTER(SolveInfo)]),
+        "lbf_sgd_solve": (C.c_int, [_vp, C.POINTER(SgdParams), _vp, _vp, _vp, C.c_longlong, C.POINTER(Record),
+                                    C.POINTER(SolveInfo)]),
         "lbf_synth_regression": (C.c_int, [_vp, C.c_longlong, C.c_longlong, C.c_int, C.c_uint, C.c_uint, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
@@ -120,7 +137,8 @@ EXPORTS = ("lbf_last_error lbf_version lbf_ctx_create lbf_ctx_destroy lbf_ctx_sy
            "lbf_mlp_param_count lbf_mlp_init_params lbf_init_params_host lbf_mlp_forward lbf_mlp_loss_grad lbf_two_loop lbf_dot "
            "lbf_nrm2 lbf_axpy lbf_scal lbf_lbfgs_default_params lbf_slbfgs_default_params lbf_lbfgs_solve "
            "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_prof_enable lbf_prof_select lbf_prof_sample lbf_prof_read lbf_synth_mnist "
-           "lbf_sample_indices lbf_synth_regression").split()
+           "lbf_sample_indices lbf_synth_regression lbf_gd_default_params lbf_sgd_default_params lbf_gd_solve "
+           "lbf_sgd_solve lbf_idx_read_images lbf_idx_read_labels").split()
 
 
 def check(rc: int, what: str) -> None:

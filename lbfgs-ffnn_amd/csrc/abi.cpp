@@ -321,6 +321,41 @@ void lbf_lbfgs_default_params(lbf_lbfgs_params *p, int line_search) {
   }
 }
 
+void lbf_gd_default_params(lbf_gd_params *p) { // gd.cuh:103-104, minimizer_base.cuh:62-63
+  if (!p) return;
+  p->lr = 0.01;
+  p->momentum = 0.9;
+  p->max_iters = 200;
+  p->tol = 1e-6;
+}
+
+void lbf_sgd_default_params(lbf_sgd_params *p) { // sgd.cuh:156-161, minimizer_base.cuh:62-63
+  if (!p) return;
+  p->lr = 0.01;
+  p->momentum = 0.9;
+  p->batch = 64;
+  p->decay_rate = 1.0;
+  p->decay_step = 0;
+  p->max_epochs = 200;
+  p->tol = 1e-6;
+}
+
+int lbf_gd_solve(lbf_mlp *net, const lbf_gd_params *prm, float *d_params, const float *d_X, const float *d_Y,
+                 long long n_local, long long n_global, lbf_record *rec, lbf_solve_info *info) {
+  return guard([&] {
+    LBF_REQUIRE(net && prm, "null argument");
+    run_gd(net->net.get(), *prm, d_params, d_X, d_Y, n_local, n_global, rec, info);
+  });
+}
+
+int lbf_sgd_solve(lbf_mlp *net, const lbf_sgd_params *prm, float *d_params, const float *d_X, const float *d_Y,
+                  long long N, lbf_record *rec, lbf_solve_info *info) {
+  return guard([&] {
+    LBF_REQUIRE(net && prm, "null argument");
+    run_sgd(net->net.get(), *prm, d_params, d_X, d_Y, N, rec, info);
+  });
+}
+
 void lbf_slbfgs_default_params(lbf_slbfgs_params *p) {
   if (!p) return;
   p->max_epochs = 1000; // stochastic_minimizer.hpp:44-47
@@ -500,6 +535,15 @@ int lbf_synth_regression(lbf_ctx *ctx, long long row0, long long N, int In, unsi
     synth_regression(ctx->c.stream, row0, N, In, seed_x, seed_t, d_X, d_Y);
     LBF_HIP(hipStreamSynchronize(ctx->c.stream));
   });
+}
+
+int lbf_idx_read_images(const char *path, long long max_images, float *h_out, long long *count, int *rows,
+                        int *cols) {
+  return guard([&] { idx_read_images(path, max_images, h_out, count, rows, cols); });
+}
+
+int lbf_idx_read_labels(const char *path, long long max_labels, int classes, float *h_onehot, long long *count) {
+  return guard([&] { idx_read_labels(path, max_labels, classes, h_onehot, count); });
 }
 
 int lbf_sample_indices(long long N, int b, unsigned seed, int calls, long long *h_out) {

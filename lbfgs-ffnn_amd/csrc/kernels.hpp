@@ -170,6 +170,10 @@ void axpy(hipStream_t s, long long n, float alpha, const float *x, float *y);
 void scal(hipStream_t s, long long n, float alpha, float *x);
 // y = x + alpha * p
 void axpy_to(hipStream_t s, long long n, const float *x, float alpha, const float *p, float *y);
+// GD / SGD momentum step and SGD's device-side epoch-loss accumulator (vec_kernels.hip).
+void momentum_step(hipStream_t s, long long n, float momentum, float lr, const float *lr_dev, const float *g, float *v,
+                   float *x);
+void epoch_loss_acc(hipStream_t s, const double *scal, long long rows, float *esum);
 // u = (sum_i W[slot_i]) / cnt  in logical order, fp64 accumulation
 void average_slots(hipStream_t s, long long n, const float *W, long long ld, const int *h_slots, int cnt, float *u);
 // out = a + c*b

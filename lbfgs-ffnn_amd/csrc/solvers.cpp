@@ -676,4 +676,131 @@ void SlbfgsSolver::info(lbf_solve_info *out) const {
   out->final_grad_norm = last_gnorm_;
 }
 
+// ================================================================================================
+// GD / SGD with momentum
+// ================================================================================================
+namespace {
+void put_record(lbf_record *rec, int i, double loss, double gnorm, double ms, double lr) {
+  if (!rec || i >= rec->cap) return;
+  if (rec->loss) rec->loss[i] = loss;
+  if (rec->grad_norm) rec->grad_norm[i] = gnorm;
+  if (rec->time_ms) rec->time_ms[i] = ms;
+  if (rec->alpha) rec->alpha[i] = lr;
+  if (rec->ls_trials) rec->ls_trials[i] = 0;
+  if (rec->accepted) rec->accepted[i] = -1;
+  rec->size = std::max(rec->size, i + 1);
+}
+} // namespace
+
+// CudaGD::solve (gd.cuh:38-106): the loss/grad callback is one fused evaluation; the reference's
+// blocking cublasSnrm2 becomes the evaluation's g.g, read with the loss once per iteration.
+int run_gd(Mlp *net, const lbf_gd_params &prm, float *d_params, const float *X, const float *Y, long long n_local,
+           long long n_global, lbf_record *rec, lbf_solve_info *info) {
+  LBF_REQUIRE(d_params && X && Y && n_local >= 0 && n_global > 0, "bad argument");
+  Ctx *c = net->ctx();
+  c->set_device();
+  hipStream_t s = c->stream;
+  const long long n = (long long)net->nparams();
+  DevBuf<float> g(size_t(round4(n + 2))), v(size_t(std::max(1LL, n)));
+  DevBuf<double> scal(SC_N);
+  PinnedBuf<double> hs;
+  hs.ensure(SC_N);
+  LBF_HIP(hipMemsetAsync(v.get(), 0, size_t(n) * sizeof(float), s));
+  const long long evals0 = net->evals();
+  auto eval = [&]() {
+    net->loss_grad(d_params, g.get(), X, Y, nullptr, n_local, 1.0 / double(n_global), 0.0, nullptr, scal.get());
+    LBF_HIP(hipMemcpyAsync(hs.get(), scal.get(), SC_N * sizeof(double), hipMemcpyDeviceToHost, s));
+    LBF_HIP(hipStreamSynchronize(s));
+  };
+  const float lr = float(prm.lr), mom = float(prm.momentum), tol = float(prm.tol);
+  eval();
+  const auto t0 = std::chrono::steady_clock::now();
+  int done = 0, ri = rec ? rec->size : 0;
+  for (int it = 0; it < prm.max_iters; ++it) {
+    if (float(std::sqrt(hs[SC_TGG])) < tol) break; // gd.cuh:73
+    momentum_step(s, n, mom, lr, nullptr, g.get(), v.get(), d_params);
+    eval();
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    put_record(rec, ri++, double(float(hs[SC_LOSS])), double(float(std::sqrt(hs[SC_TGG]))), ms, double(lr));
+    ++done;
+  }
+  if (info) {
+    info->iterations = done;
+    info->n_evals = net->evals() - evals0;
+    info->final_loss = hs[SC_LOSS];
+    info->final_grad_norm = std::sqrt(hs[SC_TGG]);
+  }
+  return done;
+}
+
+// CudaSGD::solve (sgd.cuh:50-153). Batch losses accumulate on the device (epoch_loss_acc, fp32 like
+// the reference's host sum), so an epoch synchronises once, not once per batch.
+int run_sgd(Mlp *net, const lbf_sgd_params &prm, float *d_params, const float *X, const float *Y, long long N,
+            lbf_record *rec, lbf_solve_info *info) {
+  LBF_REQUIRE(d_params && X && Y && N > 0 && prm.batch > 0, "bad argument");
+  Ctx *c = net->ctx();
+  LBF_REQUIRE(!c->dp(), "SGD runs on one rank (the reference's contiguous batches have no shard split)");
+  c->set_device();
+  hipStream_t s = c->stream;
+  const long long n = (long long)net->nparams();
+  const int In = net->layers().front().in, Out = net->layers().back().out;
+  DevBuf<float> g(size_t(round4(n + 2))), v(size_t(std::max(1LL, n))), esum(1);
+  DevBuf<double> scal(SC_N);
+  PinnedBuf<double> hs;
+  hs.ensure(SC_N);
+  PinnedBuf<float> he;
+  he.ensure(1);
+  LBF_HIP(hipMemsetAsync(v.get(), 0, size_t(n) * sizeof(float), s));
+  const long long evals0 = net->evals();
+  auto full = [&]() {
+    net->loss_grad(d_params, g.get(), X, Y, nullptr, N, 1.0 / double(N), 0.0, nullptr, scal.get());
+    LBF_HIP(hipMemcpyAsync(hs.get(), scal.get(), SC_N * sizeof(double), hipMemcpyDeviceToHost, s));
+    LBF_HIP(hipStreamSynchronize(s));
+  };
+  const float mom = float(prm.momentum), tol = float(prm.tol);
+  float cur_lr = float(prm.lr);
+  const long long nb = cdiv(N, prm.batch);
+  float prev = std::numeric_limits<float>::infinity();
+  const auto t0 = std::chrono::steady_clock::now();
+  int done = 0, ri = rec ? rec->size : 0;
+  auto ms_now = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+  if (rec) { // sgd.cuh:93-98
+    full();
+    put_record(rec, ri++, double(float(hs[SC_LOSS])), double(float(std::sqrt(hs[SC_TGG]))), 0.0, double(cur_lr));
+    ++done;
+  }
+  for (int it = 0; it < prm.max_epochs; ++it) {
+    if (prm.decay_step > 0 && it > 0 && it % prm.decay_step == 0) cur_lr *= float(prm.decay_rate); // :101-103
+    LBF_HIP(hipMemsetAsync(esum.get(), 0, sizeof(float), s));
+    for (long long b = 0; b < nb; ++b) { // :107-127
+      const long long r0 = b * prm.batch, bs = std::min<long long>(prm.batch, N - r0);
+      net->loss_grad(d_params, g.get(), X + r0 * In, Y + r0 * Out, nullptr, bs, 1.0 / double(bs), 0.0, nullptr,
+                     scal.get());
+      epoch_loss_acc(s, scal.get(), bs, esum.get());
+      momentum_step(s, n, mom, cur_lr, nullptr, g.get(), v.get(), d_params);
+    }
+    LBF_HIP(hipMemcpyAsync(he.get(), esum.get(), sizeof(float), hipMemcpyDeviceToHost, s));
+    LBF_HIP(hipStreamSynchronize(s));
+    const float avg = he[0] / float(N);
+    if (tol > 0.0f && std::isfinite(prev)) { // :129-135
+      const float rel = std::fabs(prev - avg) / std::max(1.0f, std::fabs(prev));
+      if (rel < tol) break;
+    }
+    prev = avg;
+    if (rec) { // :138-148
+      full();
+      put_record(rec, ri++, double(float(hs[SC_LOSS])), double(float(std::sqrt(hs[SC_TGG]))), ms_now(),
+                 double(cur_lr));
+    }
+    ++done;
+  }
+  if (info) {
+    info->iterations = done;
+    info->n_evals = net->evals() - evals0;
+    info->final_loss = rec ? hs[SC_LOSS] : double(prev);
+    info->final_grad_norm = rec ? std::sqrt(hs[SC_TGG]) : 0.0;
+  }
+  return done;
+}
+
 } // namespace lbf

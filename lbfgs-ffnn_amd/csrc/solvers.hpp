@@ -165,6 +165,12 @@ private:
   double last_loss_ = 0, last_gnorm_ = 0;
 };
 
+// CudaGD / CudaSGD (src/cuda/gd.cuh:38-106, sgd.cuh:50-153) on the MLP; return the iterations done.
+int run_gd(Mlp *net, const lbf_gd_params &prm, float *d_params, const float *X, const float *Y, long long n_local,
+           long long n_global, lbf_record *rec, lbf_solve_info *info);
+int run_sgd(Mlp *net, const lbf_sgd_params &prm, float *d_params, const float *X, const float *Y, long long N,
+            lbf_record *rec, lbf_solve_info *info);
+
 // libstdc++ partial Fisher-Yates (s_lbfgs.hpp:141-160); shared with the ABI helper.
 std::vector<size_t> sample_minibatch(size_t N, size_t b, std::mt19937 &rng);
 

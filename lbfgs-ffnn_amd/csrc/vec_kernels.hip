@@ -445,6 +445,40 @@ __global__ __launch_bounds__(256) void axpy_to_kernel(long long n, const float *
     for (long long j = e; j < n; ++j) y[j] = x[j] + alpha * p[j];
   }
 }
+// GD / SGD step (gd.cuh:77-85, sgd.cuh:115-124): v = m v - lr g ; x += v (m > 0), else x -= lr g. The
+// reference's scal + two cuBLAS saxpys in one pass: v*m rounded, then the saxpys' fused multiply-adds.
+// lr is read from the device (SGD's decayed rate lives there) when lr_dev is non-null.
+__global__ __launch_bounds__(256) void momentum_step_kernel(long long n, float momentum, float lr, const float *lr_dev,
+                                                            const float *g, float *v, float *x) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float r = lr_dev ? *lr_dev : lr;
+  if (momentum > 0.0f) {
+    const float vi = __fmaf_rn(-r, g[i], __fmul_rn(v[i], momentum));
+    v[i] = vi;
+    x[i] = __fadd_rn(x[i], vi);
+  } else {
+    x[i] = __fmaf_rn(-r, g[i], x[i]);
+  }
+}
+void momentum_step(hipStream_t s, long long n, float momentum, float lr, const float *lr_dev, const float *g, float *v,
+                   float *x) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(momentum_step_kernel, dim3(unsigned(cdiv(n, 256))), dim3(256), 0, s, n, momentum, lr, lr_dev, g,
+                     v, x);
+  LBF_KERNEL_CHECK();
+}
+
+// SGD's epoch loss (sgd.cuh:126): esum += float(batch loss) * float(batch rows), fp32 like the reference's
+// host scalars; one thread, after each batch evaluation (no host round trip per batch).
+__global__ void epoch_loss_acc_kernel(const double *scal, float rows, float *esum) {
+  *esum = __fadd_rn(*esum, __fmul_rn(float(scal[SC_LOSS]), rows));
+}
+void epoch_loss_acc(hipStream_t s, const double *scal, long long rows, float *esum) {
+  hipLaunchKernelGGL(epoch_loss_acc_kernel, dim3(1), dim3(1), 0, s, scal, float(rows), esum);
+  LBF_KERNEL_CHECK();
+}
+
 void axpy_to(hipStream_t s, long long n, const float *x, float alpha, const float *p, float *y) {
   hipLaunchKernelGGL(axpy_to_kernel, dim3(unsigned(cdiv(cdiv(n, 4), 256))), dim3(256), 0, s, n, x, alpha, p, y);
   LBF_KERNEL_CHECK();

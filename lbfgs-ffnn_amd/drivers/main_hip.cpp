@@ -2,7 +2,7 @@
 // tests/mnist/main-gpu.cpp (UnifiedLauncher<Backend> + UnifiedConfig + train/test) with
 // Backend = HipBackend. The MNIST images are absent from the reference snapshot, so it uses the
 // synthetic MNIST-shaped data of SURVEY.md §8(d) (lbf_synth_mnist). Plain C++17, links liblbfgs_amd.so.
-//   usage: main_hip [N_train] [max_iters]
+//   usage: main_hip [N_train] [max_iters] [mnist_dir]
 #include "lbfgs_amd/hip_backend.hpp"
 
 #include <cstdlib>
@@ -29,8 +29,16 @@ int main(int argc, char **argv) {
   launcher.buildNetwork();
 
   UnifiedDataset dataset;
-  fill(train_size, dataset.train_x, dataset.train_y, 123);
-  fill(10000, dataset.test_x, dataset.test_y, 124);
+  if (argc > 3) { // an MNIST directory, as tests/mnist/main-gpu.cpp reads it (train-/t10k- idx files)
+    const std::string dir = argv[3];
+    dataset.train_x = hip_mlp::MNISTLoader::loadImages(dir + "/train-images.idx3-ubyte", int(train_size));
+    dataset.train_y = hip_mlp::MNISTLoader::loadLabels(dir + "/train-labels.idx1-ubyte", int(train_size));
+    dataset.test_x = hip_mlp::MNISTLoader::loadImages(dir + "/t10k-images.idx3-ubyte");
+    dataset.test_y = hip_mlp::MNISTLoader::loadLabels(dir + "/t10k-labels.idx1-ubyte");
+  } else { // the reference snapshot has no image files: synthetic MNIST-shaped data
+    fill(train_size, dataset.train_x, dataset.train_y, 123);
+    fill(10000, dataset.test_x, dataset.test_y, 124);
+  }
   launcher.setData(dataset);
 
   {
@@ -79,6 +87,40 @@ int main(int argc, char **argv) {
     UnifiedSLBFGS_HIP optimizer; // GPU S-LBFGS (CPU-only in the reference)
     launcher.train(optimizer, config);
     launcher.test();
+  }
+  {
+    UnifiedConfig config; // tests/mnist/main-gpu.cpp's GD block
+    config.name = "HIP_GD";
+    config.max_iters = iters;
+    config.tolerance = 1e-4;
+    config.learning_rate = 0.1;
+    config.momentum = 0.9;
+    config.log_interval = 1;
+    UnifiedGD_HIP optimizer;
+    launcher.train(optimizer, config);
+    launcher.test();
+    std::cout << "[RESULT] gd iters=" << optimizer.recorder.size() << std::endl;
+  }
+  {
+    UnifiedConfig config; // tests/mnist/main-gpu.cpp's SGD block
+    config.name = "HIP_SGD";
+    config.max_iters = 3;
+    config.learning_rate = 0.05;
+    config.momentum = 0.9;
+    config.batch_size = 256;
+    config.lr_decay = 0.5;
+    config.lr_decay_rate = 2;
+    config.log_interval = 1;
+    UnifiedSGD_HIP optimizer;
+    launcher.train(optimizer, config);
+    launcher.test();
+    std::vector<double> l, g;
+    optimizer.recorder.copy_to_host(l, g);
+    if (l.size() != 4 || !(l.back() < l.front())) {
+      std::cerr << "SGD: expected 4 records and a decrease" << std::endl;
+      return 1;
+    }
+    std::cout << "[RESULT] sgd epochs=" << l.size() - 1 << " last_loss=" << l.back() << std::endl;
   }
   std::cout << "[RESULT] ok" << std::endl;
   return 0;

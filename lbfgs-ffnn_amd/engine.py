@@ -13,8 +13,8 @@ from typing import Optional, Sequence
 import numpy as np
 import torch
 
-from ._lib import (ACTS, INIT_CPU, INIT_CUDA, LS_ARMIJO, LS_WOLFE, LbfError, LbfgsParams, Record, SlbfgsParams,
-                   SolveInfo, check, lib, ptr)
+from ._lib import (ACTS, INIT_CPU, INIT_CUDA, LS_ARMIJO, LS_WOLFE, GdParams, LbfError, LbfgsParams, Record,
+                   SgdParams, SlbfgsParams, SolveInfo, check, lib, ptr)
 
 
 class Context:
@@ -267,6 +267,37 @@ def slbfgs_solve(net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tenso
     return hist.as_dict(), info
 
 
+def gd_solve(net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, n_global: Optional[int] = None,
+             **kw):
+    """CudaGD::solve (src/cuda/gd.cuh:38-106); params updated in place. kw: lr, momentum, max_iters, tol."""
+    p = GdParams()
+    lib().lbf_gd_default_params(C.byref(p))
+    for k, v in kw.items():
+        if v is not None:
+            setattr(p, k, v)
+    hist = History(max(p.max_iters, 1))
+    info = SolveInfo()
+    n_local = int(X.shape[0])
+    check(lib().lbf_gd_solve(net.h, C.byref(p), ptr(params), ptr(X), ptr(Y), n_local, int(n_global or n_local),
+                             C.byref(hist.rec), C.byref(info)), "lbf_gd_solve")
+    return hist.as_dict(), info
+
+
+def sgd_solve(net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, record: bool = True, **kw):
+    """CudaSGD::solve (src/cuda/sgd.cuh:50-153). kw: lr, momentum, batch, decay_rate, decay_step,
+    max_epochs, tol. record=False runs without the recorder (no full-batch evaluations)."""
+    p = SgdParams()
+    lib().lbf_sgd_default_params(C.byref(p))
+    for k, v in kw.items():
+        if v is not None:
+            setattr(p, k, v)
+    hist = History(p.max_epochs + 1)
+    info = SolveInfo()
+    check(lib().lbf_sgd_solve(net.h, C.byref(p), ptr(params), ptr(X), ptr(Y), int(X.shape[0]),
+                              C.byref(hist.rec) if record else None, C.byref(info)), "lbf_sgd_solve")
+    return hist.as_dict(), info
+
+
 def init_params_host(dims: Sequence[int], acts: Sequence, seed: int = 123, mode: str = "cpu") -> np.ndarray:
     """Host-side copy of the init stream (for tests; the device path is Mlp.init_params)."""
     a = [ACTS[x] if isinstance(x, str) else int(x) for x in acts]
@@ -295,6 +326,27 @@ def synth_regression(ctx: Context, N: int, In: int = 4096, seed_x: int = 123, se
     Y = torch.empty((N, 1), dtype=torch.float32, device=f"cuda:{ctx.device}")
     check(lib().lbf_synth_regression(ctx.h, row0, N, In, seed_x, seed_t, ptr(X), ptr(Y)), "lbf_synth_regression")
     return X, Y
+
+
+def load_idx_images(path: str, max_images: int = 0) -> np.ndarray:
+    """MNISTLoader::loadImages (tests/mnist/mnist_loader.hpp:21-61): [N][rows*cols] float32 in [0, 1]."""
+    n, r, c = C.c_longlong(0), C.c_int(0), C.c_int(0)
+    check(lib().lbf_idx_read_images(path.encode(), max_images, None, C.byref(n), C.byref(r), C.byref(c)),
+          "lbf_idx_read_images")
+    out = np.empty((n.value, r.value * c.value), np.float32)
+    check(lib().lbf_idx_read_images(path.encode(), max_images, out.ctypes.data_as(C.c_void_p), C.byref(n),
+                                    C.byref(r), C.byref(c)), "lbf_idx_read_images")
+    return out
+
+
+def load_idx_labels(path: str, max_labels: int = 0, classes: int = 10) -> np.ndarray:
+    """MNISTLoader::loadLabels (tests/mnist/mnist_loader.hpp:63-100): one-hot [N][classes] float32."""
+    n = C.c_longlong(0)
+    check(lib().lbf_idx_read_labels(path.encode(), max_labels, classes, None, C.byref(n)), "lbf_idx_read_labels")
+    out = np.empty((n.value, classes), np.float32)
+    check(lib().lbf_idx_read_labels(path.encode(), max_labels, classes, out.ctypes.data_as(C.c_void_p), C.byref(n)),
+          "lbf_idx_read_labels")
+    return out
 
 
 def sample_indices(N: int, b: int, seed: int = 123, calls: int = 1) -> np.ndarray:

@@ -162,6 +162,39 @@ class UnifiedSLBFGS(UnifiedOptimizer):
         return rec
 
 
+class UnifiedGD(UnifiedOptimizer):
+    """UnifiedGD<HipBackend> (unified_optimization.hpp:518-554: CudaGD with the config's learning_rate,
+    momentum, max_iters, tolerance)."""
+
+    def optimize(self, net, data, config):
+        hist, info = engine.gd_solve(net.mlp, net.params, data.x, data.y, n_global=data.n_global,
+                                     lr=config.learning_rate, momentum=config.momentum, max_iters=config.max_iters,
+                                     tol=config.tolerance)
+        rec = IterationRecorder()
+        for i in range(len(hist["loss"])):
+            rec.record(i, float(hist["loss"][i]), float(hist["grad_norm"][i]), float(hist["time_ms"][i]))
+        self.info = info
+        self.history = hist
+        return rec
+
+
+class UnifiedSGD(UnifiedOptimizer):
+    """UnifiedSGD<HipBackend> (unified_optimization.hpp:595-632: CudaSGD with learning_rate, momentum,
+    batch_size, max_iters epochs and setLearningRateDecay(lr_decay, lr_decay_rate); the tolerance is
+    not passed, so CudaSGD's default 1e-6 applies). Single rank."""
+
+    def optimize(self, net, data, config):
+        hist, info = engine.sgd_solve(net.mlp, net.params, data.x_full, data.y_full, lr=config.learning_rate,
+                                      momentum=config.momentum, batch=config.batch_size, max_epochs=config.max_iters,
+                                      decay_rate=config.lr_decay, decay_step=config.lr_decay_rate)
+        rec = IterationRecorder()
+        for i in range(len(hist["loss"])):
+            rec.record(i, float(hist["loss"][i]), float(hist["grad_norm"][i]), float(hist["time_ms"][i]))
+        self.info = info
+        self.history = hist
+        return rec
+
+
 class _DeviceData:
     def __init__(self, dataset: UnifiedDataset, device: str, rank: int, world: int, need_full: bool = True):
         tx = np.ascontiguousarray(dataset.train_x, np.float32)   # fp64 -> fp32 upload (unified_launcher.hpp:105-128)

@@ -714,6 +714,90 @@ Vec<T> slbfgs(Vec<T> weights, BG &&batch_g, BF &&batch_f, const SlbfgsParams &pr
 }
 
 // ---------------------------------------------------------------------------------------------
+// Gradient descent with momentum — restates cuda_mlp::CudaGD::solve (src/cuda/gd.cuh:38-106): a
+// full-batch loss/grad, then per iteration: stop if ||g|| < tol (:73), v = m*v - lr*g, x += v (:79-82;
+// plain x -= lr*g without momentum, :84-85), re-evaluate and record (loss, ||g||) (:87-97).
+// T = float mirrors the reference's fp32 scalars (the axpys are FMAs, like cuBLAS saxpy).
+// rec: max_iters x 2 (loss, ||g||). Returns the iterations done.
+// ---------------------------------------------------------------------------------------------
+template <class T, class LG>
+int gd_momentum(Vec<T> &x, LG &&loss_grad, T lr, T momentum, int max_iters, T tol, double *rec) {
+  const size_t n = x.size();
+  Vec<T> g(n), v(n, T(0));
+  loss_grad(x, g);
+  int done = 0;
+  for (int it = 0; it < max_iters; ++it) {
+    if (norm(g) < tol) break;
+    if (momentum > T(0)) {
+      for (size_t j = 0; j < n; ++j) {
+        v[j] = std::fma(-lr, g[j], v[j] * momentum);
+        x[j] = x[j] + v[j];
+      }
+    } else {
+      for (size_t j = 0; j < n; ++j) x[j] = std::fma(-lr, g[j], x[j]);
+    }
+    const T loss = loss_grad(x, g);
+    rec[2 * done + 0] = double(loss);
+    rec[2 * done + 1] = double(norm(g));
+    ++done;
+  }
+  return done;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Minibatch SGD with momentum and step decay — restates cuda_mlp::CudaSGD::solve (src/cuda/sgd.cuh:
+// 50-153): an initial full-batch record (:93-98); per epoch: lr *= decay_rate every decay_step epochs
+// (:101-103), contiguous (unshuffled) batches of `batch` rows (:107-112) each followed by the momentum
+// update (:115-124), the epoch loss as the batch-size-weighted sum of batch losses (:126), the
+// relative-improvement stop when tol > 0 (:129-135), then a full-batch record (:138-148).
+// batch_lg(x, g, row0, rows) evaluates rows [row0, row0 + rows). rec: (max_epochs + 1) x 2.
+// ---------------------------------------------------------------------------------------------
+template <class T, class LG, class BLG>
+int sgd_momentum(Vec<T> &x, LG &&full_lg, BLG &&batch_lg, int64_t N, int batch, T lr, T momentum, T decay_rate,
+                 int decay_step, int max_epochs, T tol, double *rec) {
+  const size_t n = x.size();
+  Vec<T> g(n), v(n, T(0));
+  int done = 0;
+  {
+    const T loss = full_lg(x, g);
+    rec[2 * done + 0] = double(loss);
+    rec[2 * done + 1] = double(norm(g));
+    ++done;
+  }
+  T cur_lr = lr;
+  const int64_t nb = (N + batch - 1) / batch;
+  T prev = std::numeric_limits<T>::infinity();
+  for (int it = 0; it < max_epochs; ++it) {
+    if (decay_step > 0 && it > 0 && it % decay_step == 0) cur_lr *= decay_rate;
+    T esum = T(0);
+    for (int64_t b = 0; b < nb; ++b) {
+      const int64_t r0 = b * batch, bs = std::min<int64_t>(batch, N - r0);
+      const T bl = batch_lg(x, g, r0, bs);
+      if (momentum > T(0)) {
+        for (size_t j = 0; j < n; ++j) {
+          v[j] = std::fma(-cur_lr, g[j], v[j] * momentum);
+          x[j] = x[j] + v[j];
+        }
+      } else {
+        for (size_t j = 0; j < n; ++j) x[j] = std::fma(-cur_lr, g[j], x[j]);
+      }
+      esum = esum + bl * T(bs);
+    }
+    const T avg = esum / T(N);
+    if (tol > T(0) && std::isfinite(prev)) {
+      const T rel = std::abs(prev - avg) / std::max(T(1), std::abs(prev));
+      if (rel < tol) break;
+    }
+    prev = avg;
+    const T loss = full_lg(x, g);
+    rec[2 * done + 0] = double(loss);
+    rec[2 * done + 1] = double(norm(g));
+    ++done;
+  }
+  return done;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Synthetic data (SURVEY.md §8(d) cfg 1/2 recipe). Shared by the product generator and the oracle;
 // tests/test_oracle.py checks the product generator against this one byte for byte.
 //   prototypes P_c ~ U[0,1)^In (mt19937(seed)); for each sample: c ~ U{0..classes-1},

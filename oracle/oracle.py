@@ -59,6 +59,12 @@ def lib():
         L.oracle_slbfgs_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_int, C.c_double,
                                         C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, _dp,
                                         C.POINTER(C.c_int), C.c_void_p, C.c_longlong]
+        L.oracle_gd_mlp.restype = C.c_int
+        L.oracle_gd_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_double, C.c_double, C.c_int,
+                                    C.c_double, C.c_int, _dp]
+        L.oracle_sgd_mlp.restype = C.c_int
+        L.oracle_sgd_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_int, C.c_double, C.c_double,
+                                     C.c_double, C.c_int, C.c_int, C.c_double, C.c_int, _dp]
         L.oracle_lbfgs_testfn.restype = C.c_double
         L.oracle_lbfgs_testfn.argtypes = [C.c_int, C.c_int, _dp, C.c_int, C.c_int, C.c_double, C.POINTER(C.c_int)]
         L.oracle_sample_indices.argtypes = [C.c_longlong, C.c_int, C.c_uint, C.c_int, _lp]
@@ -138,6 +144,25 @@ class Net:
                                       np.ascontiguousarray(Y, np.float64), X.shape[0], m, max_iters, tol, max_ls, c1,
                                       rho, int(fp32), rec, C.byref(it))
         return P, rec[: it.value]
+
+    def gd(self, P, X, Y, lr=0.01, momentum=0.9, max_iters=20, tol=1e-6, fp32=True):
+        """CudaGD (gd.cuh:38-106); returns (params, rec [iters x (loss, ||g||)])."""
+        P = np.array(P, np.float64, copy=True)
+        rec = np.zeros((max_iters, 2), np.float64)
+        n = lib().oracle_gd_mlp(self.nl, self.dims, self.acts, P, np.ascontiguousarray(X, np.float64),
+                                np.ascontiguousarray(Y, np.float64), X.shape[0], lr, momentum, max_iters, tol,
+                                int(fp32), rec)
+        return P, rec[:n]
+
+    def sgd(self, P, X, Y, batch=128, lr=0.01, momentum=0.9, decay_rate=1.0, decay_step=0, max_epochs=3, tol=1e-6,
+            fp32=True):
+        """CudaSGD (sgd.cuh:50-153); returns (params, rec [(1 + epochs) x (loss, ||g||)])."""
+        P = np.array(P, np.float64, copy=True)
+        rec = np.zeros((max_epochs + 1, 2), np.float64)
+        n = lib().oracle_sgd_mlp(self.nl, self.dims, self.acts, P, np.ascontiguousarray(X, np.float64),
+                                 np.ascontiguousarray(Y, np.float64), X.shape[0], batch, lr, momentum, decay_rate,
+                                 decay_step, max_epochs, tol, int(fp32), rec)
+        return P, rec[:n]
 
     def slbfgs(self, P, X, Y, epochs=2, tol=0.0, M=10, L=10, b=32, bH=16, step=0.02, lam=1e-4, fp32=False,
                want_idx=False):

@@ -280,6 +280,48 @@ int oracle_slbfgs_mlp(int nl, const int *dims, const int *acts, double *params, 
                                 reinterpret_cast<int64_t *>(idx_out), idx_cap);
 }
 
+// GD (gd.cuh:38-106) / SGD (sgd.cuh:50-153) with momentum on the MLP. rec: 2 doubles per record.
+int oracle_gd_mlp(int nl, const int *dims, const int *acts, double *params, const double *X, const double *Y,
+                  long long N, double lr, double momentum, int max_iters, double tol, int fp32, double *rec) {
+  Net net(dims, acts, nl);
+  auto run = [&](auto zero) {
+    using T = decltype(zero);
+    std::vector<T> Xt = to_vec<T>(X, size_t(N) * net.dims[0]);
+    std::vector<T> Yt = to_vec<T>(Y, size_t(N) * net.dims.back());
+    MLPObjective<T> obj{&net, Xt.data(), Yt.data(), N, {}, 0, 0};
+    auto lg = [&](const Vec<T> &w, Vec<T> &g) { return obj.loss_grad_batch(w, nullptr, N, 0.0, g.data()); };
+    Vec<T> x = to_vec<T>(params, net.nparams);
+    const int done = gd_momentum<T>(x, lg, T(lr), T(momentum), max_iters, T(tol), rec);
+    from_vec(x, params);
+    return done;
+  };
+  return fp32 ? run(0.0f) : run(0.0);
+}
+
+int oracle_sgd_mlp(int nl, const int *dims, const int *acts, double *params, const double *X, const double *Y,
+                   long long N, int batch, double lr, double momentum, double decay_rate, int decay_step,
+                   int max_epochs, double tol, int fp32, double *rec) {
+  Net net(dims, acts, nl);
+  auto run = [&](auto zero) {
+    using T = decltype(zero);
+    const int In = net.dims[0], Out = net.dims.back();
+    std::vector<T> Xt = to_vec<T>(X, size_t(N) * In);
+    std::vector<T> Yt = to_vec<T>(Y, size_t(N) * Out);
+    MLPObjective<T> full{&net, Xt.data(), Yt.data(), N, {}, 0, 0};
+    auto flg = [&](const Vec<T> &w, Vec<T> &g) { return full.loss_grad_batch(w, nullptr, N, 0.0, g.data()); };
+    auto blg = [&](const Vec<T> &w, Vec<T> &g, int64_t r0, int64_t bs) {
+      MLPObjective<T> part{&net, Xt.data() + size_t(r0) * In, Yt.data() + size_t(r0) * Out, bs, {}, 0, 0};
+      return part.loss_grad_batch(w, nullptr, bs, 0.0, g.data());
+    };
+    Vec<T> x = to_vec<T>(params, net.nparams);
+    const int done = sgd_momentum<T>(x, flg, blg, N, batch, T(lr), T(momentum), T(decay_rate), decay_step,
+                                     max_epochs, T(tol), rec);
+    from_vec(x, params);
+    return done;
+  };
+  return fp32 ? run(0.0f) : run(0.0);
+}
+
 // L-BFGS (CPU semantics) on the reference's analytic test problems. Returns final ||g||.
 double oracle_lbfgs_testfn(int id, int n, double *x, int m, int max_iters, double tol, int *iters) {
   auto f = [&](const Vec<double> &v) { return tf_f(id, v); };
