@@ -2,6 +2,7 @@
 #include "runtime.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -130,7 +131,7 @@ void Mlp::plan(long long B) {
     }
     static const int legacy = env_int("LBF_SPLIT_LEGACY", 0);
     long long splits = legacy ? std::max(1LL, std::min(cdiv(512, tiles), cdiv(B, min_chunk)))
-                              : split_factor(tiles, B, min_chunk, std::max(slots - side, tiles), M * L.out);
+                              : split_factor(tiles, B, min_chunk, std::max(slots - side, slots / 2), M * L.out);
     long long kc = cdiv(cdiv(B, splits), 32) * 32;
     if (kc <= 0) kc = 32;
     splits = std::max(1LL, cdiv(B, kc));
@@ -163,6 +164,11 @@ void Mlp::plan(long long B) {
       }
     }
   }
+  static const int show = env_int("LBF_SHOW_PLAN", 0);
+  if (show)
+    for (int l = 0; l < nl; ++l)
+      std::fprintf(stderr, "[lbf plan] B=%lld layer %d: dW tile %d splits %d k_chunk %d | fwd tile %d splits %d\n", B,
+                   l, layers_[l].dtile, layers_[l].splits, layers_[l].k_chunk, layers_[l].ftile, layers_[l].fsplits);
   slab_.ensure(slab);
   fslab_.ensure(std::max<size_t>(fslab, 1));
   planned_ = B;
