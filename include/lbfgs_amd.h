@@ -90,6 +90,12 @@ int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const 
  * lbfgs.cuh:206-261) on an explicit history given in logical order (oldest first):
  * d_S, d_Y are k x n row-major, h_rho[k]. mode: 0 = CPU (returns -Hg), 1 = S-LBFGS (returns +Hg,
  * gamma guarded and clamped), 2 = CUDA (returns -Hg, gamma guarded). */
+/* Exact Hessian-vector product of the batch loss of lbf_mlp_loss_grad (same inv_scale / l2 / d_idx
+ * meaning): d_hv = H(params) d_v, computed with Pearlmutter's R-operator on the device (one forward
+ * and backward R-pass; no finite differences). With a communicator the shards' products are summed.
+ * Replaces, as an option, the finite-difference HVP of s_lbfgs.hpp:88-101. */
+int lbf_mlp_hvp(lbf_mlp *net, const float *d_params, const float *d_v, const float *d_X, const float *d_Y,
+                const int *d_idx, long long batch, double inv_scale, double l2, float *d_hv);
 int lbf_two_loop(lbf_ctx *ctx, long long n, int k, const float *d_S, const float *d_Y, const double *h_rho,
                  const float *d_g, float *d_dir, int mode);
 
@@ -117,6 +123,8 @@ typedef struct lbf_slbfgs_params {
   double lambda;      /* L2, 1e-4 in the reference (unified_optimization.hpp:334)    */
   unsigned seed;      /* kDefaultSeed = 123 (src/seed.hpp:4; s_lbfgs.hpp:183)        */
   double fd_eps;      /* finite-difference HVP epsilon, 1e-4 (s_lbfgs.hpp:90)        */
+  int hvp_exact;      /* 0: the reference's central-difference HVP (s_lbfgs.hpp:88-101); 1: the
+                         exact R-operator product (lbf_mlp_hvp), SURVEY §8(f) rank 4          */
 } lbf_slbfgs_params;
 
 /* Gradient descent with momentum == cuda_mlp::CudaGD (src/cuda/gd.cuh:38-106; setters :22-25). */

@@ -33,7 +33,7 @@ class LbfgsParams(C.Structure):
 class SlbfgsParams(C.Structure):
     _fields_ = [("max_epochs", C.c_int), ("tol", C.c_double), ("M", C.c_int), ("L", C.c_int), ("b", C.c_int),
                 ("b_H", C.c_int), ("step", C.c_double), ("reg", C.c_double), ("seed", C.c_uint),
-                ("fd_eps", C.c_double)]
+                ("fd_eps", C.c_double), ("hvp_exact", C.c_int)]
 
 
 class GdParams(C.Structure):
@@ -116,6 +116,7 @@ def lib():
         "lbf_sample_indices": (C.c_int, [C.c_longlong, C.c_int, C.c_uint, C.c_int, _vp]),
         "lbf_idx_read_images": (C.c_int, [C.c_char_p, C.c_longlong, _vp, C.POINTER(C.c_longlong), _ip, _ip]),
         "lbf_idx_read_labels": (C.c_int, [C.c_char_p, C.c_longlong, C.c_int, _vp, C.POINTER(C.c_longlong)]),
+        "lbf_mlp_hvp": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_longlong, C.c_double, C.c_double, _vp]),
         "lbf_gd_default_params": (None, [C.POINTER(GdParams)]),
         "lbf_sgd_default_params": (None, [C.POINTER(SgdParams)]),
         "lbf_gd_solve": (C.c_int, [_vp, C.POINTER(GdParams), _vp, _vp, _vp, C.c_longlong, C.c_longlong,
@@ -138,7 +139,7 @@ EXPORTS = ("lbf_last_error lbf_version lbf_ctx_create lbf_ctx_destroy lbf_ctx_sy
            "lbf_nrm2 lbf_axpy lbf_scal lbf_lbfgs_default_params lbf_slbfgs_default_params lbf_lbfgs_solve "
            "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_prof_enable lbf_prof_select lbf_prof_sample lbf_prof_read lbf_synth_mnist "
            "lbf_sample_indices lbf_synth_regression lbf_gd_default_params lbf_sgd_default_params lbf_gd_solve "
-           "lbf_sgd_solve lbf_idx_read_images lbf_idx_read_labels").split()
+           "lbf_sgd_solve lbf_idx_read_images lbf_idx_read_labels lbf_mlp_hvp").split()
 
 
 def check(rc: int, what: str) -> None:

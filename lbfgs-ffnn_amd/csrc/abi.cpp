@@ -224,6 +224,16 @@ int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const 
   });
 }
 
+int lbf_mlp_hvp(lbf_mlp *net, const float *d_params, const float *d_v, const float *d_X, const float *d_Y,
+                const int *d_idx, long long batch, double inv_scale, double l2, float *d_hv) {
+  return guard([&] {
+    LBF_REQUIRE(net && d_params && d_v && d_X && d_Y && d_hv && batch > 0, "bad argument");
+    net->ctx->c.set_device();
+    net->net->hvp(d_params, d_v, d_X, d_Y, d_idx, batch, inv_scale, l2, d_hv);
+    LBF_HIP(hipStreamSynchronize(net->ctx->c.stream));
+  });
+}
+
 int lbf_two_loop(lbf_ctx *ctx, long long n, int k, const float *d_S, const float *d_Y, const double *h_rho,
                  const float *d_g, float *d_dir, int mode) {
   return guard([&] {
@@ -368,6 +378,7 @@ void lbf_slbfgs_default_params(lbf_slbfgs_params *p) {
   p->lambda = 1e-4;
   p->seed = 123;
   p->fd_eps = 1e-4;
+  p->hvp_exact = 0;
 }
 
 int lbf_lbfgs_begin(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, const float *d_X,

@@ -145,6 +145,14 @@ constexpr int RA_SPLITS_PER_PART = 64; // 4 stripes x 16 loads per thread
 constexpr int RA_MAXFIN = 128;         // column groups the one-block finishing launch combines
 void reduce_all(hipStream_t s, const RedAllArgs &a);
 
+// Exact Hessian-vector product, elementwise R-steps (hvp.hip; products in Mlp::hvp).
+void rop_act(hipStream_t s, long long n, const float *A, const float *RZ, int act, float *RA);
+void rop_out(hipStream_t s, long long B, int Out, const float *A, const float *Y, const int *idx, const float *RZ,
+             int act, double inv_scale, float *RdZ);
+void rop_back(hipStream_t s, long long n, const float *T1, const float *T2, const float *delta, const float *A,
+              const float *RZ, int act, float *out);
+bool act_has_d2(int act);
+
 // BASELINE config 5's synthetic regression data on the device (synth.hip).
 void synth_regression(hipStream_t s, long long row0, long long N, int In, unsigned seed_x, unsigned seed_t, float *X,
                       float *Y);

@@ -498,6 +498,156 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
 }
 
 // ------------------------------------------------------------------------------------------------
+// Exact Hessian-vector product (R-operator; hvp.hip has the derivation). An unfused forward/backward
+// of the batch, then the R-forward and R-backward with the same GEMM kernels: every product that
+// involves the direction V is one more GEMM whose B operand is V's layer block.
+// ------------------------------------------------------------------------------------------------
+void Mlp::hvp(const float *P, const float *V, const float *X, const float *Y, const int *idx, long long B,
+              double inv_scale, double lambda, float *Hv) {
+  LBF_REQUIRE(P && V && X && Y && Hv && B > 0, "hvp: bad argument");
+  hipStream_t s = ctx_->stream;
+  const int nl = int(layers_.size());
+  ensure(B);
+  if (B > rcap_) {
+    RZ_.clear();
+    RA_.clear();
+    RD_.clear();
+    DL_.clear();
+    size_t wmax = 1, segmax = 1;
+    for (auto &L : layers_) {
+      RZ_.emplace_back(size_t(B) * L.out);
+      RA_.emplace_back(size_t(B) * L.out);
+      RD_.emplace_back(size_t(B) * L.out);
+      DL_.emplace_back(act_has_d2(L.act) ? size_t(B) * L.out : size_t(1));
+      wmax = std::max(wmax, size_t(L.in));
+      segmax = std::max(segmax, size_t(L.in + 1) * L.out);
+    }
+    T1_.resize(size_t(B) * wmax);
+    T2_.resize(size_t(B) * wmax);
+    seg_.resize(segmax);
+    rcap_ = B;
+  }
+  // Z = in * W + bias (no activation) for layer l, with the forward's tile / split-K plan
+  auto linear_fwd = [&](int l, const float *Wsrc, const float *in, const int *rows, bool with_bias, float *out) {
+    const Layer &L = layers_[size_t(l)];
+    GemmDesc d = fwd_desc(size_t(l), Wsrc, in, rows, B);
+    d.act = ACT_LINEAR;
+    if (!with_bias) d.bias = nullptr;
+    if (L.fsplits > 1) {
+      const float *bias = d.bias;
+      d.epi = EPI_STORE;
+      d.C = fslab_.get();
+      d.splits = L.fsplits;
+      d.k_chunk = L.fk_chunk;
+      d.slab_stride = B * L.out;
+      gemm(s, d);
+      fwd_reduce_act(s, fslab_.get(), L.fsplits, B * L.out, int(B), L.out, bias, ACT_LINEAR, out, ctx_->abort);
+    } else {
+      d.C = out;
+      gemm(s, d);
+    }
+  };
+  // [in | ones?]^T dZ for layer l into dst (the dW GEMM's plan: split-K slabs summed in split order)
+  auto weight_grad = [&](int l, const float *in, const int *rows, bool ones, const float *dZ, float *dst) {
+    const Layer &L = layers_[size_t(l)];
+    GemmDesc d;
+    d.M = L.in + 1;
+    d.N = L.out;
+    d.K = int(B);
+    d.A = in;
+    d.lda = L.in;
+    d.a_kc = false;
+    d.a_idx = rows;
+    d.a_mvalid = L.in;
+    d.a_ones = ones ? L.in : -1; // no ones column: the bias row is zero
+    d.B = dZ;
+    d.ldb = L.out;
+    d.b_kc = false;
+    d.epi = EPI_STORE;
+    d.ldc = L.out;
+    d.splits = L.splits;
+    d.k_chunk = L.k_chunk;
+    d.abort = ctx_->abort;
+    d.tile = L.dtile;
+    const long long seg = (long long)(L.in + 1) * L.out;
+    if (L.splits > 1) {
+      d.C = slab_.get() + L.slab_off;
+      d.slab_stride = seg;
+      gemm(s, d);
+      reduce_slabs(s, slab_.get() + L.slab_off, L.splits, seg, seg, dst, ctx_->abort);
+    } else {
+      d.C = dst;
+      gemm(s, d);
+    }
+  };
+  // (dZ W^T) .* act'(aux) for layer l (aux_act linear: the plain product)
+  auto back_prod = [&](int l, const float *dZ, const float *Wsrc, int aux_act, float *out) {
+    const Layer &L = layers_[size_t(l)];
+    GemmDesc x;
+    x.M = int(B);
+    x.N = L.in;
+    x.K = L.out;
+    x.A = dZ;
+    x.lda = L.out;
+    x.a_kc = true;
+    x.B = Wsrc + L.off;
+    x.ldb = L.out;
+    x.b_kc = true;
+    x.C = out;
+    x.ldc = L.in;
+    x.epi = EPI_DX;
+    x.aux = A_[size_t(l - 1)].get();
+    x.ldaux = L.in;
+    x.aux_act = aux_act;
+    x.abort = ctx_->abort;
+    gemm(s, x);
+  };
+  // ---- forward and the plain backward (dZ_l; delta_l where act'' != 0) ----
+  forward(P, X, idx, B, nl);
+  const Layer &Lo = layers_[size_t(nl - 1)];
+  loss_diff(s, A_[size_t(nl - 1)].get(), Lo.out, Y, Lo.out, idx, B, Lo.out, Lo.act, inv_scale,
+            D_[size_t(nl - 1)].get(), Lo.out, loss_part_.get());
+  for (int l = nl - 1; l >= 1; --l) {
+    const int pa = layers_[size_t(l - 1)].act;
+    back_prod(l, D_[size_t(l)].get(), P, pa, D_[size_t(l - 1)].get());
+    if (act_has_d2(pa)) back_prod(l, D_[size_t(l)].get(), P, ACT_LINEAR, DL_[size_t(l - 1)].get());
+  }
+  // ---- R-forward ----
+  for (int l = 0; l < nl; ++l) {
+    const Layer &L = layers_[size_t(l)];
+    const long long nz = B * L.out;
+    if (l == 0) {
+      linear_fwd(0, V, X, idx, true, RZ_[0].get()); // X V_0 + v_0
+    } else {
+      linear_fwd(l, V, A_[size_t(l - 1)].get(), nullptr, true, RZ_[size_t(l)].get()); // A V_l + v_l
+      linear_fwd(l, P, RA_[size_t(l - 1)].get(), nullptr, false, T1_.get());         // R{A} W_l
+      lincomb(s, nz, RZ_[size_t(l)].get(), 1.0, T1_.get(), RZ_[size_t(l)].get());
+    }
+    rop_act(s, nz, A_[size_t(l)].get(), RZ_[size_t(l)].get(), L.act, RA_[size_t(l)].get());
+  }
+  // ---- R-backward ----
+  rop_out(s, B, Lo.out, A_[size_t(nl - 1)].get(), Y, idx, RZ_[size_t(nl - 1)].get(), Lo.act, inv_scale,
+          RD_[size_t(nl - 1)].get());
+  for (int l = nl - 1; l >= 0; --l) {
+    const Layer &L = layers_[size_t(l)];
+    float *dst = Hv + L.off;
+    const long long seg = (long long)(L.in + 1) * L.out;
+    weight_grad(l, l == 0 ? X : A_[size_t(l - 1)].get(), l == 0 ? idx : nullptr, true, RD_[size_t(l)].get(), dst);
+    if (l > 0) {
+      weight_grad(l, RA_[size_t(l - 1)].get(), nullptr, false, D_[size_t(l)].get(), seg_.get());
+      lincomb(s, seg, dst, 1.0, seg_.get(), dst);
+      const int pa = layers_[size_t(l - 1)].act;
+      back_prod(l, RD_[size_t(l)].get(), P, pa, T1_.get());
+      back_prod(l, D_[size_t(l)].get(), V, pa, T2_.get());
+      rop_back(s, B * L.in, T1_.get(), T2_.get(), act_has_d2(pa) ? DL_[size_t(l - 1)].get() : nullptr,
+               A_[size_t(l - 1)].get(), RZ_[size_t(l - 1)].get(), pa, RD_[size_t(l - 1)].get());
+    }
+  }
+  if (ctx_->dp()) ctx_->allreduce(Hv, nparams_);
+  if (lambda != 0.0) lincomb(s, (long long)nparams_, Hv, lambda, V, Hv);
+}
+
+// ------------------------------------------------------------------------------------------------
 // History
 // ------------------------------------------------------------------------------------------------
 History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {

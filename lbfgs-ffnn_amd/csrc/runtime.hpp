@@ -109,6 +109,10 @@ public:
   //   scal : device fp64 status block (SC_LOSS, SC_TGG, SC_TGP, SC_WW, SC_SSE written).
   void loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
                  double inv_scale, double lambda, const float *pdir, double *scal, const TailFuse *tf = nullptr);
+  // Exact Hessian-vector product Hv = H(P) V of the same batch loss (+ lambda V), Pearlmutter's
+  // R-operator (hvp.hip); with a communicator the shards' products are all-reduced. Hv: nparams().
+  void hvp(const float *P, const float *V, const float *X, const float *Y, const int *idx, long long B,
+           double inv_scale, double lambda, float *Hv);
   long long evals() const { return evals_; }
   void discard_evals(long long k) { evals_ -= k; } // speculative evaluations that were aborted
 
@@ -127,6 +131,10 @@ private:
   int fwd_small_ = 1;         // 32x128 forward tiles for few row tiles (LBF_FWD_TILE32=0 disables)
   int dw64_ = 1;              // 64x64 dW tiles with fewer splits (LBF_DW_TILE64=0 disables)
   DevBuf<double> loss_part_, dots_part_, sse_, colpart_, trows_, tdots_;
+  // R-pass workspace (hvp): R{Z}, R{A}, R{dZ} and delta per layer, two products, one segment
+  std::vector<DevBuf<float>> RZ_, RA_, RD_, DL_;
+  DevBuf<float> T1_, T2_, seg_;
+  long long rcap_ = -1;
   long long evals_ = 0;
   void plan(long long B);
 };

@@ -622,20 +622,26 @@ int SlbfgsSolver::run(lbf_record *rec) {
           const long long ho = hb[t].first + hbn * rk / nr, hc = hbn * (rk + 1) / nr - hbn * rk / nr;
           const double eps = prm_.fd_eps;
           lincomb(s, n_, u_.get(), -1.0, up_.get(), s_.get()); // s = u - u_prev
-          lincomb(s, n_, u_.get(), eps, s_.get(), wp_.get());
-          lincomb(s, n_, u_.get(), -eps, s_.get(), wm_.get());
-          net_->loss_grad(wp_.get(), gp_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda, nullptr,
-                          hist_.scal());
-          net_->loss_grad(wm_.get(), gm_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda, nullptr,
-                          hist_.scal());
           GramArgs pa;
           pa.policy = POL_SLBFGS;
           pa.has_pair = 1;
           pa.sa = u_.get();
           pa.sb = up_.get();
+          if (prm_.hvp_exact) { // y = H(u) s on the b_H batch, R-operator (hvp.hip)
+            net_->hvp(u_.get(), s_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda, gp_.get());
+            LBF_HIP(hipMemsetAsync(gm_.get(), 0, size_t(n_) * sizeof(float), s));
+            pa.yscale = 1.0;
+          } else { // s_lbfgs.hpp:88-101: central difference of two batch gradients
+            lincomb(s, n_, u_.get(), eps, s_.get(), wp_.get());
+            lincomb(s, n_, u_.get(), -eps, s_.get(), wm_.get());
+            net_->loss_grad(wp_.get(), gp_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda,
+                            nullptr, hist_.scal());
+            net_->loss_grad(wm_.get(), gm_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda,
+                            nullptr, hist_.scal());
+            pa.yscale = 1.0 / (2.0 * eps);
+          }
           pa.ya = gp_.get();
           pa.yb = gm_.get();
-          pa.yscale = 1.0 / (2.0 * eps);
           hist_.update(pa, 0, 1, +1.0);
         }
         LBF_HIP(hipMemcpyAsync(up_.get(), u_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));

@@ -158,6 +158,18 @@ class Mlp:
                                       C.byref(loss)), "lbf_mlp_loss_grad")
         return loss.value, grad
 
+    def hvp(self, params: torch.Tensor, v: torch.Tensor, X: torch.Tensor, Y: torch.Tensor,
+            idx: Optional[torch.Tensor] = None, inv_scale: Optional[float] = None, l2: float = 0.0,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Exact H(params) v of the loss_grad batch loss (R-operator, lbf_mlp_hvp)."""
+        B = int(idx.numel()) if idx is not None else int(X.shape[0])
+        if inv_scale is None:
+            inv_scale = 1.0 / max(B, 1)
+        out = self.new_params() if out is None else out
+        check(lib().lbf_mlp_hvp(self.h, ptr(params), ptr(v), ptr(X), ptr(Y), ptr(idx), B, inv_scale, l2, ptr(out)),
+              "lbf_mlp_hvp")
+        return out
+
     def __del__(self):
         try:
             if getattr(self, "h", None):
