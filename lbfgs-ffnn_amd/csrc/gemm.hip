@@ -56,32 +56,55 @@ struct GemmK {
   double head_inv_scale;
   float *head_delta, *head_slab;
   double *head_sse;
+  int head_fold, head_fold_c0;
 };
 
-// Side job (see GemmDesc): one 64-column group x 4 split stripes per block, fp64 in split order.
+// Side job (see GemmDesc): one 256-column group (four per lane) x 4 split stripes per block, fp64 in
+// split order. Side blocks hold their slots for the whole launch, so a block takes many columns: 32
+// loads per lane in flight per round.
+constexpr int SIDE_CPL = 4;                 // columns per lane
+constexpr int SIDE_COLS = 64 * SIDE_CPL;    // columns per side block
 __device__ __forceinline__ void gemm_side_job(const GemmK &g, double *red) {
   const int t = threadIdx.x, lane = t & 63, stripe = t >> 6; // stripes 0-3 (extra waves idle)
   const int nside = gridDim.x * gridDim.y * g.side_planes;
   const int id = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-  for (long long c0 = (long long)id * 64; c0 < g.side_count; c0 += (long long)nside * 64) {
-    const long long c = c0 + lane;
-    double acc = 0.0;
-    if (c < g.side_count && stripe < 4) {
-      const float *src = g.side_slab + c;
-      int k = stripe;
-      for (; k + 28 < g.side_splits; k += 32) { // eight independent loads in flight
-        float v[8];
+  for (long long c0 = (long long)id * SIDE_COLS; c0 < g.side_count; c0 += (long long)nside * SIDE_COLS) {
+    double acc[SIDE_CPL];
+    const float *src[SIDE_CPL];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = src[(long long)(k + 4 * u) * g.side_stride];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc += double(v[u]);
-      }
-      for (; k < g.side_splits; k += 4) acc += double(src[(long long)k * g.side_stride]);
+    for (int j = 0; j < SIDE_CPL; ++j) {
+      const long long c = c0 + lane + 64 * j;
+      acc[j] = 0.0;
+      src[j] = g.side_slab + (c < g.side_count ? c : 0); // clamped; masked when stored
     }
-    if (stripe < 4) red[t] = acc;
-    __syncthreads();
-    if (stripe == 0 && c < g.side_count) g.side_dst[c] = float(((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane]);
-    __syncthreads();
+    if (stripe < 4) {
+      int k = stripe;
+      for (; k + 28 < g.side_splits; k += 32) { // eight rows x four columns in flight
+        float v[8][SIDE_CPL];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int j = 0; j < SIDE_CPL; ++j) v[u][j] = src[j][(long long)(k + 4 * u) * g.side_stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int j = 0; j < SIDE_CPL; ++j) acc[j] += double(v[u][j]);
+      }
+      for (; k < g.side_splits; k += 4)
+#pragma unroll
+        for (int j = 0; j < SIDE_CPL; ++j) acc[j] += double(src[j][(long long)k * g.side_stride]);
+#pragma unroll
+      for (int j = 0; j < SIDE_CPL; ++j) red[j * 256 + t] = acc[j];
+    }
+    lds_barrier();
+    if (stripe == 0)
+#pragma unroll
+      for (int j = 0; j < SIDE_CPL; ++j) {
+        const long long c = c0 + lane + 64 * j;
+        const double* r = red + j * 256;
+        if (c < g.side_count) g.side_dst[c] = float(((r[lane] + r[64 + lane]) + r[128 + lane]) + r[192 + lane]);
+      }
+    lds_barrier();
   }
 }
 
@@ -232,8 +255,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
     // 64-row half the activations go accumulators -> LDS (bias + activation; columns >= N zero) and
     // the head runs on them. n0 == 0 (N <= BN).
     constexpr int QM = headc::qstrips(BN);
-    const headc::Smem hs = headc::carve(lds, g.N);
+    headc::Smem hs = headc::carve(lds, g.N);
+    hs.xr = hs.ys + BM * 16;
+    const bool fold = g.head_fold >= 0; // uniform
     hpre.store(hs);
+    if (g.head_fold > 0) hpre.store_fold(hs);
     KT(26);
     KTB(2);
     headc::f32x4 cw[QM];
@@ -249,13 +275,21 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
     ta.sc = float(g.head_inv_scale);
     ta.delta = g.head_delta;
     ta.vec = (g.N & 3) == 0 && (reinterpret_cast<uintptr_t>(g.head_delta) & 15) == 0;
+    ta.nfold = g.head_fold;
+    headc::FoldAcc fa;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      fa.c[j] = (headc::f32x4){0.f, 0.f, 0.f, 0.f};
+      fa.db[j] = 0.0f;
+    }
     for (int half = 0; half < (BM + headc::TB - 1) / headc::TB; ++half) {
       const long long b0 = (long long)m0 + half * headc::TB;
       const int rows_tile = min(headc::TB, BM - half * headc::TB);
       const int rows = int(min((long long)rows_tile, (long long)g.M - b0));
       if (rows <= 0) break;
       ta.ys = hs.ys + half * headc::TB * 16;
-      if (half == 0) __syncthreads(); // hb (read below) written by hpre.store
+      ta.xr = hs.xr + half * headc::TB * headc::XLD;
+      if (half == 0) lds_barrier(); // hb (read below) written by hpre.store
       for (int e = threadIdx.x; e < (headc::TB - rows_tile) * hs.Hp; e += 256 * KW) { // rows the tile lacks
         const int r = rows_tile + e / hs.Hp, c = e % hs.Hp;
         hs.As[r * hs.LDA + c] = 0.0f;
@@ -284,16 +318,19 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
           const int r = e / (hs.Hp - BN), c = BN + e % (hs.Hp - BN);
           hs.As[r * hs.LDA + c] = 0.0f;
         }
-      __syncthreads();
+      lds_barrier();
       KT(28 + 2 * half);
       KTB(3 + 2 * half);
-      headc::tile<(KW > 1), QM>(hs, ta, b0, rows, cw, sse);
+      if (fold) headc::tile<(KW > 1), QM, true>(hs, ta, b0, rows, cw, sse, fa);
+      else headc::tile<(KW > 1), QM, false>(hs, ta, b0, rows, cw, sse, fa);
       KT(29 + 2 * half);
       KTB(4 + 2 * half);
     }
     KT(32);
-    headc::write_partials(hs, g.head_out, cw, sse, g.head_slab + (long long)blockIdx.y * (g.N + 1) * g.head_out,
-                          g.head_sse + blockIdx.y);
+    const long long nf = fold ? (long long)(g.head_fold + 1) * g.N : 0; // fold rows in front of the head's
+    float *slab = g.head_slab + (long long)blockIdx.y * (nf + (long long)(g.N + 1) * g.head_out);
+    if (fold) headc::write_fold(fa, g.N, g.head_fold, slab);
+    headc::write_partials(hs, g.head_out, cw, sse, slab + nf, g.head_sse + blockIdx.y);
     KT(33);
     KTB(7);
     return;
@@ -491,12 +528,14 @@ __global__ __launch_bounds__(256 * KW, 2) void gemm_kernel(const GemmK g) {
     }
     if constexpr (EPI == EPI_HEAD) {
       hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
+      if (g.head_fold > 0) hpre.load_fold(g.A, g.lda, g.a_idx, g.head_fold_c0, g.head_fold, m0, g.M);
       compute((nk - 1) & 1);
       __syncthreads();
       KT(25);
     }
   } else if constexpr (EPI == EPI_HEAD) {
     hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
+    if (g.head_fold > 0) hpre.load_fold(g.A, g.lda, g.a_idx, g.head_fold_c0, g.head_fold, m0, g.M);
   }
   if constexpr (KW > 1) { // group sums through LDS, in group order (group 0 keeps the result)
     float *red = lds;
@@ -701,9 +740,13 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
   };
 
   if (EPI == EPI_HEAD) KT(0);
+  if (EPI == EPI_HEAD) KTC(40);
   if (EPI == EPI_HEAD) KTB(0);
   headc::EpiPrefetch<BN, BM, 256> hpre;
-  if constexpr (EPI == EPI_HEAD) hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
+  if constexpr (EPI == EPI_HEAD) {
+    hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
+    if (g.head_fold > 0) hpre.load_fold(g.A, g.lda, g.a_idx, g.head_fold_c0, g.head_fold, m0, g.M);
+  }
   const int nk = kb < ke ? (ke - kb + BK - 1) / BK : 0;
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
@@ -717,6 +760,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
     compute(i % NS);
   }
   if (EPI == EPI_HEAD) KT(25);
+  if (EPI == EPI_HEAD) KTC(41);
   __syncthreads(); // the LDS is the epilogue's now
   gemm_epilogue<WM, WN, TM, TN, EPI, 1>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, 0);
 }
@@ -758,7 +802,7 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.aux_act = d.aux_act;
   k.abort = d.abort;
   const long long gx = (d.N + BN - 1) / BN, gy = (d.M + BM - 1) / BM;
-  k.side_planes = (d.side_slab && d.side_count > 0) ? int(cdiv(cdiv(d.side_count, 64), gx * gy)) : 0;
+  k.side_planes = (d.side_slab && d.side_count > 0) ? int(cdiv(cdiv(d.side_count, SIDE_COLS), gx * gy)) : 0;
   k.side_slab = d.side_slab;
   k.side_splits = d.side_splits;
   k.side_stride = d.side_stride;
@@ -773,6 +817,8 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.head_delta = d.head_delta;
   k.head_slab = d.head_slab;
   k.head_sse = d.head_sse;
+  k.head_fold = d.head_fold;
+  k.head_fold_c0 = d.head_fold_c0;
   dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
   static const bool glds_on = env_int("LBF_GEMM_GLDS", 1) != 0;
   if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
@@ -834,6 +880,10 @@ void gemm(hipStream_t s, const GemmDesc &d) {
     gemm_tile_for(d.N, d.tile, &BM, &BN);
     if (!(d.a_kc && !d.b_kc) || d.N > BN || d.splits > 1 || d.head_out < 1 || d.head_out > headc::HMAX_OUT)
       throw std::runtime_error("gemm: EPI_HEAD needs an unsplit forward GEMM with N <= the tile width");
+    if (d.head_fold >= 0 &&
+        (d.N > 128 || d.head_fold > headc::FOLD_MAX || d.head_fold % 4 || d.head_fold_c0 % 4 || d.lda % 4 ||
+         d.head_fold_c0 + d.head_fold != d.K || !aligned16(d.A)))
+      throw std::runtime_error("gemm: EPI_HEAD fold needs N <= 128, <= 16 aligned input columns ending at K");
     dispatch_tile<true, false, EPI_HEAD>(s, d);
   } else if (d.epi == EPI_FWD && d.a_kc && !d.b_kc) dispatch_tile<true, false, EPI_FWD>(s, d);
   else if (d.epi == EPI_DX && d.a_kc && d.b_kc) dispatch_tile<true, true, EPI_DX>(s, d);

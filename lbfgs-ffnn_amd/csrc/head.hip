@@ -57,6 +57,9 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
   ta.sc = float(inv_scale);
   ta.delta = delta;
   ta.vec = vec;
+  ta.xr = nullptr;
+  ta.nfold = 0;
+  FoldAcc fa; // unused (no fold in the standalone kernel)
   for (long long tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
     const long long b0 = tl * TB;
     const int rows = int(min((long long)TB, B - b0));
@@ -75,7 +78,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
       }
     }
     __syncthreads();
-    tile<false, QM>(sm, ta, b0, rows, cw, sse);
+    tile<false, QM, false>(sm, ta, b0, rows, cw, sse, fa);
   }
   write_partials(sm, Out, cw, sse, slab + (long long)blockIdx.x * (H + 1) * Out, sse_part + blockIdx.x);
 }

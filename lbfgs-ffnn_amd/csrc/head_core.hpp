@@ -41,10 +41,14 @@ constexpr __host__ __device__ int qstrips(int H) { return (H + 1 + 63) / 64; }
 
 __device__ __forceinline__ int round64(int x) { return (x + 63) & ~63; }
 
+constexpr int XLD = 20;                    // folded input-column rows [yrows][XLD]: conflict-free b32 reads
+constexpr int FOLD_MAX = 16;               // input columns a GEMM epilogue can fold (one 16-wide strip)
+
 // LDS carve-up (floats): As [TB][LDA] | Wt [16][LDA] | Wr [Hp][16] | Dz [TB][LDZ] | bias [16] | red [8]
-// The GEMM epilogue appends hb [Hp] (the hidden layer's bias) and ys [yrows][16] (the block's targets).
+// The GEMM epilogue appends hb [Hp] (the hidden layer's bias), ys [yrows][16] (the block's targets)
+// and xr [yrows][XLD] (the input columns folded into the epilogue, see TileArgs::fold).
 struct Smem {
-  float *As, *Wt, *Wr, *Dz, *bias, *hb, *ys;
+  float *As, *Wt, *Wr, *Dz, *bias, *hb, *ys, *xr;
   double *red;
   int H, Hp, LDA;
 };
@@ -53,7 +57,7 @@ constexpr __host__ __device__ int smem_floats(int H) {
   return TB * LDA + 16 * LDA + Hp * 16 + TB * LDZ + 16 + 8;
 }
 constexpr __host__ __device__ int smem_floats_epi(int H, int yrows) {
-  return smem_floats(H) + ((H + 63) & ~63) + yrows * 16;
+  return smem_floats(H) + ((H + 63) & ~63) + yrows * 16 + yrows * XLD;
 }
 __device__ inline Smem carve(float *base, int H) {
   Smem s;
@@ -68,6 +72,7 @@ __device__ inline Smem carve(float *base, int H) {
   s.red = reinterpret_cast<double *>(s.bias + 16); // 8-byte aligned: every region above is a multiple of 2
   s.hb = s.bias + 16 + 8;                           // after red (4 doubles)
   s.ys = s.hb + s.Hp;
+  s.xr = nullptr; // the GEMM epilogue sets it (after its ys rows)
   return s;
 }
 
@@ -94,8 +99,36 @@ __device__ inline void stage_w(const Smem &s, const float *P, int Out) {
 template <int HN, int YR, int NT>
 struct EpiPrefetch {
   static constexpr int PW = (16 * HN + NT - 1) / NT, PY = (YR * 16 + NT - 1) / NT;
+  static constexpr int PX = (YR * 4 + NT - 1) / NT; // 16-B chunks of the folded input columns
   static_assert(NT >= HN + 16, "one thread per bias element");
   float w[PW], y[PY], hb, ob;
+  f32x4 x[PX];
+
+  // The block's rows of the folded input columns [c0, c0 + nfold) (nfold % 4 == 0, 16-B aligned rows):
+  // unconditional loads from clamped addresses, masked afterwards.
+  __device__ inline void load_fold(const float *A, long long lda, const int *aidx, int c0, int nfold, long long m0,
+                                   long long M) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+      const int e = t + j * NT, r = e >> 2, q = e & 3;
+      const bool ok = e < YR * 4 && 4 * q < nfold && m0 + r < M;
+      const long long m = ok ? m0 + r : 0;
+      const long long row = aidx ? (long long)aidx[m] : m;
+      const f32x4 v = *reinterpret_cast<const f32x4 *>(A + row * lda + c0 + (ok ? 4 * q : 0));
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      const unsigned k = ok ? 0xffffffffu : 0u;
+      x[j] = __builtin_bit_cast(f32x4, __builtin_bit_cast(u32x4, v) & (u32x4){k, k, k, k});
+    }
+  }
+  __device__ inline void store_fold(const Smem &s) const {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+      const int e = t + j * NT;
+      if (e < YR * 4) *reinterpret_cast<f32x4 *>(s.xr + (e >> 2) * XLD + 4 * (e & 3)) = x[j];
+    }
+  }
 
   __device__ inline void load(const float *P, int H, int Out, const float *bias, const float *Y, const int *idx,
                               long long m0, long long M) {
@@ -143,28 +176,43 @@ struct TileArgs {
   int Out, act_out, act_prev;
   float sc; // inv_scale
   float *delta;
-  bool vec; // 16-B aligned delta rows
+  bool vec; // 16-B aligned rows (the standalone kernel's staging loads)
+  // Fold (GEMM epilogue, H <= 128): the rows of the previous layer's [dW ; db] that its dW GEMM's
+  // last, mostly empty row tile would hold — input columns c0 .. c0+nfold-1 and the bias row — are
+  // accumulated here from the delta accumulators: fold[i][c] += sum_b x[b][c0+i] delta[b][c] and
+  // db[c] += sum_b delta[b][c]. xr: this tile's rows of those input columns in LDS ([TB][XLD]).
+  const float *xr;
+  int nfold;
+};
+// Per-lane fold accumulators: wave w owns the delta columns of strips 2w and 2w+1.
+struct FoldAcc {
+  f32x4 c[2];
+  float db[2];
 };
 
 // One tile: s.As holds the activations of samples b0..b0+rows-1 (zero-padded to Hp columns), staged
-// and followed by a __syncthreads. Accumulates [dW ; db] into cw and the SSE into sse; writes the
-// tile's delta rows to global. Ends with __syncthreads (As free again).
-// QM: dW strips per wave (>= ceil(ceil((H+1)/16)/4)); strips past H are computed and never written.
-template <bool EXTRA_WAVES, int QM> // EXTRA_WAVES: blocks with more than 4 waves; waves >= 4 only join barriers
-__device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int rows, f32x4 (&cw)[QM], double &sse) {
+// and followed by a barrier. Accumulates [dW ; db] into cw and the SSE into sse; writes the tile's
+// delta rows to global straight from the MFMA accumulators. Ends with an LDS barrier (As free again).
+// QM: dW strips per wave (>= ceil(ceil((H+1)/16)/4)); strips past H are skipped (wave-uniform).
+// Barriers here only order LDS (lds_barrier): a __syncthreads would also wait for the delta stores.
+// FOLD: accumulate the fold (TileArgs::xr / nfold) into fa; needs H <= 128 (one pass of column strips).
+template <bool EXTRA_WAVES, int QM, bool FOLD> // EXTRA_WAVES: waves >= 4 only join barriers
+__device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int rows, f32x4 (&cw)[QM], double &sse,
+                            FoldAcc &fa) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int r0 = wave * 16, LDA = s.LDA, H = s.H;
   const bool active = !EXTRA_WAVES || wave < 4;
   KT(34);
-  // ---- forward: Z strip (16 samples x 16 outputs) of this wave ----
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int kc = 0; active && kc < s.Hp; kc += 64) {
-    float af[16], bf[16];
-    const float *pa = s.As + (r0 + li) * LDA + kc + g * 16;
-    const float *pb = s.Wt + li * LDA + kc + g * 16;
+  // ---- forward: Z strip (16 samples x 16 outputs) of this wave, two interleaved chains ----
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; active && kc < s.Hp; kc += 32) { // 32 k per round: 8 steps, two chains
+    float af[8], bf[8];
+    const int kh = kc & 63, k64 = kc & ~63; // lane group g consumes k = k64 + 16 g + s, s = kh/4 .. kh/4 + 7
+    const float *pa = s.As + (r0 + li) * LDA + k64 + g * 16 + (kh >> 2);
+    const float *pb = s.Wt + li * LDA + k64 + g * 16 + (kh >> 2);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 2; ++q) {
       const f32x4 va = *reinterpret_cast<const f32x4 *>(pa + 4 * q);
       const f32x4 vb = *reinterpret_cast<const f32x4 *>(pb + 4 * q);
 #pragma unroll
@@ -174,8 +222,12 @@ __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int 
       }
     }
 #pragma unroll
-    for (int st = 0; st < 16; ++st) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[st], bf[st], acc, 0, 0, 0);
+    for (int st = 0; st < 8; st += 2) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[st], bf[st], acc, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[st + 1], bf[st + 1], acc1, 0, 0, 0);
+    }
   }
+  acc += acc1;
   KT(35);
   // ---- loss and dZ (lane: samples r0 + g*4 + r, output o = li); targets loaded as one batch ----
   if (active) {
@@ -205,75 +257,115 @@ __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int 
       }
     });
   }
-  __syncthreads();
+  lds_barrier();
   KT(36);
   // ---- [dW ; db] += [A | 1]^T dZ over this tile (strips of 16 rows i; row H is the bias) ----
-  // The QM strips are independent accumulation chains, interleaved per k.
+  // Step k of lane group g takes sample b = (k & 3) + 4g + 16(k >> 2): the four groups of a step read
+  // rows 4 apart (bank offset 16 with LDA = 4 mod 64, 80 with LDZ = 20), so the reads are
+  // conflict-free. Every LDS read is unconditional (clamped column) and all are issued before the
+  // MFMA chains; strips past the bias row are skipped wave-uniformly.
   if (active) {
-    f32x4 c[QM];
 #pragma unroll
-    for (int q = 0; q < QM; ++q) c[q] = cw[q];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int b = g * 16 + k;
-      const float dz = s.Dz[b * LDZ + li];
-#pragma unroll
-      for (int q = 0; q < QM; ++q) {
-        const int ic = (wave + 4 * q) * 16 + li;
-        const float av = ic < H ? s.As[b * LDA + ic] : (ic == H ? 1.0f : 0.0f);
-        c[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, dz, c[q], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < QM; ++q) cw[q] = c[q];
-  }
-  __syncthreads(); // every wave done reading As before delta overwrites it
-  KT(37);
-  // ---- delta = (dZ W^T) .* act_prev'(A), in place over this wave's 16 rows, then stored ----
-  // Column strips in pairs (two independent chains); strips past H read zero rows of Wr and write
-  // only LDS padding.
-  if (a.delta) {
-    if (active) {
-      const f32x4 da = *reinterpret_cast<const f32x4 *>(s.Dz + (r0 + li) * LDZ + g * 4);
-      const int nit = ((H + 31) >> 5) << 1;
-      with_act(a.act_prev, [&](auto AC) __attribute__((always_inline)) {
-      constexpr int A = decltype(AC)::value;
-      for (int it = 0; it < nit; it += 2) {
-        const f32x4 wb0 = *reinterpret_cast<const f32x4 *>(s.Wr + (it * 16 + li) * 16 + g * 4);
-        const f32x4 wb1 = *reinterpret_cast<const f32x4 *>(s.Wr + ((it + 1) * 16 + li) * 16 + g * 4);
-        f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < QM; ++q) {
+      const int st = wave + 4 * q;
+      if (st * 16 > H) continue; // wave-uniform
+      const int ic = st * 16 + li;
+      const int icc = ic < H ? ic : 0;
+      const bool bias_strip = st * 16 + 15 >= H; // wave-uniform
+      f32x4 c = cw[q];
+#pragma unroll 1
+      for (int k0 = 0; k0 < 16; k0 += 4) { // four steps of loads in flight, then their MFMAs
+        float av[4], dz[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(da[k], wb0[k], c0, 0, 0, 0);
-          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(da[k], wb1[k], c1, 0, 0, 0);
+          const int b = k + 4 * g + k0 * 4; // (k & 3) + 4g + 16 (k >> 2) for step k0 + k
+          dz[k] = s.Dz[b * LDZ + li];
+          av[k] = s.As[b * LDA + icc];
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float *p = s.As + (r0 + g * 4 + r) * LDA + it * 16 + li;
-          p[0] = c0[r] * dact_c<A>(p[0]);
-          p[16] = c1[r] * dact_c<A>(p[16]);
+        for (int k = 0; k < 4; ++k) {
+          const float x = bias_strip ? (ic < H ? av[k] : (ic == H ? 1.0f : 0.0f)) : av[k];
+          c = __builtin_amdgcn_mfma_f32_16x16x4f32(x, dz[k], c, 0, 0, 0);
         }
       }
-      });
-    }
-    __syncthreads();
-    KT(38);
-    const int Hq = H >> 2, nt = blockDim.x;
-    if (a.vec) {
-      for (int e = t; e < rows * Hq; e += nt) {
-        const int r = e / Hq, c4 = e - r * Hq;
-        *reinterpret_cast<f32x4 *>(a.delta + (b0 + r) * H + 4 * c4) =
-            *reinterpret_cast<const f32x4 *>(s.As + r * LDA + 4 * c4);
-      }
-    } else {
-      for (int e = t; e < rows * H; e += nt) {
-        const int r = e / H, c = e - r * H;
-        a.delta[(b0 + r) * H + c] = s.As[r * LDA + c];
-      }
+      cw[q] = c;
     }
   }
-  __syncthreads();
+  KT(37);
+  // ---- delta = (dZ W^T) .* act_prev'(A), stored from the accumulators ----
+  // Wave w takes the column strips 2w, 2w+1 (+8, +9, ... for H > 128) over all TB rows, one 16-row
+  // strip at a time (two MFMA chains of 4 each). Lanes li of a row write 64 contiguous bytes.
+  // Strip cb+1 may pass H: Wr's zero rows (Hp >= 16 (cb + 2)) make it zero and nothing is stored.
+  if (a.delta && active) {
+    const int ncs = (H + 15) >> 4;
+    with_act(a.act_prev, [&](auto AC) __attribute__((always_inline)) {
+      constexpr int A = decltype(AC)::value;
+      for (int cb = 2 * wave; cb < ncs; cb += 8) { // wave-uniform; one pass when H <= 128
+        const f32x4 wb0 = *reinterpret_cast<const f32x4 *>(s.Wr + (cb * 16 + li) * 16 + g * 4);
+        const f32x4 wb1 = *reinterpret_cast<const f32x4 *>(s.Wr + ((cb + 1) * 16 + li) * 16 + g * 4);
+        const int col = cb * 16 + li;
+#pragma unroll 1
+        for (int rs = 0; rs < 4; ++rs) {
+          const f32x4 da = *reinterpret_cast<const f32x4 *>(s.Dz + (rs * 16 + li) * LDZ + g * 4);
+          float ap0[4], ap1[4], xa[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { // columns < 16 (cb + 2) <= Hp: always inside the row
+            const float *p = s.As + (rs * 16 + g * 4 + r) * LDA + col;
+            ap0[r] = p[0];
+            ap1[r] = p[16];
+            if constexpr (FOLD) xa[r] = a.xr[(rs * 16 + g * 4 + r) * XLD + li];
+          }
+          f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(da[k], wb0[k], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(da[k], wb1[k], c1, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = rs * 16 + g * 4 + r;
+            const float d0 = c0[r] * dact_c<A>(ap0[r]);
+            const float d1 = c1[r] * dact_c<A>(ap1[r]);
+            if (row < rows) {
+              float *d = a.delta + (b0 + row) * H + col;
+              if (col < H) d[0] = d0;
+              if (col + 16 < H) d[16] = d1;
+            }
+            if constexpr (FOLD) { // rows past `rows` have dZ = 0, so d0 = d1 = 0 there
+              // B operand: lane (li, g) holds delta[row(k = g)][column li]; A operand: x[row(k = g)][i = li]
+              fa.c[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r], d0, fa.c[0], 0, 0, 0);
+              fa.c[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[r], d1, fa.c[1], 0, 0, 0);
+              fa.db[0] += d0;
+              fa.db[1] += d1;
+            }
+          }
+        }
+      }
+    });
+  }
+  KT(38);
+  lds_barrier(); // every wave done reading As / Dz
   KT(39);
+}
+
+// The fold's partial rows [nfold + 1][H] (input columns, then the bias row) of the workgroup's slab.
+// Every lane runs the shuffles; H <= 128.
+__device__ inline void write_fold(const FoldAcc &fa, int H, int nfold, float *slab) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    float db = fa.db[j];
+    db += __shfl_xor(db, 16); // sum over the four row groups, fixed order
+    db += __shfl_xor(db, 32);
+    const int col = (2 * wave + j) * 16 + li;
+    if (wave < 4 && col < H) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (g * 4 + r < nfold) slab[(g * 4 + r) * H + col] = fa.c[j][r];
+      if (g == 0) slab[nfold * H + col] = db;
+    }
+  }
 }
 
 // The workgroup's [dW ; db] partial slab and SSE partial.
@@ -297,7 +389,7 @@ __device__ inline void write_partials(const Smem &s, int Out, const f32x4 (&cw)[
   }
   sse = wave_sum_f64(sse);
   if (lane == 0 && wave < 4) s.red[wave] = sse;
-  __syncthreads();
+  lds_barrier();
   if (t == 0) *sse_out = ((s.red[0] + s.red[1]) + s.red[2]) + s.red[3];
 }
 

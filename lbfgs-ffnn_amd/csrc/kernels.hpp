@@ -63,6 +63,11 @@ struct GemmDesc {
   double head_inv_scale = 1.0;
   float *head_delta = nullptr, *head_slab = nullptr; // slab per workgroup: [(N+1) x head_out]
   double *head_sse = nullptr;                        // SSE partial per workgroup
+  // Fold (head_fold >= 0, N <= 128): this layer's [dW ; db] rows head_fold_c0 .. K (input columns
+  // head_fold_c0 .. K-1, head_fold = K - head_fold_c0 <= 16 of them, % 4 == 0, then the bias row) are
+  // accumulated in the epilogue and written in front of the head's rows: the slab per workgroup is
+  // then [(head_fold + 1) x N | (N+1) x head_out], and the dW GEMM covers rows < head_fold_c0 only.
+  int head_fold = -1, head_fold_c0 = 0;
 };
 // Row tiles of the forward GEMM for M rows and N columns (== EPI_HEAD partial slabs).
 int gemm_row_tiles(int M, int tile);

@@ -79,6 +79,7 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
   use_gemm_head_ = !(ng && ng[0] == '1');
   if (const char *e = std::getenv("LBF_FWD_TILE32")) fwd_small_ = e[0] != '0';
   if (const char *e = std::getenv("LBF_DW_TILE64")) dw64_ = e[0] != '0';
+  if (const char *e = std::getenv("LBF_NO_FOLD")) fold_on_ = e[0] != '1';
 }
 
 // Split-K factor for `tiles` output tiles over a K of `K` rows: the GEMM tiles run two workgroups per
@@ -104,45 +105,15 @@ static long long split_factor(long long tiles, long long K, long long min_chunk,
   return best;
 }
 
-// Split-K plan of every dW GEMM for batch B (workgroup-slot aware, split_factor), k chunks a multiple
-// of the 32-deep LDS tile.
+// Forward plan (split-K for few row tiles), the EPI_HEAD fold, then the split-K plan of every dW GEMM
+// for batch B (workgroup-slot aware, split_factor), k chunks a multiple of the 32-deep LDS tile.
 void Mlp::plan(long long B) {
   if (planned_ == B) return;
   size_t slab = 0, fslab = 0;
   const int nl = int(layers_.size());
   const bool fused = use_head_ && nl >= 2 && head_supported(layers_[nl - 1].in, layers_[nl - 1].out);
   const long long slots = 2LL * ctx_->cus;
-  // dW tiles and split-K, last layer first: layer l's launch also carries the side blocks that finish
-  // layer l+1's slabs (side_reduced), and those take workgroup slots too
-  for (int l = nl - 1; l >= 0; --l) {
-    Layer &L = layers_[l];
-    int BM, BN;
-    const long long M = L.in + 1;
-    // dW: 64x64 tiles over narrow outputs -> fewer, longer K splits (a third of the slab traffic)
-    // (only for short K: at long K the 128x128 tile's reuse wins over the slab savings)
-    L.dtile = (dw64_ && L.out <= 128 && M <= 1024 && B <= 16384) ? TILE_64x64 : TILE_AUTO;
-    gemm_tile_for(L.out, L.dtile, &BM, &BN);
-    const long long tiles = cdiv(M, BM) * cdiv(L.out, BN);
-    const long long min_chunk = L.dtile == TILE_64x64 ? 256 : 128;
-    long long side = 0;
-    if (side_reduced(l + 1, fused, 0)) {
-      const Layer &N1 = layers_[l + 1];
-      side = cdiv(cdiv((long long)(N1.in + 1) * N1.out, 64), tiles) * tiles;
-    }
-    static const int legacy = env_int("LBF_SPLIT_LEGACY", 0);
-    long long splits = legacy ? std::max(1LL, std::min(cdiv(512, tiles), cdiv(B, min_chunk)))
-                              : split_factor(tiles, B, min_chunk, std::max(slots - side, slots / 2), M * L.out);
-    long long kc = cdiv(cdiv(B, splits), 32) * 32;
-    if (kc <= 0) kc = 32;
-    splits = std::max(1LL, cdiv(B, kc));
-    L.splits = int(splits);
-    L.k_chunk = int(kc);
-  }
   for (auto &L : layers_) {
-    const long long M = L.in + 1;
-    const long long splits = L.splits;
-    L.slab_off = slab;
-    if (splits > 1) slab += size_t(splits) * size_t(M) * L.out; // every layer keeps its own slabs until reduce_all
     // forward GEMM: with fewer row tiles than CUs (a data-parallel rank's shard), split K so the chip
     // fills; the partial slabs are summed in split order with the bias and activation afterwards
     int fBM, fBN;
@@ -163,15 +134,72 @@ void Mlp::plan(long long B) {
         fslab = std::max(fslab, size_t(fs) * size_t(B) * L.out);
       }
     }
+    // dW: 64x64 tiles over narrow outputs -> fewer, longer K splits (a third of the slab traffic)
+    // (only for short K: at long K the 128x128 tile's reuse wins over the slab savings)
+    L.dtile = (dw64_ && L.out <= 128 && L.in + 1 <= 1024 && B <= 16384) ? TILE_64x64 : TILE_AUTO;
+  }
+  // The last hidden layer's dW GEMM has in + 1 rows; when they pass a multiple of its tile height by
+  // at most 16 input columns + the bias row (784 + 1 = 6 x 128 + 17 at cfg 2), those rows go to the
+  // EPI_HEAD epilogue, which holds delta in registers, instead of a last row tile that would be
+  // mostly padding (a seventh of the dW GEMM's MFMA work at cfg 2).
+  fold_ = -1;
+  fold_c0_ = 0;
+  if (fold_on_ && gemm_head_on()) {
+    const Layer &L = layers_[size_t(nl - 2)];
+    int BM, BN;
+    gemm_tile_for(L.out, L.dtile, &BM, &BN);
+    const int c0 = L.in / BM * BM;
+    if (c0 > 0 && L.in - c0 <= 16 && L.in % 4 == 0 && L.out <= 128) {
+      fold_ = L.in - c0;
+      fold_c0_ = c0;
+    }
+  }
+  // dW tiles and split-K, last layer first: layer l's launch also carries the side blocks that finish
+  // layer l+1's slabs (side_reduced), and those take workgroup slots too
+  for (int l = nl - 1; l >= 0; --l) {
+    Layer &L = layers_[l];
+    int BM, BN;
+    const long long M = (fold_ >= 0 && l == nl - 2) ? fold_c0_ : L.in + 1;
+    gemm_tile_for(L.out, L.dtile, &BM, &BN);
+    const long long tiles = cdiv(M, BM) * cdiv(L.out, BN);
+    const long long min_chunk = L.dtile == TILE_64x64 ? 256 : 128;
+    long long side = 0;
+    if (side_reduced(l + 1, fused, 0)) {
+      const Layer &N1 = layers_[l + 1];
+      long long cols = (long long)(N1.in + 1) * N1.out;
+      if (fold_ >= 0 && l == nl - 2) cols += (long long)(fold_ + 1) * L.out;
+      side = cdiv(cdiv(cols, 256), tiles) * tiles; // gemm.hip SIDE_COLS per side block
+    }
+    static const int legacy = env_int("LBF_SPLIT_LEGACY", 0);
+    long long splits = legacy ? std::max(1LL, std::min(cdiv(512, tiles), cdiv(B, min_chunk)))
+                              : split_factor(tiles, B, min_chunk, std::max(slots - side, slots / 2), M * L.out);
+    long long kc = cdiv(cdiv(B, splits), 32) * 32;
+    if (kc <= 0) kc = 32;
+    splits = std::max(1LL, cdiv(B, kc));
+    L.splits = int(splits);
+    L.k_chunk = int(kc);
+  }
+  for (auto &L : layers_) {
+    L.slab_off = slab;
+    if (L.splits > 1) slab += size_t(L.splits) * size_t(L.in + 1) * L.out; // every layer keeps its own slabs
   }
   static const int show = env_int("LBF_SHOW_PLAN", 0);
-  if (show)
+  if (show) {
     for (int l = 0; l < nl; ++l)
       std::fprintf(stderr, "[lbf plan] B=%lld layer %d: dW tile %d splits %d k_chunk %d | fwd tile %d splits %d\n", B,
                    l, layers_[l].dtile, layers_[l].splits, layers_[l].k_chunk, layers_[l].ftile, layers_[l].fsplits);
+    std::fprintf(stderr, "[lbf plan] B=%lld fold %d from column %d\n", B, fold_, fold_c0_);
+  }
   slab_.ensure(slab);
   fslab_.ensure(std::max<size_t>(fslab, 1));
   planned_ = B;
+}
+
+bool Mlp::gemm_head_on() const {
+  const int nl = int(layers_.size());
+  if (!(use_head_ && use_gemm_head_ && nl >= 2)) return false;
+  const Layer &Lo = layers_[size_t(nl - 1)];
+  return head_supported(Lo.in, Lo.out) && layers_[size_t(nl - 2)].fsplits == 1 && Lo.in <= 128;
 }
 
 void Mlp::ensure(long long B) {
@@ -192,7 +220,7 @@ void Mlp::ensure(long long B) {
     const size_t hw =
         size_t(std::max(head_nwg(B, Lo.in), gemm_row_tiles(int(std::max(1LL, B)), layers_[nl - 2].ftile)));
     nloss = std::max(nloss, hw);
-    head_slab_.ensure(hw * size_t(Lo.in + 1) * Lo.out);
+    head_slab_.ensure(hw * (size_t(Lo.in + 1) * Lo.out + (fold_ >= 0 ? size_t(fold_ + 1) * Lo.in : 0)));
   }
   loss_part_.ensure(nloss);
   long long ncg = 0;
@@ -269,7 +297,9 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
   ensure(B);
   // the output layer inside the last hidden layer's forward GEMM (EPI_HEAD), when that GEMM is one
   // unsplit tile column: its activations then never reach HBM
-  const bool gemm_head = fused && use_gemm_head_ && layers_[nl - 2].fsplits == 1 && Lo.in <= 128;
+  const bool gemm_head = gemm_head_on();
+  const int fold = gemm_head ? fold_ : -1;
+  const long long nfold = fold >= 0 ? (long long)(fold + 1) * Lo.in : 0; // fold rows in the head slab
   forward(P, X, idx, B, fused ? (gemm_head ? nl - 2 : nl - 1) : nl);
   int nloss, lstart;
   if (gemm_head) {
@@ -286,6 +316,8 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     d.head_delta = D_[nl - 2].get();
     d.head_slab = head_slab_.get();
     d.head_sse = loss_part_.get();
+    d.head_fold = fold;
+    d.head_fold_c0 = fold_c0_;
     ProfScope ps(ctx_, PK_FWD, nl - 2);
     gemm(s, d);
     lstart = nl - 2;
@@ -328,19 +360,25 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     d.k_chunk = L.k_chunk;
     d.abort = ctx_->abort;
     d.tile = L.dtile;
+    const bool folded = fold >= 0 && l == nl - 2; // rows >= fold_c0_ come from the EPI_HEAD epilogue
+    if (folded) {
+      d.M = fold_c0_;
+      d.a_mvalid = fold_c0_;
+      d.a_ones = -1;
+    }
     if (l + 1 < nl && side_reduced(l + 1, fused, nloss)) {
       // finish layer l+1's [dW ; db] slabs (the fused head's, or many split-K slabs) in side blocks
-      // of this launch, while its GEMM runs
+      // of this launch, while its GEMM runs; the head's slab starts with this layer's folded rows
       const Layer &N1 = layers_[l + 1];
-      const long long nseg = (long long)(N1.in + 1) * N1.out;
       const bool head = fused && l + 1 == nl - 1;
+      const long long nseg = (long long)(N1.in + 1) * N1.out + (head ? nfold : 0);
       d.side_slab = head ? head_slab_.get() : slab_.get() + N1.slab_off;
       d.side_splits = head ? nloss : N1.splits;
       d.side_stride = nseg;
       d.side_count = nseg;
-      d.side_dst = G + N1.off;
+      d.side_dst = G + N1.off - (head ? nfold : 0);
     }
-    const long long seg = (long long)(L.in + 1) * L.out;
+    const long long seg = (long long)d.M * L.out;
     if (L.splits > 1) {
       d.C = slab_.get() + L.slab_off;
       d.slab_stride = seg;
@@ -394,6 +432,11 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     RedSeg &g = ra.seg[l];
     g.count = (long long)(L.in + 1) * L.out;
     g.goff = (long long)L.off;
+    if (fold >= 0 && l == nl - 2) g.count = (long long)fold_c0_ * L.out; // the rest is the head's segment
+    if (fold >= 0 && l == nl - 1) {
+      g.count += nfold;
+      g.goff -= nfold;
+    }
     g.stride = g.count;
     if (side_reduced(l, fused, nloss)) {
       // finished by the side blocks of the next dW launch: as written

@@ -130,6 +130,12 @@ private:
   bool use_gemm_head_ = true; // ... inside the forward GEMM's epilogue (LBF_NO_GEMM_HEAD=1 disables)
   int fwd_small_ = 1;         // 32x128 forward tiles for few row tiles (LBF_FWD_TILE32=0 disables)
   int dw64_ = 1;              // 64x64 dW tiles with fewer splits (LBF_DW_TILE64=0 disables)
+  bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1 disables)
+  // Planned fold: the last hidden layer's [dW ; db] rows fold_c0_ .. in (fold_ input columns and the
+  // bias row) are computed in the forward GEMM's EPI_HEAD epilogue instead of a mostly empty last
+  // row tile of its dW GEMM; fold_ = -1: none.
+  int fold_ = -1, fold_c0_ = 0;
+  bool gemm_head_on() const; // the output layer runs inside the last hidden layer's forward GEMM
   DevBuf<double> loss_part_, dots_part_, sse_, colpart_, trows_, tdots_;
   // R-pass workspace (hvp): R{Z}, R{A}, R{dZ} and delta per layer, two products, one segment
   std::vector<DevBuf<float>> RZ_, RA_, RD_, DL_;

@@ -23,12 +23,14 @@ def main():
         for _ in range(3):
             net.loss_grad(P, X, Y)
         torch.cuda.synchronize()
-        buf = (C.c_ulonglong * 40)()
+        buf = (C.c_ulonglong * 42)()
         L.lbf_dbg_ktrace_gemm.argtypes = [C.c_void_p, C.c_int]
-        assert L.lbf_dbg_ktrace_gemm(buf, 40) == 0
+        assert L.lbf_dbg_ktrace_gemm(buf, 42) == 0
         t0 = buf[0]
         its = [(buf[i] - t0) / 100.0 for i in range(1, 26)]
         print(f"N={N} k-iters end (us):", " ".join(f"{x:.2f}" for x in its))
+        print(f"N={N} main loop: {buf[41] - buf[40]} shader cycles in {(buf[25] - buf[0]) / 100.0:.2f} us "
+              f"-> {(buf[41] - buf[40]) / ((buf[25] - buf[0]) * 10.0):.3f} GHz")
         print(f"N={N} head epilogue end {(buf[32] - t0) / 100.0:.2f}  partials end {(buf[33] - t0) / 100.0:.2f}")
         print(f"N={N} epilogue: start {(buf[26]-t0)/100:.2f} w-staged {(buf[27]-t0)/100:.2f} "
               f"half0 staged {(buf[28]-t0)/100:.2f} done {(buf[29]-t0)/100:.2f} "
