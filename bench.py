@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--comm1", action="store_true",
                     help="at N=1, route evaluations through a 1-rank RCCL communicator (the DP code path)")
-    ap.add_argument("--cpu-iters", type=int, default=8)
+    ap.add_argument("--cpu-iters", type=int, default=64)  # ~20 s of the oracle at N = 60000 on 16 threads
     ap.add_argument("--cpu-samples", type=int, default=0,
                     help="rows of the CPU-baseline sample (0: all rows up to 60000, else 2000; scaled to N)")
     ap.add_argument("--data", choices=["mnist", "regression"], default="mnist",
