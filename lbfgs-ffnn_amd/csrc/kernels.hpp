@@ -316,8 +316,11 @@ struct TailArgs {
   double *dots = nullptr; // [nc]
   int tcg0[RA_MAXSEG] = {}; // first TAIL_COLS column group of each segment
   int nb = 0, nc = 0;       // nb: TAIL_COLS column groups over all segments (one block each)
+  // Non-null: the last tail_cols block to finish (arrival counter, zero between launches) runs
+  // tail_fin's body itself, and tail_fin() must not be launched.
+  unsigned *cols_done = nullptr;
 };
-void tail_reduce(hipStream_t s, const TailArgs &a); // tail_reduce + tail_cols launches
+void tail_reduce(hipStream_t s, const TailArgs &a); // tail_reduce + tail_cols (+ fin) launches
 void tail_fin(hipStream_t s, const TailArgs &a);    // one block
 int tail_vpw(int m);                                // vectors per wave of the Gram sweep (0: unsupported)
 

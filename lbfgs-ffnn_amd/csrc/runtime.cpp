@@ -502,11 +502,19 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     tdots_.ensure(size_t(ta.nc));
     ta.rows = trows_.get();
     ta.dots = tdots_.get();
-    {
-      ProfScope ps(ctx_, PK_GRAM, 1);
-      tail_reduce(s, ta);
+    static const int tail_split = env_int("LBF_TAIL_SPLIT", 0); // 1: tail_fin as its own launch
+    if (!tail_split) {
+      if (!cols_done_.get()) {
+        cols_done_.resize(1);
+        LBF_HIP(hipMemsetAsync(cols_done_.get(), 0, sizeof(unsigned), s));
+      }
+      ta.cols_done = cols_done_.get();
     }
     {
+      ProfScope ps(ctx_, PK_GRAM, 1);
+      tail_reduce(s, ta); // + tail_fin in the last tail_cols block (cols_done)
+    }
+    if (tail_split) {
       ProfScope ps(ctx_, PK_COEF, 1);
       tail_fin(s, ta);
     }

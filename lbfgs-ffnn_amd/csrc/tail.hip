@@ -215,8 +215,7 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
 
 // dots[c] = sum over rows in row order (per-thread strided rows, then a fixed tree); rows are stored
 // transposed ([nc][nb]), so each block reads one contiguous column.
-__global__ __launch_bounds__(256) void tail_cols_kernel(const TailArgs a) {
-  if (a.ra.abort && *a.ra.abort) return;
+__device__ __forceinline__ void tail_cols_body(const TailArgs &a) {
   __shared__ double ws[4];
   const int c = blockIdx.x, t = threadIdx.x;
   const int count0 = a.h.ist[IST_COUNT];
@@ -240,6 +239,11 @@ __global__ __launch_bounds__(256) void tail_cols_kernel(const TailArgs a) {
   if (t == 0) a.dots[c] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
 }
 
+__global__ __launch_bounds__(256) void tail_cols_kernel(const TailArgs a) {
+  if (a.ra.abort && *a.ra.abort) return;
+  tail_cols_body(a);
+}
+
 constexpr int TF_THREADS = 256;
 
 // One block. Every global value it needs (dot columns, SSE partials, status words, ring header, rho,
@@ -247,9 +251,8 @@ constexpr int TF_THREADS = 256;
 // Wave 0 (decision, then the recurrences) issues no global store until the coefficients: the status
 // block, the host record (system-scope stores to host-mapped memory, whose acknowledgement the
 // sequence word must wait for) and the history step's ring/Gram writes are made by waves 1..3.
-__global__ __launch_bounds__(TF_THREADS) void tail_fin_kernel(const TailArgs a) {
+__device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
   const RedAllArgs &ra = a.ra;
-  if (ra.abort && *ra.abort) return;
   extern __shared__ double dyn[]; // sy [2*m*m] (SY and its transpose) | yy [m*m] | SY, YY [S*S] | rho [S]
   __shared__ HistSmem sm;
   __shared__ double v[4];
@@ -370,12 +373,39 @@ __global__ __launch_bounds__(TF_THREADS) void tail_fin_kernel(const TailArgs a) 
   KT(44);
 }
 
+__global__ __launch_bounds__(TF_THREADS) void tail_fin_kernel(const TailArgs a) {
+  if (a.ra.abort && *a.ra.abort) return;
+  tail_fin_body(a);
+}
+
+// tail_cols, then (cols_done) the last block to finish runs the one-block fin: one launch fewer on
+// the iteration's critical path. Release: each block's dots store, fence, arrival; acquire: the last
+// arrival fences before reading the other blocks' dots (agent scope: the blocks span XCDs' L2s).
+__global__ __launch_bounds__(TF_THREADS) void tail_cols_fin_kernel(const TailArgs a) {
+  if (a.ra.abort && *a.ra.abort) return; // uniform for the launch: nobody arrives, the counter stays 0
+  tail_cols_body(a);
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    s_last = atomicAdd(a.cols_done, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (threadIdx.x == 0) *a.cols_done = 0u; // ready for the next launch (stream-ordered)
+  tail_fin_body(a);
+}
+
 } // namespace
 
 int tail_vpw(int m) {
   const int per_wave = (2 * m + 3) / 4;
   if (m > TAIL_MAXM) return 0;
   return per_wave <= 2 ? 2 : per_wave <= 4 ? 4 : per_wave <= 8 ? 8 : 16;
+}
+
+static size_t fin_shmem(const TailArgs &a) {
+  return (size_t(3) * a.h.m * a.h.m + 2 * size_t(a.h.slots) * a.h.slots + a.h.slots) * sizeof(double);
 }
 
 void tail_reduce(hipStream_t s, const TailArgs &a) {
@@ -388,13 +418,17 @@ void tail_reduce(hipStream_t s, const TailArgs &a) {
   default: throw Error(2, "tail_reduce: history size not supported by the fused tail");
   }
   LBF_KERNEL_CHECK();
-  hipLaunchKernelGGL(tail_cols_kernel, dim3(unsigned(a.nc)), dim3(256), 0, s, a);
+  if (a.cols_done) {
+    hipLaunchKernelGGL(tail_cols_fin_kernel, dim3(unsigned(a.nc)), dim3(TF_THREADS), fin_shmem(a), s, a);
+  } else {
+    hipLaunchKernelGGL(tail_cols_kernel, dim3(unsigned(a.nc)), dim3(256), 0, s, a);
+  }
   LBF_KERNEL_CHECK();
 }
 
 void tail_fin(hipStream_t s, const TailArgs &a) {
-  const size_t shmem = (size_t(3) * a.h.m * a.h.m + 2 * size_t(a.h.slots) * a.h.slots + a.h.slots) * sizeof(double);
-  hipLaunchKernelGGL(tail_fin_kernel, dim3(1), dim3(TF_THREADS), shmem, s, a);
+  if (a.cols_done) throw Error(2, "tail_fin: already run by the last tail_cols block");
+  hipLaunchKernelGGL(tail_fin_kernel, dim3(1), dim3(TF_THREADS), fin_shmem(a), s, a);
   LBF_KERNEL_CHECK();
 }
 
