@@ -56,6 +56,37 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpu():
+    """CPU model and core counts of this host (/proc/cpuinfo, the data lscpu prints)."""
+    model, cores = None, set()
+    try:
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model is None:
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+            elif not k and phys is not None:
+                cores.add((phys, core))
+                phys = core = None
+        if phys is not None:
+            cores.add((phys, core))
+    except OSError:
+        pass
+    return dict(model=model, physical_cores=len(cores) or None, logical_cpus=os.cpu_count(),
+                usable_cpus=len(os.sched_getaffinity(0)))
+
+
+def route_env():
+    """LBF_* variables that reroute kernels (tests and A/B builds use them); reported in the bench line so
+    a stray one cannot change the measured route without a trace."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("LBF_")}
+
+
 def cpu_baseline(dims, acts, N, m, iters, data, rows):
     """The oracle (fp64 C++/OpenMP restatement of the reference CPU path, literal call pattern incl. its
     redundant f/grad re-evaluations) timed on this host; bounded sample of the same workload: `rows` of
@@ -69,6 +100,7 @@ def cpu_baseline(dims, acts, N, m, iters, data, rows):
     ms = info["ms"]
     scale = rows / N
     return dict(value=round(iters / (ms / 1e3) * scale, 6), unit="iters/s", cores=O.num_threads(), kind="port",
+                host=host_cpu(),
                 sample=f"{iters} L-BFGS iterations (Wolfe, m={m}) of the {'-'.join(map(str, dims))} MLP on "
                        f"{rows} of the N={N} rows{f' (rate scaled by {rows}/{N})' if rows != N else ''}, fp64 "
                        f"oracle (oracle/oracle.hpp) with the reference's f/grad call pattern "
@@ -206,6 +238,7 @@ def main():
             "evals_per_iter": round(evals / max(iters_done, 1), 3),
             "roofline": roof,
             "kernel_ms_per_step": {k: round(v[0] / bd_steps, 4) for k, v in sorted(breakdown.items())},
+            "route_env": route_env(),
         }
         if world == 1 and not a.no_cpu_baseline:
             rows = a.cpu_samples or (N if N <= 60000 else 2000)

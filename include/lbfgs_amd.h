@@ -96,6 +96,11 @@ int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const 
  * Replaces, as an option, the finite-difference HVP of s_lbfgs.hpp:88-101. */
 int lbf_mlp_hvp(lbf_mlp *net, const float *d_params, const float *d_v, const float *d_X, const float *d_Y,
                 const int *d_idx, long long batch, double inv_scale, double l2, float *d_hv);
+/* finite_difference_hvp_batch (src/minimizer/s_lbfgs.hpp:88-101): y = (g(w + eps v) - g(w - eps v)) / (2 eps)
+ * of the batch loss (inv_scale, + l2 w), computed exactly as the S-LBFGS solver's curvature pair does
+ * (two fused batch evaluations; the fp32 difference times the once-rounded 1/(2 eps)). */
+int lbf_mlp_fd_hvp(lbf_mlp *net, const float *d_params, const float *d_v, const float *d_X, const float *d_Y,
+                   const int *d_idx, long long batch, double inv_scale, double l2, double eps, float *d_y);
 int lbf_two_loop(lbf_ctx *ctx, long long n, int k, const float *d_S, const float *d_Y, const double *h_rho,
                  const float *d_g, float *d_dir, int mode);
 

@@ -117,6 +117,8 @@ def lib():
         "lbf_idx_read_images": (C.c_int, [C.c_char_p, C.c_longlong, _vp, C.POINTER(C.c_longlong), _ip, _ip]),
         "lbf_idx_read_labels": (C.c_int, [C.c_char_p, C.c_longlong, C.c_int, _vp, C.POINTER(C.c_longlong)]),
         "lbf_mlp_hvp": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_longlong, C.c_double, C.c_double, _vp]),
+        "lbf_mlp_fd_hvp": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_longlong, C.c_double, C.c_double,
+                                     C.c_double, _vp]),
         "lbf_gd_default_params": (None, [C.POINTER(GdParams)]),
         "lbf_sgd_default_params": (None, [C.POINTER(SgdParams)]),
         "lbf_gd_solve": (C.c_int, [_vp, C.POINTER(GdParams), _vp, _vp, _vp, C.c_longlong, C.c_longlong,
@@ -139,7 +141,7 @@ EXPORTS = ("lbf_last_error lbf_version lbf_ctx_create lbf_ctx_destroy lbf_ctx_sy
            "lbf_nrm2 lbf_axpy lbf_scal lbf_lbfgs_default_params lbf_slbfgs_default_params lbf_lbfgs_solve "
            "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_prof_enable lbf_prof_select lbf_prof_sample lbf_prof_read lbf_synth_mnist "
            "lbf_sample_indices lbf_synth_regression lbf_gd_default_params lbf_sgd_default_params lbf_gd_solve "
-           "lbf_sgd_solve lbf_idx_read_images lbf_idx_read_labels lbf_mlp_hvp").split()
+           "lbf_sgd_solve lbf_idx_read_images lbf_idx_read_labels lbf_mlp_hvp lbf_mlp_fd_hvp").split()
 
 
 def check(rc: int, what: str) -> None:
@@ -148,11 +150,17 @@ def check(rc: int, what: str) -> None:
         raise LbfError(f"{what} failed (status {rc}): {msg}")
 
 
-def ptr(t: Optional[torch.Tensor]):
+def ptr(t: Optional[torch.Tensor], dtype: torch.dtype = torch.float32, numel: Optional[int] = None):
+    """Device pointer of a contiguous tensor of `dtype` (and exactly `numel` elements when given): the
+    kernels read raw memory, so an int64 index list or a float64 matrix would be silently misread."""
     if t is None:
         return None
     if not t.is_cuda:
         raise LbfError("expected a device (cuda/hip) tensor")
     if not t.is_contiguous():
         raise LbfError("expected a contiguous tensor")
+    if t.dtype != dtype:
+        raise LbfError(f"expected a {dtype} tensor, got {t.dtype}")
+    if numel is not None and t.numel() != numel:
+        raise LbfError(f"expected {numel} elements, got {t.numel()}")
     return C.c_void_p(t.data_ptr())

@@ -227,10 +227,26 @@ int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const 
 int lbf_mlp_hvp(lbf_mlp *net, const float *d_params, const float *d_v, const float *d_X, const float *d_Y,
                 const int *d_idx, long long batch, double inv_scale, double l2, float *d_hv) {
   return guard([&] {
-    LBF_REQUIRE(net && d_params && d_v && d_X && d_Y && d_hv && batch > 0, "bad argument");
+    LBF_REQUIRE(net && d_params && d_v && d_hv && batch >= 0 && (batch == 0 || (d_X && d_Y)), "bad argument");
     net->ctx->c.set_device();
     net->net->hvp(d_params, d_v, d_X, d_Y, d_idx, batch, inv_scale, l2, d_hv);
     LBF_HIP(hipStreamSynchronize(net->ctx->c.stream));
+  });
+}
+
+int lbf_mlp_fd_hvp(lbf_mlp *net, const float *d_params, const float *d_v, const float *d_X, const float *d_Y,
+                   const int *d_idx, long long batch, double inv_scale, double l2, double eps, float *d_y) {
+  return guard([&] {
+    LBF_REQUIRE(net && d_params && d_v && d_y && batch >= 0 && (batch == 0 || (d_X && d_Y)) && eps > 0.0,
+                "bad argument");
+    lbf_ctx *c = net->ctx;
+    c->c.set_device();
+    const size_t n = net->net->nparams(), ld = (n + 3) / 4 * 4, lg = (n + 2 + 3) / 4 * 4;
+    DevBuf<float> w(2 * ld), g(2 * lg);
+    fd_hvp_grads(net->net.get(), d_params, d_v, d_X, d_Y, d_idx, batch, inv_scale, l2, eps, w.get(), w.get() + ld,
+                 g.get(), g.get() + lg, c->scal.get());
+    diff_scale(c->c.stream, (long long)n, g.get(), g.get() + lg, float(1.0 / (2.0 * eps)), d_y);
+    LBF_HIP(hipStreamSynchronize(c->c.stream));
   });
 }
 

@@ -191,6 +191,7 @@ void epoch_loss_acc(hipStream_t s, const double *scal, long long rows, float *es
 void average_slots(hipStream_t s, long long n, const float *W, long long ld, const int *h_slots, int cnt, float *u);
 // out = a + c*b
 void lincomb(hipStream_t s, long long n, const float *a, double c, const float *b, float *out);
+void diff_scale(hipStream_t s, long long n, const float *a, const float *b, float scale, float *out);
 
 // ------------------------------------------------------------------------------------------------
 // Device-resident L-BFGS history ("vector-free" two-loop: Chen, Wang & Zhou, NIPS 2014).

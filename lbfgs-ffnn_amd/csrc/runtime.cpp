@@ -80,6 +80,7 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
   if (const char *e = std::getenv("LBF_FWD_TILE32")) fwd_small_ = e[0] != '0';
   if (const char *e = std::getenv("LBF_DW_TILE64")) dw64_ = e[0] != '0';
   if (const char *e = std::getenv("LBF_NO_FOLD")) fold_on_ = e[0] != '1';
+  tail_split_ = env_int("LBF_TAIL_SPLIT", 0) != 0; // 1: tail_fin as its own launch (A/B and tests)
 }
 
 // Split-K factor for `tiles` output tiles over a K of `K` rows: the GEMM tiles run two workgroups per
@@ -298,13 +299,16 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
   // the output layer inside the last hidden layer's forward GEMM (EPI_HEAD), when that GEMM is one
   // unsplit tile column: its activations then never reach HBM
   const bool gemm_head = gemm_head_on();
-  const int fold = gemm_head ? fold_ : -1;
+  // the fold reads the last hidden layer's input with 16-byte loads; an unaligned caller X (2-layer
+  // nets) takes the unfolded route instead
+  const float *head_in = nl >= 3 ? A_[nl - 3].get() : X;
+  const int fold = (gemm_head && (reinterpret_cast<uintptr_t>(head_in) & 15u) == 0) ? fold_ : -1;
   const long long nfold = fold >= 0 ? (long long)(fold + 1) * Lo.in : 0; // fold rows in the head slab
   forward(P, X, idx, B, fused ? (gemm_head ? nl - 2 : nl - 1) : nl);
   int nloss, lstart;
   if (gemm_head) {
     nloss = gemm_row_tiles(int(B), layers_[nl - 2].ftile);
-    GemmDesc d = fwd_desc(size_t(nl - 2), P, nl >= 3 ? A_[nl - 3].get() : X, idx, B);
+    GemmDesc d = fwd_desc(size_t(nl - 2), P, head_in, idx, B);
     d.epi = EPI_HEAD;
     d.C = nullptr;
     d.head_P = P + Lo.off;
@@ -502,8 +506,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     tdots_.ensure(size_t(ta.nc));
     ta.rows = trows_.get();
     ta.dots = tdots_.get();
-    static const int tail_split = env_int("LBF_TAIL_SPLIT", 0); // 1: tail_fin as its own launch
-    if (!tail_split) {
+    if (!tail_split_) {
       if (!cols_done_.get()) {
         cols_done_.resize(1);
         LBF_HIP(hipMemsetAsync(cols_done_.get(), 0, sizeof(unsigned), s));
@@ -514,7 +517,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
       ProfScope ps(ctx_, PK_GRAM, 1);
       tail_reduce(s, ta); // + tail_fin in the last tail_cols block (cols_done)
     }
-    if (tail_split) {
+    if (tail_split_) {
       ProfScope ps(ctx_, PK_COEF, 1);
       tail_fin(s, ta);
     }
@@ -555,9 +558,15 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
 // ------------------------------------------------------------------------------------------------
 void Mlp::hvp(const float *P, const float *V, const float *X, const float *Y, const int *idx, long long B,
               double inv_scale, double lambda, float *Hv) {
-  LBF_REQUIRE(P && V && X && Y && Hv && B > 0, "hvp: bad argument");
+  LBF_REQUIRE(P && V && Hv && B >= 0 && (B == 0 || (X && Y)), "hvp: bad argument");
   hipStream_t s = ctx_->stream;
   const int nl = int(layers_.size());
+  if (B == 0) { // a data-parallel rank with an empty share still joins the all-reduce
+    LBF_HIP(hipMemsetAsync(Hv, 0, nparams_ * sizeof(float), s));
+    if (ctx_->dp()) ctx_->allreduce(Hv, nparams_);
+    if (lambda != 0.0) lincomb(s, (long long)nparams_, Hv, lambda, V, Hv);
+    return;
+  }
   ensure(B);
   if (B > rcap_) {
     RZ_.clear();
@@ -570,7 +579,8 @@ void Mlp::hvp(const float *P, const float *V, const float *X, const float *Y, co
       RA_.emplace_back(size_t(B) * L.out);
       RD_.emplace_back(size_t(B) * L.out);
       DL_.emplace_back(act_has_d2(L.act) ? size_t(B) * L.out : size_t(1));
-      wmax = std::max(wmax, size_t(L.in));
+      // T1_ holds R{A} W_l (B x out) in the R-forward and (dZ W^T) (B x in) in the R-backward
+      wmax = std::max(wmax, size_t(std::max(L.in, L.out)));
       segmax = std::max(segmax, size_t(L.in + 1) * L.out);
     }
     T1_.resize(size_t(B) * wmax);

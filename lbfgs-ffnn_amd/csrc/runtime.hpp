@@ -131,6 +131,7 @@ private:
   int fwd_small_ = 1;         // 32x128 forward tiles for few row tiles (LBF_FWD_TILE32=0 disables)
   int dw64_ = 1;              // 64x64 dW tiles with fewer splits (LBF_DW_TILE64=0 disables)
   bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1 disables)
+  bool tail_split_ = false;   // tail_fin as a separate launch (LBF_TAIL_SPLIT=1)
   // Planned fold: the last hidden layer's [dW ; db] rows fold_c0_ .. in (fold_ input columns and the
   // bias row) are computed in the forward GEMM's EPI_HEAD epilogue instead of a mostly empty last
   // row tile of its dW GEMM; fold_ = -1: none.

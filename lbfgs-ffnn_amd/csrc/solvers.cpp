@@ -482,6 +482,17 @@ void LbfgsSolver::info(lbf_solve_info *out) const {
 // ================================================================================================
 // S-LBFGS
 // ================================================================================================
+void fd_hvp_grads(Mlp *net, const float *u, const float *s, const float *X, const float *Y, const int *idx,
+                  long long count, double inv_scale, double lambda, double eps, float *wp, float *wm, float *gp,
+                  float *gm, double *scal) {
+  hipStream_t st = net->ctx()->stream;
+  const long long n = (long long)net->nparams();
+  lincomb(st, n, u, eps, s, wp);
+  lincomb(st, n, u, -eps, s, wm);
+  net->loss_grad(wp, gp, X, Y, idx, count, inv_scale, lambda, nullptr, scal);
+  net->loss_grad(wm, gm, X, Y, idx, count, inv_scale, lambda, nullptr, scal);
+}
+
 SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_params, const float *X, const float *Y,
                            long long N)
     : net_(net), ctx_(net->ctx()), prm_(prm), user_params_(d_params), X_(X), Y_(Y), N_(N),
@@ -632,12 +643,8 @@ int SlbfgsSolver::run(lbf_record *rec) {
             LBF_HIP(hipMemsetAsync(gm_.get(), 0, size_t(n_) * sizeof(float), s));
             pa.yscale = 1.0;
           } else { // s_lbfgs.hpp:88-101: central difference of two batch gradients
-            lincomb(s, n_, u_.get(), eps, s_.get(), wp_.get());
-            lincomb(s, n_, u_.get(), -eps, s_.get(), wm_.get());
-            net_->loss_grad(wp_.get(), gp_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda,
-                            nullptr, hist_.scal());
-            net_->loss_grad(wm_.get(), gm_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda,
-                            nullptr, hist_.scal());
+            fd_hvp_grads(net_, u_.get(), s_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda, eps,
+                         wp_.get(), wm_.get(), gp_.get(), gm_.get(), hist_.scal());
             pa.yscale = 1.0 / (2.0 * eps);
           }
           pa.ya = gp_.get();

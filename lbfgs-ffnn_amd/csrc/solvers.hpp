@@ -171,6 +171,13 @@ int run_gd(Mlp *net, const lbf_gd_params &prm, float *d_params, const float *X, 
 int run_sgd(Mlp *net, const lbf_sgd_params &prm, float *d_params, const float *X, const float *Y, long long N,
             lbf_record *rec, lbf_solve_info *info);
 
+// finite_difference_hvp_batch (s_lbfgs.hpp:88-101) up to the last step: wp/wm = u +- eps s, gp/gm = the
+// batch gradients there (1/count scale, + lambda w). y = (gp - gm) / (2 eps) is formed by the caller (the
+// S-LBFGS pair sweep, or diff_scale) in fp32 with the factor rounded once.
+void fd_hvp_grads(Mlp *net, const float *u, const float *s, const float *X, const float *Y, const int *idx,
+                  long long count, double inv_scale, double lambda, double eps, float *wp, float *wm, float *gp,
+                  float *gm, double *scal);
+
 // libstdc++ partial Fisher-Yates (s_lbfgs.hpp:141-160); shared with the ABI helper.
 std::vector<size_t> sample_minibatch(size_t N, size_t b, std::mt19937 &rng);
 

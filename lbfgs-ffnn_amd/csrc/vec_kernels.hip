@@ -504,6 +504,18 @@ void lincomb(hipStream_t s, long long n, const float *a, double c, const float *
   LBF_KERNEL_CHECK();
 }
 
+// y = (a - b) * scale in fp32: the pair sweep's y of a finite-difference HVP (gram_kernel forms the
+// same product when it writes the ring slot)
+__global__ __launch_bounds__(256) void diff_scale_kernel(long long n, const float *a, const float *b, float scale,
+                                                         float *out) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) out[e] = (a[e] - b[e]) * scale;
+}
+void diff_scale(hipStream_t s, long long n, const float *a, const float *b, float scale, float *out) {
+  hipLaunchKernelGGL(diff_scale_kernel, dim3(unsigned(cdiv(n, 256))), dim3(256), 0, s, n, a, b, scale, out);
+  LBF_KERNEL_CHECK();
+}
+
 // S-LBFGS iterate averaging (s_lbfgs.hpp:236-243): u = (sum_i w_i) / cnt in logical order.
 struct SlotList {
   int cnt;

@@ -132,6 +132,13 @@ class Mlp:
         self.h = h
         self.nparams = int(lib().lbf_mlp_param_count(h))
 
+    def _check_data(self, X: torch.Tensor, Y: Optional[torch.Tensor]):
+        """X [rows][In], Y [rows][Out] (the reference's column-major In x N / Out x N)."""
+        if X is not None and (X.dim() != 2 or X.shape[1] != self.dims[0]):
+            raise LbfError(f"X must be [rows][{self.dims[0]}], got {tuple(X.shape)}")
+        if Y is not None and (Y.dim() != 2 or Y.shape[1] != self.dims[-1] or Y.shape[0] != X.shape[0]):
+            raise LbfError(f"Y must be [{X.shape[0]}][{self.dims[-1]}], got {tuple(Y.shape)}")
+
     def new_params(self) -> torch.Tensor:
         return torch.empty(self.nparams, dtype=torch.float32, device=f"cuda:{self.ctx.device}")
 
@@ -143,7 +150,9 @@ class Mlp:
 
     def forward(self, params: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
         out = torch.empty((X.shape[0], self.dims[-1]), dtype=torch.float32, device=X.device)
-        check(lib().lbf_mlp_forward(self.h, ptr(params), ptr(X), X.shape[0], ptr(out)), "lbf_mlp_forward")
+        self._check_data(X, None)
+        check(lib().lbf_mlp_forward(self.h, ptr(params, numel=self.nparams), ptr(X), X.shape[0], ptr(out)),
+              "lbf_mlp_forward")
         return out
 
     def loss_grad(self, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, idx: Optional[torch.Tensor] = None,
@@ -153,9 +162,11 @@ class Mlp:
         if inv_scale is None:
             inv_scale = 1.0 / max(B, 1)
         grad = self.new_params() if grad is None else grad
+        self._check_data(X, Y)
         loss = C.c_double()
-        check(lib().lbf_mlp_loss_grad(self.h, ptr(params), ptr(grad), ptr(X), ptr(Y), ptr(idx), B, inv_scale, l2,
-                                      C.byref(loss)), "lbf_mlp_loss_grad")
+        check(lib().lbf_mlp_loss_grad(self.h, ptr(params, numel=self.nparams), ptr(grad, numel=self.nparams), ptr(X),
+                                      ptr(Y), ptr(idx, torch.int32), B, inv_scale, l2, C.byref(loss)),
+              "lbf_mlp_loss_grad")
         return loss.value, grad
 
     def hvp(self, params: torch.Tensor, v: torch.Tensor, X: torch.Tensor, Y: torch.Tensor,
@@ -166,8 +177,24 @@ class Mlp:
         if inv_scale is None:
             inv_scale = 1.0 / max(B, 1)
         out = self.new_params() if out is None else out
-        check(lib().lbf_mlp_hvp(self.h, ptr(params), ptr(v), ptr(X), ptr(Y), ptr(idx), B, inv_scale, l2, ptr(out)),
-              "lbf_mlp_hvp")
+        self._check_data(X, Y)
+        n = self.nparams
+        check(lib().lbf_mlp_hvp(self.h, ptr(params, numel=n), ptr(v, numel=n), ptr(X), ptr(Y), ptr(idx, torch.int32),
+                                B, inv_scale, l2, ptr(out, numel=n)), "lbf_mlp_hvp")
+        return out
+
+    def fd_hvp(self, params: torch.Tensor, v: torch.Tensor, X: torch.Tensor, Y: torch.Tensor,
+               idx: Optional[torch.Tensor] = None, inv_scale: Optional[float] = None, l2: float = 0.0,
+               eps: float = 1e-4, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """finite_difference_hvp_batch (s_lbfgs.hpp:88-101), the S-LBFGS curvature pair's y."""
+        B = int(idx.numel()) if idx is not None else int(X.shape[0])
+        if inv_scale is None:
+            inv_scale = 1.0 / max(B, 1)
+        out = self.new_params() if out is None else out
+        self._check_data(X, Y)
+        n = self.nparams
+        check(lib().lbf_mlp_fd_hvp(self.h, ptr(params, numel=n), ptr(v, numel=n), ptr(X), ptr(Y),
+                                   ptr(idx, torch.int32), B, inv_scale, l2, eps, ptr(out, numel=n)), "lbf_mlp_fd_hvp")
         return out
 
     def __del__(self):

@@ -619,6 +619,23 @@ inline std::vector<size_t> sample_minibatch_indices(size_t N, size_t b, std::mt1
   return idx;
 }
 
+// finite_difference_hvp_batch (s_lbfgs.hpp:88-101): y = (g_S(w + eps v) - g_S(w - eps v)) / (2 eps) on the
+// Hessian batch S, eps = 1e-4 (:90).
+template <class T, class BG>
+Vec<T> finite_difference_hvp_batch(BG &&batch_g, const Vec<T> &w, const Vec<T> &v, const std::vector<size_t> &S,
+                                   double eps) {
+  const size_t n = w.size();
+  Vec<T> wp(n), wm(n), gp(n, T(0)), gm(n, T(0)), y(n);
+  for (size_t j = 0; j < n; ++j) {
+    wp[j] = w[j] + T(eps) * v[j];
+    wm[j] = w[j] - T(eps) * v[j];
+  }
+  batch_g(wp, S, gp);
+  batch_g(wm, S, gm);
+  for (size_t j = 0; j < n; ++j) y[j] = (gp[j] - gm[j]) / T(2.0 * eps);
+  return y;
+}
+
 struct SlbfgsParams {
   int max_iters = 1000; // epochs
   double tol = 1e-4;
@@ -673,15 +690,7 @@ Vec<T> slbfgs(Vec<T> weights, BG &&batch_g, BF &&batch_f, const SlbfgsParams &pr
           for (size_t j = 0; j < n; ++j) s[j] = u[j] - up[j];
           auto hb = sample_minibatch_indices(size_t(prm.N), size_t(prm.b_H), rng);
           if (sampled) sampled->push_back(hb);
-          const double eps = 1e-4;
-          Vec<T> wp(n), wm(n), gp(n, T(0)), gm(n, T(0)), y(n);
-          for (size_t j = 0; j < n; ++j) {
-            wp[j] = u[j] + T(eps) * s[j];
-            wm[j] = u[j] - T(eps) * s[j];
-          }
-          batch_g(wp, hb, gp);
-          batch_g(wm, hb, gm);
-          for (size_t j = 0; j < n; ++j) y[j] = (gp[j] - gm[j]) / T(2.0 * eps);
+          Vec<T> y = finite_difference_hvp_batch<T>(batch_g, u, s, hb, 1e-4);
           double ys = double(dot(y, s));
           if (std::abs(ys) > 1e-10) {
             s_list.push_back(s);

@@ -45,6 +45,8 @@ def lib():
         L.oracle_loss_grad.restype = C.c_double
         L.oracle_loss_grad.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_void_p, C.c_longlong, C.c_double,
                                        C.c_void_p]
+        L.oracle_fd_hvp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, C.c_void_p, C.c_longlong, C.c_double,
+                                    C.c_double, _dp]
         L.oracle_loss_grad_f32.restype = C.c_double
         L.oracle_loss_grad_f32.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, _dp]
         L.oracle_loss.restype = C.c_double
@@ -112,6 +114,17 @@ class Net:
             ip = None
         l = lib().oracle_loss_grad(self.nl, self.dims, self.acts, P, X, Y, ip, B, lam, g.ctypes.data)
         return l, g
+
+    def fd_hvp(self, P, V, X, Y, idx=None, lam: float = 0.0, eps: float = 1e-4):
+        """finite_difference_hvp_batch (s_lbfgs.hpp:88-101), fp64."""
+        idx = None if idx is None else np.ascontiguousarray(idx, np.int64)
+        B = len(idx) if idx is not None else X.shape[0]
+        y = np.empty(self.nparams, np.float64)
+        lib().oracle_fd_hvp(self.nl, self.dims, self.acts, np.ascontiguousarray(P, np.float64),
+                            np.ascontiguousarray(V, np.float64), np.ascontiguousarray(X, np.float64),
+                            np.ascontiguousarray(Y, np.float64), idx.ctypes.data if idx is not None else None, B, lam,
+                            eps, y)
+        return y
 
     def loss_grad_f32(self, P, X, Y):
         g = np.empty(self.nparams, np.float64)

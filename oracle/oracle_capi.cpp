@@ -199,6 +199,23 @@ double oracle_loss_grad(int nl, const int *dims, const int *acts, const double *
   return l;
 }
 
+// finite_difference_hvp_batch (s_lbfgs.hpp:88-101) in fp64 on the rows idx (B of them), batch_g of
+// UnifiedSLBFGS_CPU (1/B scale, + lambda w; unified_optimization.hpp:343-376).
+void oracle_fd_hvp(int nl, const int *dims, const int *acts, const double *P, const double *V, const double *X,
+                   const double *Y, const long long *idx, long long B, double lambda, double eps, double *y_out) {
+  Net net(dims, acts, nl);
+  MLPObjective<double> obj{&net, X, Y, B, {}, 0, 0};
+  auto bg = [&](const Vec<double> &w, const std::vector<size_t> &ind, Vec<double> &g) {
+    std::vector<int64_t> ii(ind.begin(), ind.end());
+    obj.loss_grad_batch(w, ii.data(), int64_t(ii.size()), lambda, g.data());
+  };
+  std::vector<size_t> S(static_cast<size_t>(B));
+  for (long long i = 0; i < B; ++i) S[size_t(i)] = idx ? size_t(idx[i]) : size_t(i);
+  Vec<double> w(P, P + net.nparams), v(V, V + net.nparams);
+  Vec<double> y = finite_difference_hvp_batch<double>(bg, w, v, S, eps);
+  std::copy(y.begin(), y.end(), y_out);
+}
+
 // fp32 instantiation of the same (inputs/outputs as double for ctypes convenience).
 double oracle_loss_grad_f32(int nl, const int *dims, const int *acts, const double *P, const double *X,
                             const double *Y, long long B, double *grad) {

@@ -17,6 +17,9 @@ NETS = [
     ([784, 128, 10], ["relu", "linear"]),
     ([64, 96, 33, 1], ["sigmoid", "tanh", "linear"]),
     ([40, 8], ["tanh"]),
+    # output wider than every input: the R-forward's R{A} W product is B x out
+    ([4, 6, 12], ["tanh", "linear"]),
+    ([10, 5, 20], ["relu", "sigmoid"]),
 ]
 ACTS = {"linear": lambda z: z, "relu": torch.relu, "tanh": torch.tanh, "sigmoid": torch.sigmoid}
 
@@ -111,3 +114,18 @@ def test_slbfgs_exact_hvp_option(ctx, pkg):
     assert np.array_equal(res[0]["accepted"], res[1]["accepted"])
     r = np.abs(res[1]["loss"] - res[0]["loss"]) / np.abs(res[0]["loss"])
     assert r.max() <= 5e-2, r
+
+
+def test_hvp_empty_batch(ctx, pkg):
+    """A data-parallel rank's share of the b_H batch may be empty: H v is then the L2 term lambda v (and
+    the rank still joins the all-reduce), not an error."""
+    dims, acts = [30, 24, 4], ["tanh", "linear"]
+    X = torch.zeros((1, 30), device="cuda")
+    Y = torch.zeros((1, 4), device="cuda")
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(5, "cpu")
+    v = torch.randn(net.nparams, device="cuda", generator=torch.Generator(device="cuda").manual_seed(2))
+    idx = torch.zeros(0, dtype=torch.int32, device="cuda")
+    hv = net.hvp(P, v, X, Y, idx=idx, inv_scale=1.0, l2=1e-4)
+    ref = (1e-4 * v.double()).float()
+    assert torch.allclose(hv, ref, rtol=1e-6, atol=0)
