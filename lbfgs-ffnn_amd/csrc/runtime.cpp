@@ -375,7 +375,10 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
       // of this launch, while its GEMM runs; the head's slab starts with this layer's folded rows
       const Layer &N1 = layers_[l + 1];
       const bool head = fused && l + 1 == nl - 1;
-      const long long nseg = (long long)(N1.in + 1) * N1.out + (head ? nfold : 0);
+      // the segment exactly as layer l+1's launch wrote its slabs: a folded layer's GEMM has fold_c0_
+      // rows (its remaining rows live in the head's segment)
+      const long long n1rows = (fold >= 0 && l + 1 == nl - 2) ? fold_c0_ : N1.in + 1;
+      const long long nseg = head ? (long long)(N1.in + 1) * N1.out + nfold : n1rows * N1.out;
       d.side_slab = head ? head_slab_.get() : slab_.get() + N1.slab_off;
       d.side_splits = head ? nloss : N1.splits;
       d.side_stride = nseg;

