@@ -161,8 +161,9 @@ typedef struct lbf_record {
 
 typedef struct lbf_solve_info {
   int iterations;
-  long long n_evals;  /* fused loss+grad evaluations executed */
+  long long n_evals;  /* fused loss+grad evaluations executed by this solve */
   double final_loss, final_grad_norm;
+  long long n_rows;   /* batch rows those evaluations covered on this rank (0 for callback objectives) */
 } lbf_solve_info;
 
 void lbf_lbfgs_default_params(lbf_lbfgs_params *p, int line_search);

@@ -54,7 +54,7 @@ class Record(C.Structure):
 
 class SolveInfo(C.Structure):
     _fields_ = [("iterations", C.c_int), ("n_evals", C.c_longlong), ("final_loss", C.c_double),
-                ("final_grad_norm", C.c_double)]
+                ("final_grad_norm", C.c_double), ("n_rows", C.c_longlong)]
 
 
 _lib = None

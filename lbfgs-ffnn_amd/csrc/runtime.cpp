@@ -525,6 +525,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
       tail_fin(s, ta);
     }
     ++evals_;
+    rows_ += B;
     return;
   }
   {
@@ -533,6 +534,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
   }
   if (ra.dots) {
     ++evals_;
+    rows_ += B;
     return;
   }
   const float *hilo = nullptr;
@@ -552,6 +554,7 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
     eval_tail(s, dots_part_.get(), nd, loss_part_.get(), nloss, hilo, inv_scale, lambda, scal, ctx_->abort);
   }
   ++evals_;
+    rows_ += B;
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -114,7 +114,11 @@ public:
   void hvp(const float *P, const float *V, const float *X, const float *Y, const int *idx, long long B,
            double inv_scale, double lambda, float *Hv);
   long long evals() const { return evals_; }
-  void discard_evals(long long k) { evals_ -= k; } // speculative evaluations that were aborted
+  long long rows() const { return rows_; } // batch rows evaluated (sum of B over loss_grad calls)
+  void discard_evals(long long k, long long B) { // speculative evaluations (B rows each) that were aborted
+    evals_ -= k;
+    rows_ -= k * B;
+  }
 
 private:
   void ensure(long long B);
@@ -143,7 +147,7 @@ private:
   std::vector<DevBuf<float>> RZ_, RA_, RD_, DL_;
   DevBuf<float> T1_, T2_, seg_;
   long long rcap_ = -1;
-  long long evals_ = 0;
+  long long evals_ = 0, rows_ = 0;
   void plan(long long B);
 };
 

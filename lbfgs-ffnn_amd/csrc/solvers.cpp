@@ -80,6 +80,8 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
     std::memset(spec_rec_, 0xff, kSpecRing * sizeof(SpecRecord));
   }
   LBF_HIP(hipMemcpyAsync(x_, d_params, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, ctx_->stream));
+  evals0_ = obj_->evals();
+  rows0_ = obj_->rows();
   // initial evaluation (lbfgs.hpp:44 / lbfgs.cuh:147)
   eval(x_, g_, nullptr);
   read_status();
@@ -474,7 +476,8 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
 void LbfgsSolver::info(lbf_solve_info *out) const {
   if (!out) return;
   out->iterations = iter_;
-  out->n_evals = obj_->evals();
+  out->n_evals = obj_->evals() - evals0_;
+  out->n_rows = obj_->rows() - rows0_;
   out->final_loss = loss_;
   out->final_grad_norm = std::sqrt(gg_);
 }
@@ -516,6 +519,8 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
   gm_.resize(ng);
   wh_.resize(nv * size_t(prm.L + 1));
   hs_.ensure(SC_N);
+  evals0_ = net->evals();
+  rows0_ = net->rows();
 }
 
 void SlbfgsSolver::eval_batch(const float *w, float *g, const int *d_idx, long long count, const float *pdir) {
@@ -684,7 +689,8 @@ int SlbfgsSolver::run(lbf_record *rec) {
 void SlbfgsSolver::info(lbf_solve_info *out) const {
   if (!out) return;
   out->iterations = iters_;
-  out->n_evals = net_->evals();
+  out->n_evals = net_->evals() - evals0_;
+  out->n_rows = net_->rows() - rows0_;
   out->final_loss = last_loss_;
   out->final_grad_norm = last_gnorm_;
 }
@@ -719,7 +725,7 @@ int run_gd(Mlp *net, const lbf_gd_params &prm, float *d_params, const float *X, 
   PinnedBuf<double> hs;
   hs.ensure(SC_N);
   LBF_HIP(hipMemsetAsync(v.get(), 0, size_t(n) * sizeof(float), s));
-  const long long evals0 = net->evals();
+  const long long evals0 = net->evals(), rows0 = net->rows();
   auto eval = [&]() {
     net->loss_grad(d_params, g.get(), X, Y, nullptr, n_local, 1.0 / double(n_global), 0.0, nullptr, scal.get());
     LBF_HIP(hipMemcpyAsync(hs.get(), scal.get(), SC_N * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -740,6 +746,7 @@ int run_gd(Mlp *net, const lbf_gd_params &prm, float *d_params, const float *X, 
   if (info) {
     info->iterations = done;
     info->n_evals = net->evals() - evals0;
+    info->n_rows = net->rows() - rows0;
     info->final_loss = hs[SC_LOSS];
     info->final_grad_norm = std::sqrt(hs[SC_TGG]);
   }
@@ -764,7 +771,7 @@ int run_sgd(Mlp *net, const lbf_sgd_params &prm, float *d_params, const float *X
   PinnedBuf<float> he;
   he.ensure(1);
   LBF_HIP(hipMemsetAsync(v.get(), 0, size_t(n) * sizeof(float), s));
-  const long long evals0 = net->evals();
+  const long long evals0 = net->evals(), rows0 = net->rows();
   auto full = [&]() {
     net->loss_grad(d_params, g.get(), X, Y, nullptr, N, 1.0 / double(N), 0.0, nullptr, scal.get());
     LBF_HIP(hipMemcpyAsync(hs.get(), scal.get(), SC_N * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -810,6 +817,7 @@ int run_sgd(Mlp *net, const lbf_sgd_params &prm, float *d_params, const float *X
   if (info) {
     info->iterations = done;
     info->n_evals = net->evals() - evals0;
+    info->n_rows = net->rows() - rows0;
     info->final_loss = rec ? hs[SC_LOSS] : double(prev);
     info->final_grad_norm = rec ? std::sqrt(hs[SC_TGG]) : 0.0;
   }

@@ -19,6 +19,7 @@ struct Objective {
   virtual long long n() const = 0;
   virtual void eval(const float *x, float *g, const float *pdir, double *scal) = 0;
   virtual long long evals() const = 0;
+  virtual long long rows() const { return 0; } // batch rows evaluated (0: not an MLP objective)
   // Asynchronous objectives can be enqueued ahead of the host's line-search decisions.
   virtual bool async() const { return false; }
   virtual void discard_evals(long long) {}
@@ -40,8 +41,9 @@ struct MlpObjective : Objective {
     net->loss_grad(x, g, X, Y, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal);
   }
   long long evals() const override { return net->evals(); }
+  long long rows() const override { return net->rows(); }
   bool async() const override { return true; }
-  void discard_evals(long long k) override { net->discard_evals(k); }
+  void discard_evals(long long k) override { net->discard_evals(k, nloc); }
   bool fused_tail() const override { return true; }
   void eval_fused(const float *x, float *g, const float *pdir, double *scal, const TailFuse &tf) override {
     net->loss_grad(x, g, X, Y, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal, &tf);
@@ -139,6 +141,7 @@ private:
   int iter_ = 0;
   bool pending_pair_ = false, pending_reset_ = false, converged_ = false;
   int rec_idx_ = 0;
+  long long evals0_ = 0, rows0_ = 0; // the objective's counters when this solve began
   std::chrono::steady_clock::time_point t0_;
 };
 
@@ -163,6 +166,7 @@ private:
   PinnedBuf<double> hs_;
   int iters_ = 0;
   double last_loss_ = 0, last_gnorm_ = 0;
+  long long evals0_ = 0, rows0_ = 0; // the net's counters when this solve began
 };
 
 // CudaGD / CudaSGD (src/cuda/gd.cuh:38-106, sgd.cuh:50-153) on the MLP; return the iterations done.
