@@ -277,7 +277,7 @@ def main():
         torch.distributed.broadcast_object_list(obj, src=0)
         dominant = obj[0]
     # timed region: only the dominant kernel carries an event pair
-    evals0 = run.info.n_evals
+    evals0, lonly0 = run.info.n_evals, run.info.n_loss_only
     it0 = run.hist.size
     ctx.prof_select(dominant)
     ctx.prof_sample(PROF_EVERY)
@@ -305,11 +305,13 @@ def main():
     ctx.prof_select(None)
     ctx.prof_sample(1)
     evals = run.info.n_evals - evals0
+    lonly = run.info.n_loss_only - lonly0
     iters_done = run.hist.size - it0
 
     if rank == 0:
         F = pkg.grad_flops_per_sample(dims) * N            # algorithmic flops per full-batch evaluation
-        gflops = evals * F / elapsed / 1e9
+        Ffwd = sum(2 * dims[l] * dims[l + 1] for l in range(len(dims) - 1)) * N  # loss-only trial (forward)
+        gflops = (evals * F + lonly * Ffwd) / elapsed / 1e9
         # dominant kernel: largest total time in the timed region (HIP events on the library stream)
         name, (ms, cnt) = dominant, prof[dominant]
         avg_s = ms / 1e3 / cnt
@@ -337,7 +339,7 @@ def main():
         ms_step = elapsed / max(iters_done, 1) * 1e3
         value = iters_done / elapsed
         out = {
-            "metric": METRIC,
+            "metric": METRIC if a.dims == "784,128,10" else METRIC.replace("784-128-10", a.dims.replace(",", "-")),
             "value": round(value, 3),
             "unit": "iters/s",
             "n_gpus": world,
@@ -355,6 +357,7 @@ def main():
                        "parallelism": f"dp{world}" + ("+rccl1" if a.comm1 and world == 1 else "")},
             "grad_eval_gflops": round(gflops, 1),
             "evals_per_iter": round(evals / max(iters_done, 1), 3),
+            "loss_only_trials_per_iter": round(lonly / max(iters_done, 1), 3),
             "roofline": roof,
             "kernel_ms_per_step": {k: round(v[0] / bd_steps, 4) for k, v in sorted(breakdown.items())},
             "route_env": route_env(),

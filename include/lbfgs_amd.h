@@ -96,6 +96,11 @@ int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const 
  * Replaces, as an option, the finite-difference HVP of s_lbfgs.hpp:88-101. */
 int lbf_mlp_hvp(lbf_mlp *net, const float *d_params, const float *d_v, const float *d_X, const float *d_Y,
                 const int *d_idx, long long batch, double inv_scale, double l2, float *d_hv);
+/* Loss only (CudaNetwork::forward_only, network.cuh:79-88, + the MSE of network.cuh:105; the CPU f closure of
+ * unified_optimization.hpp:101-108): forward pass and 0.5 * inv_scale * ||out - Y||^2 (summed over ranks with a
+ * communicator), bitwise the loss lbf_mlp_loss_grad reports for the same point. */
+int lbf_mlp_loss(lbf_mlp *net, const float *d_params, const float *d_X, const float *d_Y, const int *d_idx,
+                 long long batch, double inv_scale, double *h_loss);
 /* finite_difference_hvp_batch (src/minimizer/s_lbfgs.hpp:88-101): y = (g(w + eps v) - g(w - eps v)) / (2 eps)
  * of the batch loss (inv_scale, + l2 w), computed exactly as the S-LBFGS solver's curvature pair does
  * (two fused batch evaluations; the fp32 difference times the once-rounded 1/(2 eps)). */
@@ -164,6 +169,7 @@ typedef struct lbf_solve_info {
   long long n_evals;  /* fused loss+grad evaluations executed by this solve */
   double final_loss, final_grad_norm;
   long long n_rows;   /* batch rows those evaluations covered on this rank (0 for callback objectives) */
+  long long n_loss_only; /* line-search trials evaluated forward + loss only (rejected by Armijo) */
 } lbf_solve_info;
 
 void lbf_lbfgs_default_params(lbf_lbfgs_params *p, int line_search);

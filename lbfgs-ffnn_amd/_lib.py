@@ -54,7 +54,7 @@ class Record(C.Structure):
 
 class SolveInfo(C.Structure):
     _fields_ = [("iterations", C.c_int), ("n_evals", C.c_longlong), ("final_loss", C.c_double),
-                ("final_grad_norm", C.c_double), ("n_rows", C.c_longlong)]
+                ("final_grad_norm", C.c_double), ("n_rows", C.c_longlong), ("n_loss_only", C.c_longlong)]
 
 
 _lib = None
@@ -117,6 +117,7 @@ def lib():
         "lbf_idx_read_images": (C.c_int, [C.c_char_p, C.c_longlong, _vp, C.POINTER(C.c_longlong), _ip, _ip]),
         "lbf_idx_read_labels": (C.c_int, [C.c_char_p, C.c_longlong, C.c_int, _vp, C.POINTER(C.c_longlong)]),
         "lbf_mlp_hvp": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_longlong, C.c_double, C.c_double, _vp]),
+        "lbf_mlp_loss": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_longlong, C.c_double, _dp]),
         "lbf_mlp_fd_hvp": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_longlong, C.c_double, C.c_double,
                                      C.c_double, _vp]),
         "lbf_gd_default_params": (None, [C.POINTER(GdParams)]),
@@ -141,7 +142,7 @@ EXPORTS = ("lbf_last_error lbf_version lbf_ctx_create lbf_ctx_destroy lbf_ctx_sy
            "lbf_nrm2 lbf_axpy lbf_scal lbf_lbfgs_default_params lbf_slbfgs_default_params lbf_lbfgs_solve "
            "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_prof_enable lbf_prof_select lbf_prof_sample lbf_prof_read lbf_synth_mnist "
            "lbf_sample_indices lbf_synth_regression lbf_gd_default_params lbf_sgd_default_params lbf_gd_solve "
-           "lbf_sgd_solve lbf_idx_read_images lbf_idx_read_labels lbf_mlp_hvp lbf_mlp_fd_hvp").split()
+           "lbf_sgd_solve lbf_idx_read_images lbf_idx_read_labels lbf_mlp_hvp lbf_mlp_fd_hvp lbf_mlp_loss").split()
 
 
 def check(rc: int, what: str) -> None:

@@ -224,6 +224,20 @@ int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const 
   });
 }
 
+int lbf_mlp_loss(lbf_mlp *net, const float *d_params, const float *d_X, const float *d_Y, const int *d_idx,
+                 long long batch, double inv_scale, double *h_loss) {
+  return guard([&] {
+    LBF_REQUIRE(net && d_params && d_X && d_Y && h_loss && batch > 0, "bad argument");
+    lbf_ctx *c = net->ctx;
+    c->c.set_device();
+    net->net->loss_only(d_params, d_X, d_Y, d_idx, batch, inv_scale, c->scal.get());
+    double tmp[SC_N];
+    LBF_HIP(hipMemcpyAsync(tmp, c->scal.get(), SC_N * sizeof(double), hipMemcpyDeviceToHost, c->c.stream));
+    LBF_HIP(hipStreamSynchronize(c->c.stream));
+    *h_loss = tmp[SC_LOSS];
+  });
+}
+
 int lbf_mlp_hvp(lbf_mlp *net, const float *d_params, const float *d_v, const float *d_X, const float *d_Y,
                 const int *d_idx, long long batch, double inv_scale, double l2, float *d_hv) {
   return guard([&] {

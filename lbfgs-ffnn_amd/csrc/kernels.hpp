@@ -175,6 +175,10 @@ void eval_status(hipStream_t s, const double *sse_d, const float *sse_hilo, doub
 void eval_tail(hipStream_t s, const double *dots_part, int nd, const double *sse_part, int nsse, const float *hilo,
                double inv_scale, double lambda, double *scal, const int *abort = nullptr);
 // DP: reduce SSE partials into an fp32 (hi, lo) pair (all-reduced together with the gradient).
+// Loss-only status of a forward pass: SC_SSE / SC_LOSS from the SSE partials (reduce_fin's order) or,
+// data parallel, from the all-reduced (hi, lo) pair.
+void sse_loss(hipStream_t s, const double *sse_part, int nsse, const float *hilo, double inv_scale, double *scal,
+              const int *abort);
 void sse_pack(hipStream_t s, const double *sse_part, int nsse, float *hilo, const int *abort = nullptr);
 // hilo[0] = float(x), hilo[1] = float(x - hilo[0])
 void pack_hilo(hipStream_t s, const double *x, float *hilo);

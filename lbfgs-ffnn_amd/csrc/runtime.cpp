@@ -289,8 +289,11 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
   return in;
 }
 
-void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
-                    double inv_scale, double lambda, const float *pdir, double *scal, const TailFuse *tf) {
+// Forward phase of an evaluation: every forward GEMM, the output layer (fused head or loss_diff) with
+// its SSE partials, delta of the last layer the head covers, and the head's [dW ; db] partial slabs.
+// What the backward phase needs is kept in fs_.
+void Mlp::forward_phase(const float *P, const float *X, const float *Y, const int *idx, long long B,
+                        double inv_scale) {
   hipStream_t s = ctx_->stream;
   const int nl = int(layers_.size());
   const Layer &Lo = layers_[nl - 1];
@@ -303,7 +306,6 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
   // nets) takes the unfolded route instead
   const float *head_in = nl >= 3 ? A_[nl - 3].get() : X;
   const int fold = (gemm_head && (reinterpret_cast<uintptr_t>(head_in) & 15u) == 0) ? fold_ : -1;
-  const long long nfold = fold >= 0 ? (long long)(fold + 1) * Lo.in : 0; // fold rows in the head slab
   forward(P, X, idx, B, fused ? (gemm_head ? nl - 2 : nl - 1) : nl);
   int nloss, lstart;
   if (gemm_head) {
@@ -341,6 +343,56 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
               loss_part_.get());
     lstart = nl - 1;
   }
+  fs_.B = B;
+  fs_.fused = fused;
+  fs_.fold = fold;
+  fs_.nloss = nloss;
+  fs_.lstart = lstart;
+}
+
+// Loss only (forward phase + the SSE reduction; the reference's f(x) of a line-search trial,
+// full_batch_minimizer.hpp:136): SC_SSE / SC_LOSS of scal, bitwise the values a full evaluation of
+// the same point writes (same partials, same reduction order). The forward state stays for
+// grad_after_loss. lambda must be 0 (the L-BFGS objectives).
+void Mlp::loss_only(const float *P, const float *X, const float *Y, const int *idx, long long B, double inv_scale,
+                    double *scal) {
+  forward_phase(P, X, Y, idx, B, inv_scale);
+  hipStream_t s = ctx_->stream;
+  const float *hilo = nullptr;
+  if (ctx_->dp()) {
+    hilo_.ensure(4);
+    sse_pack(s, loss_part_.get(), fs_.nloss, hilo_.get(), ctx_->abort);
+    ProfScope ps(ctx_, PK_ALLREDUCE);
+    ctx_->allreduce(hilo_.get(), 2);
+    hilo = hilo_.get();
+  }
+  ProfScope ps(ctx_, PK_FINAL, 2);
+  sse_loss(s, loss_part_.get(), fs_.nloss, hilo, inv_scale, scal, ctx_->abort);
+  ++loss_only_;
+}
+
+void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
+                    double inv_scale, double lambda, const float *pdir, double *scal, const TailFuse *tf) {
+  forward_phase(P, X, Y, idx, B, inv_scale);
+  backward_phase(P, G, X, idx, B, inv_scale, lambda, pdir, scal, tf);
+}
+
+void Mlp::grad_after_loss(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
+                          double lambda, const float *pdir, double *scal) {
+  LBF_REQUIRE(fs_.B == B, "grad_after_loss: no forward phase of this batch");
+  backward_phase(P, G, X, idx, B, inv_scale, lambda, pdir, scal, nullptr);
+}
+
+// Backward phase: the dW / dX GEMMs below the head, every layer's slab reduction, the gradient
+// finish (+ all-reduce, dots, status block) or the fused optimizer tail.
+void Mlp::backward_phase(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
+                         double lambda, const float *pdir, double *scal, const TailFuse *tf) {
+  hipStream_t s = ctx_->stream;
+  const int nl = int(layers_.size());
+  const Layer &Lo = layers_[nl - 1];
+  const bool fused = fs_.fused;
+  const int fold = fs_.fold, nloss = fs_.nloss, lstart = fs_.lstart;
+  const long long nfold = fold >= 0 ? (long long)(fold + 1) * Lo.in : 0; // fold rows in the head slab
   for (int l = lstart; l >= 0; --l) {
     const Layer &L = layers_[l];
     const float *Ain = (l == 0) ? X : A_[l - 1].get();

@@ -109,6 +109,15 @@ public:
   //   scal : device fp64 status block (SC_LOSS, SC_TGG, SC_TGP, SC_WW, SC_SSE written).
   void loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
                  double inv_scale, double lambda, const float *pdir, double *scal, const TailFuse *tf = nullptr);
+  // The same evaluation in two steps (a line-search trial needs f first and the gradient only once
+  // Armijo holds, full_batch_minimizer.hpp:136-146): loss_only runs the forward phase and writes
+  // SC_SSE / SC_LOSS (lambda == 0); grad_after_loss then runs the backward phase of that same forward
+  // state. loss_only followed by grad_after_loss == loss_grad, bit for bit.
+  void loss_only(const float *P, const float *X, const float *Y, const int *idx, long long B, double inv_scale,
+                 double *scal);
+  void grad_after_loss(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
+                       double lambda, const float *pdir, double *scal);
+  long long loss_only_evals() const { return loss_only_; }
   // Exact Hessian-vector product Hv = H(P) V of the same batch loss (+ lambda V), Pearlmutter's
   // R-operator (hvp.hip); with a communicator the shards' products are all-reduced. Hv: nparams().
   void hvp(const float *P, const float *V, const float *X, const float *Y, const int *idx, long long B,
@@ -121,6 +130,16 @@ public:
   }
 
 private:
+  void forward_phase(const float *P, const float *X, const float *Y, const int *idx, long long B, double inv_scale);
+  void backward_phase(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
+                      double lambda, const float *pdir, double *scal, const TailFuse *tf);
+  struct FwdState {
+    long long B = -1;
+    bool fused = false;
+    int fold = -1, nloss = 0, lstart = 0;
+  } fs_;
+  DevBuf<float> hilo_;
+  long long loss_only_ = 0;
   void ensure(long long B);
   bool side_reduced(int l, bool fused, int nloss) const;
   GemmDesc fwd_desc(size_t l, const float *P, const float *in, const int *idx, long long B) const;

@@ -82,6 +82,7 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
   LBF_HIP(hipMemcpyAsync(x_, d_params, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, ctx_->stream));
   evals0_ = obj_->evals();
   rows0_ = obj_->rows();
+  lonly0_ = obj_->loss_only_evals();
   // initial evaluation (lbfgs.hpp:44 / lbfgs.cuh:147)
   eval(x_, g_, nullptr);
   read_status();
@@ -232,14 +233,20 @@ void LbfgsSolver::finish_wolfe(lbf_record *rec) {
     const double f_old = loss_, gfo = hs_[SC_GTP];
     double amin = 0.0, amax = inf;
     alpha = 1.0;
-    bool evaluated = true;
+    bool evaluated = true, have_grad = true;
+    const bool split = obj_->split_eval();
     for (int i = 0; i < prm_.max_line_iters; ++i) {
       if (!evaluated) {
         {
           ProfScope ps(ctx_, PK_AXPY);
           axpy_to(ctx_->stream, n_, x_, float(alpha), p_.get(), xt_);
         }
-        eval(xt_, gt_, p_.get());
+        if (split) { // f(x + alpha p) first; the gradient only once Armijo holds (:136-146)
+          obj_->eval_loss(xt_, hist_.scal());
+          have_grad = false;
+        } else {
+          eval(xt_, gt_, p_.get());
+        }
         read_status();
         evaluated = true;
       }
@@ -250,6 +257,11 @@ void LbfgsSolver::finish_wolfe(lbf_record *rec) {
         alpha = prm_.rho * (amin + amax);
         evaluated = false;
         continue;
+      }
+      if (!have_grad) { // backward phase of the forward pass just taken: bitwise the full evaluation
+        obj_->eval_grad_after_loss(xt_, gt_, p_.get(), hist_.scal());
+        read_status();
+        have_grad = true;
       }
       const double gnp = hs_[SC_TGP];
       if (gnp < prm_.c2 * gfo) {
@@ -263,6 +275,9 @@ void LbfgsSolver::finish_wolfe(lbf_record *rec) {
     if (!evaluated) { // exhausted: the returned alpha was never evaluated (lbfgs.hpp:67-70)
       axpy_to(ctx_->stream, n_, x_, float(alpha), p_.get(), xt_);
       eval(xt_, gt_, p_.get());
+      read_status();
+    } else if (!have_grad) { // exhausted on an Armijo failure: x_new's gradient is still needed
+      obj_->eval_grad_after_loss(xt_, gt_, p_.get(), hist_.scal());
       read_status();
     }
   }
@@ -295,10 +310,17 @@ void LbfgsSolver::finish_armijo(float alpha, lbf_record *rec) {
   bool ok = false;
   int trials = 0;
   float lnew = 0.f, a_eval = alpha;
+  const bool split = obj_->split_eval();
+  bool have_grad = true;
   for (int ls = 0; ls < prm_.max_line_iters; ++ls) {
-    if (ls > 0) {
+    if (ls > 0) { // loss only; the accepted (or last) trial's gradient afterwards (lbfgs.cuh:115-140)
       axpy_to(ctx_->stream, n_, x_, alpha, p_.get(), xt_);
-      eval(xt_, gt_, p_.get());
+      if (split) {
+        obj_->eval_loss(xt_, hist_.scal());
+        have_grad = false;
+      } else {
+        eval(xt_, gt_, p_.get());
+      }
       read_status();
     }
     ++trials;
@@ -318,6 +340,10 @@ void LbfgsSolver::finish_armijo(float alpha, lbf_record *rec) {
       }
     }
     if (fb) alpha *= rho;
+  }
+  if (!have_grad) {
+    obj_->eval_grad_after_loss(xt_, gt_, p_.get(), hist_.scal());
+    read_status();
   }
   accept_roles();
   pending_reset_ = !ok; // lbfgs.cuh:147
@@ -478,6 +504,7 @@ void LbfgsSolver::info(lbf_solve_info *out) const {
   out->iterations = iter_;
   out->n_evals = obj_->evals() - evals0_;
   out->n_rows = obj_->rows() - rows0_;
+  out->n_loss_only = obj_->loss_only_evals() - lonly0_;
   out->final_loss = loss_;
   out->final_grad_norm = std::sqrt(gg_);
 }

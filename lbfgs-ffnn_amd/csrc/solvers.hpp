@@ -23,6 +23,12 @@ struct Objective {
   // Asynchronous objectives can be enqueued ahead of the host's line-search decisions.
   virtual bool async() const { return false; }
   virtual void discard_evals(long long) {}
+  // Two-step evaluation of a line-search trial (split_eval()): the loss alone (SC_LOSS, SC_SSE), then the
+  // gradient and dots of that same point; together bitwise equal to eval().
+  virtual bool split_eval() const { return false; }
+  virtual void eval_loss(const float *, double *) {}
+  virtual void eval_grad_after_loss(const float *, float *, const float *, double *) {}
+  virtual long long loss_only_evals() const { return 0; }
   // Evaluation followed by the fused optimizer tail (tail.hip); only when fused_tail() is true.
   virtual bool fused_tail() const { return false; }
   virtual void eval_fused(const float *, float *, const float *, double *, const TailFuse &) {}
@@ -44,6 +50,14 @@ struct MlpObjective : Objective {
   long long rows() const override { return net->rows(); }
   bool async() const override { return true; }
   void discard_evals(long long k) override { net->discard_evals(k, nloc); }
+  bool split_eval() const override { return true; }
+  void eval_loss(const float *x, double *scal) override {
+    net->loss_only(x, X, Y, nullptr, nloc, 1.0 / double(nglob), scal);
+  }
+  void eval_grad_after_loss(const float *x, float *g, const float *pdir, double *scal) override {
+    net->grad_after_loss(x, g, X, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal);
+  }
+  long long loss_only_evals() const override { return net->loss_only_evals(); }
   bool fused_tail() const override { return true; }
   void eval_fused(const float *x, float *g, const float *pdir, double *scal, const TailFuse &tf) override {
     net->loss_grad(x, g, X, Y, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal, &tf);
@@ -141,7 +155,7 @@ private:
   int iter_ = 0;
   bool pending_pair_ = false, pending_reset_ = false, converged_ = false;
   int rec_idx_ = 0;
-  long long evals0_ = 0, rows0_ = 0; // the objective's counters when this solve began
+  long long evals0_ = 0, rows0_ = 0, lonly0_ = 0; // the objective's counters when this solve began
   std::chrono::steady_clock::time_point t0_;
 };
 

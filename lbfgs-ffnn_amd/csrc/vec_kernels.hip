@@ -340,6 +340,34 @@ __global__ __launch_bounds__(RF_THREADS) void reduce_fin_kernel(const RedAllArgs
   KT(35);
 }
 
+// Forward-only loss of a line-search trial: the SSE partials summed exactly as reduce_fin_kernel sums
+// them (same threads, same strided rows, same wave and cross-wave order), so the loss is bitwise the
+// one the full evaluation of the same point reports; data parallel: from the all-reduced (hi, lo).
+__global__ __launch_bounds__(RF_THREADS) void sse_loss_kernel(const double *sse_part, int nsse, const float *hilo,
+                                                              double inv_scale, double *scal, const int *abort) {
+  if (abort && *abort) return;
+  __shared__ double ws[RF_THREADS / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  double acc = 0.0;
+  if (!hilo)
+    for (int r = t; r < nsse; r += RF_THREADS) acc += sse_part[r];
+  const double w = wave_sum(acc);
+  if (lane == 0) ws[wave] = w;
+  __syncthreads();
+  if (t == 0) {
+    double x = 0.0;
+    for (int i = 0; i < RF_THREADS / 64; ++i) x += ws[i];
+    const double sse = hilo ? (double(hilo[0]) + double(hilo[1])) : x;
+    scal[SC_SSE] = sse;
+    scal[SC_LOSS] = 0.5 * sse * inv_scale;
+  }
+}
+void sse_loss(hipStream_t s, const double *sse_part, int nsse, const float *hilo, double inv_scale, double *scal,
+              const int *abort) {
+  hipLaunchKernelGGL(sse_loss_kernel, dim3(1), dim3(RF_THREADS), 0, s, sse_part, nsse, hilo, inv_scale, scal, abort);
+  LBF_KERNEL_CHECK();
+}
+
 void reduce_all(hipStream_t s, const RedAllArgs &a) {
   if (a.nwg <= 0) return;
   hipLaunchKernelGGL(reduce_all_kernel, dim3(unsigned(a.nwg)), dim3(256), 0, s, a);

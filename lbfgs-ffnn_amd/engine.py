@@ -169,6 +169,18 @@ class Mlp:
               "lbf_mlp_loss_grad")
         return loss.value, grad
 
+    def loss(self, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, idx: Optional[torch.Tensor] = None,
+             inv_scale: Optional[float] = None) -> float:
+        """Forward + MSE only (lbf_mlp_loss): the f of a line-search trial."""
+        B = int(idx.numel()) if idx is not None else int(X.shape[0])
+        if inv_scale is None:
+            inv_scale = 1.0 / max(B, 1)
+        self._check_data(X, Y)
+        out = C.c_double()
+        check(lib().lbf_mlp_loss(self.h, ptr(params, numel=self.nparams), ptr(X), ptr(Y), ptr(idx, torch.int32), B,
+                                 inv_scale, C.byref(out)), "lbf_mlp_loss")
+        return out.value
+
     def hvp(self, params: torch.Tensor, v: torch.Tensor, X: torch.Tensor, Y: torch.Tensor,
             idx: Optional[torch.Tensor] = None, inv_scale: Optional[float] = None, l2: float = 0.0,
             out: Optional[torch.Tensor] = None) -> torch.Tensor:

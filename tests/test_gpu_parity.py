@@ -334,3 +334,38 @@ def test_tail_fin_in_last_block_equals_separate_launch(ctx, pkg, monkeypatch, li
     b, bi, bP = _spec_run(pkg, ctx, monkeypatch, 3, line_search, 0.0, 30, m=10, tail_split=True)
     assert _same(a, b)
     assert ai == bi and np.array_equal(aP, bP)
+
+
+@pytest.mark.parametrize("dims,acts", NETS[:6])
+@pytest.mark.parametrize("N", [257, 20000])
+def test_loss_only_equals_fused_loss(ctx, pkg, O, dims, acts, N):
+    """lbf_mlp_loss (forward + MSE, a line-search trial's f) reports bitwise the loss of the full
+    evaluation of the same point (same SSE partials, same reduction order): the Wolfe / Armijo decisions
+    taken on it are the full evaluation's."""
+    X, Y = random_problem(dims, N, seed=7)
+    Xd, Yd = dev(X), dev(Y)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    lf = net.loss(P, Xd, Yd)
+    lg, _ = net.loss_grad(P, Xd, Yd)
+    assert lf == lg
+    if N <= 1000:
+        assert abs(lf - O.Net(dims, acts).loss(host(P), X, Y)) <= LOSS_RTOL * abs(lf)
+
+
+def test_armijo_rejections_run_forward_only(ctx, pkg, monkeypatch):
+    """Trials after a rejected first trial are forward + loss only until Armijo holds (the reference's
+    line_search evaluates f first and Gradient only then, full_batch_minimizer.hpp:136-146); the
+    trajectory is the one every other route takes (test_speculative_line_search_is_exact)."""
+    monkeypatch.setenv("LBF_SPEC_DEPTH", "3")
+    dims, acts = [784, 32, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(256)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(7, "cpu")
+    run = pkg.LbfgsRun(net, P, dev(Xh), dev(Yh), m=5, max_iters=40, tol=0.0)
+    run.iterate(40)
+    info = run.info
+    h = run.hist.as_dict()
+    run.close()
+    assert np.any(h["ls_trials"][1:] > 1)
+    assert info.n_loss_only > 0
