@@ -196,6 +196,14 @@ void Mlp::plan(long long B) {
   planned_ = B;
 }
 
+// dX GEMM tile: 128-row tiles unless they leave most CUs idle (a minibatch of a few hundred rows:
+// S-LBFGS's b = 256 gives 8 tiles of 128 x 128 for a 512-wide layer), then 32 x 128 (four times the
+// row tiles; the epilogue needs the full K, so no split-K here).
+int Mlp::dx_tile(long long B, int N) const {
+  if (N >= 128 && cdiv(B, 128) * cdiv((long long)N, 128) < ctx_->cus / 2) return TILE_32x128;
+  return TILE_AUTO;
+}
+
 bool Mlp::gemm_head_on() const {
   const int nl = int(layers_.size());
   if (!(use_head_ && use_gemm_head_ && nl >= 2)) return false;
@@ -468,6 +476,7 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       x.ldaux = L.in;
       x.aux_act = P0.act;
       x.abort = ctx_->abort;
+      x.tile = dx_tile(B, L.in);
       ProfScope ps(ctx_, PK_DX, l);
       gemm(s, x);
     }
@@ -719,6 +728,7 @@ void Mlp::hvp(const float *P, const float *V, const float *X, const float *Y, co
     x.ldaux = L.in;
     x.aux_act = aux_act;
     x.abort = ctx_->abort;
+    x.tile = dx_tile(B, L.in);
     gemm(s, x);
   };
   // ---- forward and the plain backward (dZ_l; delta_l where act'' != 0) ----

@@ -160,6 +160,7 @@ private:
   // row tile of its dW GEMM; fold_ = -1: none.
   int fold_ = -1, fold_c0_ = 0;
   bool gemm_head_on() const; // the output layer runs inside the last hidden layer's forward GEMM
+  int dx_tile(long long B, int N) const;
   DevBuf<double> loss_part_, dots_part_, sse_, colpart_, trows_, tdots_;
   DevBuf<unsigned> cols_done_; // tail_cols arrival counter (zero between launches)
   // R-pass workspace (hvp): R{Z}, R{A}, R{dZ} and delta per layer, two products, one segment
