@@ -47,6 +47,20 @@ void Profiler::resolve() {
   used = 0;
 }
 
+void Profiler::merge_into(Profiler &dst) {
+  resolve();
+  if (dst.ms.size() < ms.size()) {
+    dst.ms.resize(ms.size(), 0.0);
+    dst.cnt.resize(ms.size(), 0);
+  }
+  for (size_t i = 0; i < ms.size(); ++i) {
+    dst.ms[i] += ms[i];
+    dst.cnt[i] += cnt[i];
+  }
+  ms.assign(ms.size(), 0.0);
+  cnt.assign(cnt.size(), 0);
+}
+
 void Ctx::set_device() const { LBF_HIP(hipSetDevice(device)); }
 
 void Ctx::allreduce(float *buf, size_t count) {

@@ -33,6 +33,7 @@ struct Profiler {
   ~Profiler();
   size_t mark(hipStream_t s);
   void resolve();
+  void merge_into(Profiler &dst); // resolve this one and add its totals to dst's
 };
 
 struct Ctx {

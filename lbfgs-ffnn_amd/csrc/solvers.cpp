@@ -548,6 +548,46 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
   hs_.ensure(SC_N);
   evals0_ = net->evals();
   rows0_ = net->rows();
+  if (!ctx_->dp() && env_int("LBF_SLBFGS_TWIN", 1)) {
+    tctx_.reset(new Ctx());
+    tctx_->device = ctx_->device;
+    tctx_->cus = ctx_->cus;
+    LBF_HIP(hipStreamCreateWithFlags(&tctx_->stream, hipStreamNonBlocking));
+    tctx_->own_stream = true;
+    tctx_->prof.on = ctx_->prof.on; // the benchmark's section timing covers the twin's launches too
+    tctx_->prof.only = ctx_->prof.only;
+    tctx_->prof.every = ctx_->prof.every;
+    std::vector<int> dims, acts;
+    for (const Layer &L : net->layers()) {
+      dims.push_back(L.in);
+      acts.push_back(L.act);
+    }
+    dims.push_back(net->layers().back().out);
+    tnet_.reset(new Mlp(tctx_.get(), int(acts.size()), dims.data(), acts.data()));
+    tscal_.resize(SC_N);
+    LBF_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    LBF_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+  }
+}
+
+SlbfgsSolver::~SlbfgsSolver() {
+  if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+  if (ev_join_) (void)hipEventDestroy(ev_join_);
+}
+
+void SlbfgsSolver::eval_pair(const float *wa, float *ga, const float *wb, float *gb, const int *d_idx,
+                             long long count, double inv_scale) {
+  if (!tnet_) {
+    net_->loss_grad(wa, ga, X_, Y_, d_idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
+    net_->loss_grad(wb, gb, X_, Y_, d_idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
+    return;
+  }
+  LBF_HIP(hipEventRecord(ev_fork_, ctx_->stream)); // wa, wb, the index list and gb's last reader are done
+  LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
+  tnet_->loss_grad(wb, gb, X_, Y_, d_idx, count, inv_scale, prm_.lambda, nullptr, tscal_.get());
+  net_->loss_grad(wa, ga, X_, Y_, d_idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
+  LBF_HIP(hipEventRecord(ev_join_, tctx_->stream));
+  LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_join_, 0));
 }
 
 void SlbfgsSolver::eval_batch(const float *w, float *g, const int *d_idx, long long count, const float *pdir) {
@@ -641,10 +681,7 @@ int SlbfgsSolver::run(lbf_record *rec) {
     for (int t = 0; t < m_inner; ++t) {
       const long long b = mb[t].second;
       const long long o = mb[t].first + b * rk / nr, c = b * (rk + 1) / nr - b * rk / nr;
-      net_->loss_grad(wt_.get(), g1_.get(), X_, Y_, idx_.get() + o, c, 1.0 / double(b), prm_.lambda, nullptr,
-                      hist_.scal());
-      net_->loss_grad(w_.get(), g2_.get(), X_, Y_, idx_.get() + o, c, 1.0 / double(b), prm_.lambda, nullptr,
-                      hist_.scal());
+      eval_pair(wt_.get(), g1_.get(), w_.get(), g2_.get(), idx_.get() + o, c, 1.0 / double(b));
       GramArgs ga;
       ga.policy = POL_SLBFGS;
       ga.has_g = 1;
@@ -675,8 +712,9 @@ int SlbfgsSolver::run(lbf_record *rec) {
             LBF_HIP(hipMemsetAsync(gm_.get(), 0, size_t(n_) * sizeof(float), s));
             pa.yscale = 1.0;
           } else { // s_lbfgs.hpp:88-101: central difference of two batch gradients
-            fd_hvp_grads(net_, u_.get(), s_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda, eps,
-                         wp_.get(), wm_.get(), gp_.get(), gm_.get(), hist_.scal());
+            lincomb(s, n_, u_.get(), eps, s_.get(), wp_.get()); // fd_hvp_grads, the two evaluations paired
+            lincomb(s, n_, u_.get(), -eps, s_.get(), wm_.get());
+            eval_pair(wp_.get(), gp_.get(), wm_.get(), gm_.get(), idx_.get() + ho, hc, 1.0 / double(hbn));
             pa.yscale = 1.0 / (2.0 * eps);
           }
           pa.ya = gp_.get();
@@ -710,14 +748,18 @@ int SlbfgsSolver::run(lbf_record *rec) {
   }
   LBF_HIP(hipMemcpyAsync(user_params_, w_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
   LBF_HIP(hipStreamSynchronize(s));
+  if (tctx_) {
+    LBF_HIP(hipStreamSynchronize(tctx_->stream));
+    tctx_->prof.merge_into(ctx_->prof);
+  }
   return iters_;
 }
 
 void SlbfgsSolver::info(lbf_solve_info *out) const {
   if (!out) return;
   out->iterations = iters_;
-  out->n_evals = net_->evals() - evals0_;
-  out->n_rows = net_->rows() - rows0_;
+  out->n_evals = net_->evals() - evals0_ + (tnet_ ? tnet_->evals() : 0);
+  out->n_rows = net_->rows() - rows0_ + (tnet_ ? tnet_->rows() : 0);
   out->final_loss = last_loss_;
   out->final_grad_norm = last_gnorm_;
 }

@@ -163,11 +163,16 @@ class SlbfgsSolver {
 public:
   SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_params, const float *X, const float *Y,
                long long N);
+  ~SlbfgsSolver();
   int run(lbf_record *rec);
   void info(lbf_solve_info *out) const;
 
 private:
   void eval_batch(const float *w, float *g, const int *d_idx, long long count, const float *pdir);
+  // Two independent batch gradients of one step (minibatch at w_t and at the anchor w; the FD pair at
+  // u +- eps s): the second on the twin's stream when there is one, joined before the next launch.
+  void eval_pair(const float *wa, float *ga, const float *wb, float *gb, const int *d_idx, long long count,
+                 double inv_scale);
   Mlp *net_;
   Ctx *ctx_;
   lbf_slbfgs_params prm_;
@@ -181,6 +186,13 @@ private:
   int iters_ = 0;
   double last_loss_ = 0, last_gnorm_ = 0;
   long long evals0_ = 0, rows0_ = 0; // the net's counters when this solve began
+  // Twin evaluator (single rank): a second workspace of the same network on its own stream, so the
+  // two latency-bound minibatch evaluations of a step run concurrently (results unchanged: each is
+  // the same launch sequence on its own buffers). Data parallel: off (one communicator, one order).
+  std::unique_ptr<Ctx> tctx_;
+  std::unique_ptr<Mlp> tnet_;
+  DevBuf<double> tscal_;
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
 };
 
 // CudaGD / CudaSGD (src/cuda/gd.cuh:38-106, sgd.cuh:50-153) on the MLP; return the iterations done.
