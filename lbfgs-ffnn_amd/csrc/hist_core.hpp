@@ -214,7 +214,41 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
   };
   const bool yy_lds = k * k <= yy_cap;
   const bool sy_t = 2 * k * k <= sy_cap;
-  for (int e0 = t; e0 < k * k; e0 += nt * 4) { // independent loads in flight
+  // No room for SY, its transpose and YY (m = 100): SY with an odd row stride (k + 1, so its column
+  // reads are nearly conflict-free and need no transposed copy) and YY's lower triangle, both in the
+  // SY area (m = 100: 10100 + 5050 doubles)
+  const int kp = k + 1;
+  const bool big = !(k <= 64 && sy_t && yy_lds) && k * kp + (k * kp) / 2 <= sy_cap;
+  if (big) {
+    double *yt = sy + k * kp;
+    constexpr int B = 16; // loads in flight per thread: k * k = 10^4 entries in three round trips
+    for (int e0 = t; e0 < k * k; e0 += nt * B) {
+      double a16[B], b16[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) { // every stored entry loaded unconditionally (clamped): one round trip
+        const int e = min(e0 + nt * u, k * k - 1);
+        const int i = e / k, j = e - i * k;
+        const int pq = L[i] * S_ + L[j];
+        a16[u] = hc_ld<LDS>(SYsrc, pq);
+        b16[u] = hc_ld<LDS>(YYsrc, pq);
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int e = e0 + nt * u;
+        if (e < k * k) {
+          const int i = e / k, j = e - i * k, p_ = L[i], q_ = L[j];
+          double sv = a16[u], yv = b16[u];
+          if (a.has_pair && (p_ == w || q_ == w)) { // the pushed pair's row / column: fresh dots (LDS)
+            sv = SYv(p_, q_);
+            yv = YYv(p_, q_);
+          }
+          sy[i * kp + j] = sv;
+          if (j <= i) yt[(i * (i + 1)) / 2 + j] = yv;
+        }
+      }
+    }
+  }
+  for (int e0 = t; !big && e0 < k * k; e0 += nt * 4) { // independent loads in flight
     double a4[4], b4[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -275,8 +309,9 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
   const double gg = a.has_g ? self[5] : h.scal[SC_GG];
   double gamma = 1.0;
   if (k > 0) {
-    const double ys = sy[(k - 1) * k + (k - 1)];
-    const double yy = yy_lds ? yyl[(k - 1) * k + (k - 1)] : YYv(L[k - 1], L[k - 1]);
+    const double ys = big ? sy[(k - 1) * kp + (k - 1)] : sy[(k - 1) * k + (k - 1)];
+    const double yy = big ? sy[k * kp + ((k - 1) * k) / 2 + (k - 1)]
+                          : (yy_lds ? yyl[(k - 1) * k + (k - 1)] : YYv(L[k - 1], L[k - 1]));
     if (a.policy == POL_CPU) {
       gamma = ys / yy; // lbfgs.hpp:127-128, no guard
     } else if (a.policy == POL_CUDA) {
@@ -340,6 +375,81 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
           const double ci = lane_f64(al0, i) - lane_f64(cand, i);
           if (lane == i) c0 = ci;
           tv = (lane > i && lane < k) ? tv + ci * row[u] : tv;
+        }
+      }
+    }
+  } else if (big) {
+    // Two indices per lane (l0 = lane, l1 = lane + 64); the LDS operands of 8 steps are loaded ahead
+    // of them, so each step is VALU + v_readlane only (the k <= 64 fast path, widened).
+    const double *yt = sy + k * kp;
+    const int l0 = lane, l1 = lane + 64;
+    const bool in0 = l0 < k, in1 = l1 < k;
+    auto tri = [&](int a_, int b_) { return a_ >= b_ ? (a_ * (a_ + 1)) / 2 + b_ : (b_ * (b_ + 1)) / 2 + a_; };
+    const double rho0 = in0 ? rho_l[l0] : 0.0, rho1 = in1 ? rho_l[l1] : 0.0;
+    double r0 = in0 ? gS_l[l0] : 0.0, r1 = in1 ? gS_l[l1] : 0.0;
+    for (int i0 = k - 1; i0 >= 0; i0 -= 8) { // backward: alpha_i = rho_i (gS_i - sum_{j>i} alpha_j SY[i][j])
+      double c0v[8], c1v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 - u;
+        c0v[u] = (i >= 0 && l0 < i) ? sy[l0 * kp + i] : 0.0; // column i of SY: s_l . y_i
+        c1v[u] = (i >= 0 && l1 < i) ? sy[l1 * kp + i] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 - u;
+        if (i >= 0) { // wave-uniform
+          const double ai = (i < 64) ? lane_f64(rho0 * r0, i) : lane_f64(rho1 * r1, i - 64);
+          if (i < 64 && lane == i) al0 = ai;
+          if (i >= 64 && lane == i - 64) al1 = ai;
+          r0 = l0 < i ? r0 - ai * c0v[u] : r0;
+          r1 = l1 < i ? r1 - ai * c1v[u] : r1;
+        }
+      }
+    }
+    KT(60);
+    double acc0 = in0 ? gY_l[l0] : 0.0, acc1 = in1 ? gY_l[l1] : 0.0; // gY_l - sum_j alpha_j YY[l][j]
+    for (int j0 = 0; j0 < k; j0 += 8) {
+      double y0v[8], y1v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u;
+        y0v[u] = (j < k && in0) ? yt[tri(l0, j)] : 0.0;
+        y1v[u] = (j < k && in1) ? yt[tri(l1, j)] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u;
+        if (j < k) {
+          const double aj = (j < 64) ? lane_f64(al0, j) : lane_f64(al1, j - 64);
+          acc0 -= aj * y0v[u];
+          acc1 -= aj * y1v[u];
+        }
+      }
+    }
+    double t0 = gamma * acc0, t1 = gamma * acc1;
+    for (int i0 = 0; i0 < k; i0 += 8) { // forward: beta_i = rho_i t_i ; t_l += (alpha_i - beta_i) SY[i][l]
+      double w0v[8], w1v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u;
+        w0v[u] = (i < k && l0 > i && in0) ? sy[i * kp + l0] : 0.0;
+        w1v[u] = (i < k && l1 > i && in1) ? sy[i * kp + l1] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u;
+        if (i < k) {
+          double ci;
+          if (i < 64) {
+            ci = lane_f64(al0, i) - lane_f64(rho0 * t0, i);
+            if (lane == i) c0 = ci;
+          } else {
+            ci = lane_f64(al1, i - 64) - lane_f64(rho1 * t1, i - 64);
+            if (lane == i - 64) c1 = ci;
+          }
+          t0 = (l0 > i && in0) ? t0 + ci * w0v[u] : t0;
+          t1 = (l1 > i && in1) ? t1 + ci * w1v[u] : t1;
         }
       }
     }

@@ -298,6 +298,7 @@ struct CoefArgs {
   int fused = 0;  // hist_core<true>: SY, YY, rho prefetched into LDS, stores off wave 0 (set by hist_coef)
   double dsign = -1.0;
 };
+int hist_stage_rows(int m);
 void hist_coef(hipStream_t s, const CoefArgs &a);
 
 // Fused optimizer tail of a speculative L-BFGS iteration (tail.hip): the evaluation's gradient

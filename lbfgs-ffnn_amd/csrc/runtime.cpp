@@ -851,9 +851,12 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
   c.h.abort = ctx_->abort;
   c.partials = part_.get();
   c.nwg = gram_nwg(v_.n);
-  if (c.nwg > 2 * kGramFold) { // tall partial table (large n): fold it on many blocks first, so the
-    ProfScope pf(ctx_, PK_COEF); // single-workgroup history step reads kGramFold rows, not thousands
-    c.nwg = fold_rows(s, part_.get(), c.nwg, gram_ncols(v_.m), kGramFold, red_.get());
+  // tall partial table (large n, or a large m whose rows fill the step's staging area): fold it on many
+  // blocks first, so the single-workgroup history step reads one staging round of rows, not thousands
+  const int fold_to = std::min(kGramFold, hist_stage_rows(v_.m));
+  if (c.nwg > 2 * fold_to) {
+    ProfScope pf(ctx_, PK_COEF);
+    c.nwg = fold_rows(s, part_.get(), c.nwg, gram_ncols(v_.m), fold_to, red_.get());
     c.partials = red_.get();
   }
   c.has_pair = g.has_pair;

@@ -842,6 +842,23 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
   }
 }
 
+// Partial rows of the Gram table that one staging round of the history step holds (History::update
+// folds taller tables to this many rows first, so step A is one round trip).
+int hist_stage_rows(int m) {
+  const long long total = (160 * 1024 - HIST_STATIC_LDS) / 8, m2 = (long long)m * m;
+  const long long need_stage = 6LL * m + 6, S = m + 1, pre = 2 * S * S + S;
+  const bool fused = S * S <= 256LL * HIST_PRE_UNROLL && 2 * m2 + HIST_STAGE_DOUBLES + pre <= total;
+  const long long avail = total - (fused ? pre : 0);
+  const long long big = (long long)m * (m + 1) + ((long long)m * (m + 1)) / 2;
+  long long sy_cap;
+  if (2 * m2 + HIST_STAGE_DOUBLES <= avail || big + 4 * need_stage > avail)
+    sy_cap = std::min(2 * m2, avail - need_stage);
+  else
+    sy_cap = big;
+  const long long stage = std::min<long long>(HIST_STAGE_DOUBLES, avail - sy_cap);
+  return int(std::max(1LL, stage / need_stage));
+}
+
 void hist_coef(hipStream_t s, const CoefArgs &a) {
   LBF_REQUIRE(a.h.m <= COEF_MAXK, "history size m must be <= 128");
   static bool attr_set = false;
@@ -861,7 +878,13 @@ void hist_coef(hipStream_t s, const CoefArgs &a) {
   c.fused = (fused_on && a.want_dir == 1 && S * S <= 256LL * HIST_PRE_UNROLL &&
              2 * m2 + HIST_STAGE_DOUBLES + pre <= total) ? 1 : 0;
   const long long avail = total - (c.fused ? pre : 0);
-  c.sy_cap = int(std::min(2 * m2, avail - need_stage)); // SY, and its transpose when it fits
+  // SY and its transpose when they fit beside a full staging area; else (m = 100) hist_core's compact
+  // layout (SY with stride m + 1, YY's lower triangle) so that step A keeps a staging area of many rows
+  const long long big = (long long)a.h.m * (a.h.m + 1) + ((long long)a.h.m * (a.h.m + 1)) / 2;
+  if (2 * m2 + HIST_STAGE_DOUBLES <= avail || big + 4 * need_stage > avail)
+    c.sy_cap = int(std::min(2 * m2, avail - need_stage)); // SY, and its transpose when it fits
+  else
+    c.sy_cap = int(big);
   LBF_REQUIRE(c.sy_cap >= m2, "hist_step: LDS too small for the SY block");
   c.stage = int(std::min<long long>(HIST_STAGE_DOUBLES, avail - c.sy_cap));
   const size_t shmem = (size_t(c.sy_cap) + size_t(c.stage) + (c.fused ? size_t(pre) : 0)) * sizeof(double);

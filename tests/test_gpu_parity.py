@@ -120,10 +120,11 @@ def make_history(n, k, seed=0):
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
-@pytest.mark.parametrize("k", [0, 1, 5, 10, 50, 128])
+@pytest.mark.parametrize("k", [0, 1, 5, 10, 30, 50, 70, 100, 128])
 @pytest.mark.parametrize("n", [1000, 100003])
 def test_two_loop_matches_oracle(ctx, O, mode, k, n):
-    """k = 128 is the largest history (YY no longer fits the LDS staging: global reads)."""
+    """k = 30 / 70 / 100 (m = k): SY with an odd row stride and YY's lower triangle in LDS, two indices
+    per lane (the m = 100 history step); k = 128 is the largest history (global YY reads)."""
     S, Yv, rho, g = make_history(n, k, seed=k + n)
     ref = O.two_loop(mode, S if k else np.zeros((0, n)), Yv if k else np.zeros((0, n)), rho, g)
     out = ctx.two_loop(dev(S) if k else None, dev(Yv) if k else None, rho, dev(g), mode=mode)
