@@ -195,6 +195,8 @@ void epoch_loss_acc(hipStream_t s, const double *scal, long long rows, float *es
 void average_slots(hipStream_t s, long long n, const float *W, long long ld, const int *h_slots, int cnt, float *u);
 // out = a + c*b
 void lincomb(hipStream_t s, long long n, const float *a, double c, const float *b, float *out);
+void gather_rows(hipStream_t s, const float *src, long long ld, const int *idx, long long count, int cols,
+                 float *dst);
 void diff_scale(hipStream_t s, long long n, const float *a, const float *b, float scale, float *out);
 
 // ------------------------------------------------------------------------------------------------

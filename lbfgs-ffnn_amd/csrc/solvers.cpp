@@ -575,17 +575,22 @@ SlbfgsSolver::~SlbfgsSolver() {
   if (ev_join_) (void)hipEventDestroy(ev_join_);
 }
 
-void SlbfgsSolver::eval_pair(const float *wa, float *ga, const float *wb, float *gb, const int *d_idx,
+void SlbfgsSolver::eval_pair(const float *wa, float *ga, const float *wb, float *gb, long long off,
                              long long count, double inv_scale) {
+  // the step's rows were gathered for the whole epoch (contiguous slices, same values in the same order
+  // as the gathering GEMMs would read), which also lets the dW GEMM of layer 0 take the LDS-DMA path
+  const int In = net_->layers().front().in, Out = net_->layers().back().out;
+  const float *X = xg_.get() + off * In, *Y = yg_.get() + off * Out;
+  const int *idx = nullptr;
   if (!tnet_) {
-    net_->loss_grad(wa, ga, X_, Y_, d_idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
-    net_->loss_grad(wb, gb, X_, Y_, d_idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
+    net_->loss_grad(wa, ga, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
+    net_->loss_grad(wb, gb, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
     return;
   }
-  LBF_HIP(hipEventRecord(ev_fork_, ctx_->stream)); // wa, wb, the index list and gb's last reader are done
+  LBF_HIP(hipEventRecord(ev_fork_, ctx_->stream)); // wa, wb, the gathered rows and gb's last reader are done
   LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
-  tnet_->loss_grad(wb, gb, X_, Y_, d_idx, count, inv_scale, prm_.lambda, nullptr, tscal_.get());
-  net_->loss_grad(wa, ga, X_, Y_, d_idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
+  tnet_->loss_grad(wb, gb, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, tscal_.get());
+  net_->loss_grad(wa, ga, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
   LBF_HIP(hipEventRecord(ev_join_, tctx_->stream));
   LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_join_, 0));
 }
@@ -657,6 +662,12 @@ int SlbfgsSolver::run(lbf_record *rec) {
     idx_.ensure(std::max<size_t>(1, flat.size()));
     if (!flat.empty())
       LBF_HIP(hipMemcpyAsync(idx_.get(), flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    // every sampled row of the epoch gathered once, in sampling order: step t's minibatch (and its
+    // Hessian batch) is then a contiguous slice (batch_g's column gather, unified_optimization.hpp:361-364)
+    xg_.ensure(std::max<size_t>(1, flat.size()) * size_t(In));
+    yg_.ensure(std::max<size_t>(1, flat.size()) * size_t(Out));
+    gather_rows(s, X_, In, idx_.get(), (long long)flat.size(), int(In), xg_.get());
+    gather_rows(s, Y_, Out, idx_.get(), (long long)flat.size(), int(Out), yg_.get());
     LBF_HIP(hipStreamSynchronize(s)); // flat is a pageable temporary
     // --- epoch -----------------------------------------------------------------------------------
     LBF_HIP(hipMemcpyAsync(wt_.get(), w_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -681,7 +692,7 @@ int SlbfgsSolver::run(lbf_record *rec) {
     for (int t = 0; t < m_inner; ++t) {
       const long long b = mb[t].second;
       const long long o = mb[t].first + b * rk / nr, c = b * (rk + 1) / nr - b * rk / nr;
-      eval_pair(wt_.get(), g1_.get(), w_.get(), g2_.get(), idx_.get() + o, c, 1.0 / double(b));
+      eval_pair(wt_.get(), g1_.get(), w_.get(), g2_.get(), o, c, 1.0 / double(b));
       GramArgs ga;
       ga.policy = POL_SLBFGS;
       ga.has_g = 1;
@@ -714,7 +725,7 @@ int SlbfgsSolver::run(lbf_record *rec) {
           } else { // s_lbfgs.hpp:88-101: central difference of two batch gradients
             lincomb(s, n_, u_.get(), eps, s_.get(), wp_.get()); // fd_hvp_grads, the two evaluations paired
             lincomb(s, n_, u_.get(), -eps, s_.get(), wm_.get());
-            eval_pair(wp_.get(), gp_.get(), wm_.get(), gm_.get(), idx_.get() + ho, hc, 1.0 / double(hbn));
+            eval_pair(wp_.get(), gp_.get(), wm_.get(), gm_.get(), ho, hc, 1.0 / double(hbn));
             pa.yscale = 1.0 / (2.0 * eps);
           }
           pa.ya = gp_.get();

@@ -171,8 +171,8 @@ private:
   void eval_batch(const float *w, float *g, const int *d_idx, long long count, const float *pdir);
   // Two independent batch gradients of one step (minibatch at w_t and at the anchor w; the FD pair at
   // u +- eps s): the second on the twin's stream when there is one, joined before the next launch.
-  void eval_pair(const float *wa, float *ga, const float *wb, float *gb, const int *d_idx, long long count,
-                 double inv_scale);
+  void eval_pair(const float *wa, float *ga, const float *wb, float *gb, long long off, long long count,
+                 double inv_scale); // rows off .. off+count-1 of the epoch's gathered block
   Mlp *net_;
   Ctx *ctx_;
   lbf_slbfgs_params prm_;
@@ -192,6 +192,7 @@ private:
   std::unique_ptr<Ctx> tctx_;
   std::unique_ptr<Mlp> tnet_;
   DevBuf<double> tscal_;
+  DevBuf<float> xg_, yg_; // the epoch's sampled rows, gathered once (all minibatches and Hessian batches)
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
 };
 

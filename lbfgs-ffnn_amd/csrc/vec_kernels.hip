@@ -532,6 +532,31 @@ void lincomb(hipStream_t s, long long n, const float *a, double c, const float *
   LBF_KERNEL_CHECK();
 }
 
+// Minibatch rows gathered into a contiguous block (S-LBFGS: both evaluations of an inner step read the
+// same rows; batch_g's column gather, unified_optimization.hpp:361-364). 16-B lanes when cols % 4 == 0.
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float *src, long long ld, const int *idx,
+                                                          long long count, int cols, float *dst) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((cols & 3) == 0 && (ld & 3) == 0) {
+    const int c4 = cols >> 2;
+    if (q >= count * c4) return;
+    const long long r = q / c4, c = (q - r * c4) * 4;
+    *reinterpret_cast<f32x4 *>(dst + r * cols + c) = *reinterpret_cast<const f32x4 *>(src + (long long)idx[r] * ld + c);
+  } else {
+    if (q >= count * cols) return;
+    const long long r = q / cols, c = q - r * cols;
+    dst[r * cols + c] = src[(long long)idx[r] * ld + c];
+  }
+}
+void gather_rows(hipStream_t s, const float *src, long long ld, const int *idx, long long count, int cols,
+                 float *dst) {
+  if (count <= 0) return;
+  const long long per = (cols & 3) == 0 && (ld & 3) == 0 ? cols / 4 : cols;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(unsigned(cdiv(count * per, 256))), dim3(256), 0, s, src, ld, idx, count,
+                     cols, dst);
+  LBF_KERNEL_CHECK();
+}
+
 // y = (a - b) * scale in fp32: the pair sweep's y of a finite-difference HVP (gram_kernel forms the
 // same product when it writes the ring slot)
 __global__ __launch_bounds__(256) void diff_scale_kernel(long long n, const float *a, const float *b, float scale,
