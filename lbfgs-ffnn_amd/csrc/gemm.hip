@@ -606,8 +606,11 @@ struct GldsPiece {
   int kq;                  // k offset of this lane's chunk / row inside a k-tile
 };
 
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS>
-__global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
+// KW = 2 (small tiles that run one workgroup per CU, e.g. 32 x 128 for a rank's shard): eight waves, two
+// per SIMD; k-group q computes steps [8q, 8q+8) of every 32-deep tile from the same LDS stage, group 0
+// alone issues the LDS-DMA pieces, and the groups' accumulators are summed through LDS in group order.
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1>
+__global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(const GemmK g) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32;
   constexpr int ASZ = BM * BK, STG = (BM + BN) * BK;
   constexpr int PA = BM / 8, P = (BM + BN) / 32; // A pieces per k-tile, pieces per wave per k-tile
@@ -623,7 +626,8 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
     return;
   }
   const int zsplit = int(blockIdx.z) - g.side_planes;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
+  const int kgrp = KW > 1 ? __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 8)) : 0;
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 31, lh = lane >> 5;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
@@ -638,7 +642,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 
-  // ---- this wave's pieces: j = wave + 4 i; j < PA -> A, else B ----
+  // ---- this wave's pieces: j = wave + 4 i; j < PA -> A, else B (k-group 0 only) ----
   const unsigned long long zero_u = reinterpret_cast<unsigned long long>(lbf_glds_const);
   GldsPiece pc[P];
 #pragma unroll
@@ -678,6 +682,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
     pc[i] = q;
   }
   auto issue = [&](int t) {
+    if (KW > 1 && kgrp != 0) return; // wave-uniform
     float *stage = lds + (t % NS) * STG;
     const int kt = kb + t * BK;
 #pragma unroll
@@ -691,6 +696,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
   auto compute = [&](int buf) {
     const float *As = lds + buf * STG;
     const float *Bs = As + ASZ;
+    constexpr int QW = 4 / KW; // 16-B quads of the k-contiguous fragments this k-group consumes
     float af[TM][AKC ? 16 : 1], bf[TN][BKC ? 16 : 1];
     if constexpr (AKC) {
 #pragma unroll
@@ -698,10 +704,11 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
         const int row = wm * TM * 32 + tm * 32 + li;
         const int sw = (row >> 1) & 7;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int qq = 0; qq < QW; ++qq) {
+          const int q = kgrp * QW + qq;
           const f32x4 v = *reinterpret_cast<const f32x4 *>(As + row * BK + 4 * ((lh * 4 + q) ^ sw));
 #pragma unroll
-          for (int e = 0; e < 4; ++e) af[tm][q * 4 + e] = v[e];
+          for (int e = 0; e < 4; ++e) af[tm][qq * 4 + e] = v[e];
         }
       }
     }
@@ -711,24 +718,26 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
         const int row = wn * TN * 32 + tn * 32 + li;
         const int sw = (row >> 1) & 7;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int qq = 0; qq < QW; ++qq) {
+          const int q = kgrp * QW + qq;
           const f32x4 v = *reinterpret_cast<const f32x4 *>(Bs + row * BK + 4 * ((lh * 4 + q) ^ sw));
 #pragma unroll
-          for (int e = 0; e < 4; ++e) bf[tn][q * 4 + e] = v[e];
+          for (int e = 0; e < 4; ++e) bf[tn][qq * 4 + e] = v[e];
         }
       }
     }
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int ss = 0; ss < 16 / KW; ++ss) {
+      const int s = kgrp * (16 / KW) + ss; // this k-group's steps (uniform)
       float av[TM], bv[TN];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
-        if constexpr (AKC) av[tm] = af[tm][s];
+        if constexpr (AKC) av[tm] = af[tm][ss];
         else av[tm] = As[(lh * 16 + s) * BM + ((wm * TM * 32 + tm * 32 + li) ^ (lh << 5))];
       }
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
-        if constexpr (BKC) bv[tn] = bf[tn][s];
+        if constexpr (BKC) bv[tn] = bf[tn][ss];
         else bv[tn] = Bs[(lh * 16 + s) * BN + ((wn * TN * 32 + tn * 32 + li) ^ (lh << 5))];
       }
 #pragma unroll
@@ -742,7 +751,7 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
   if (EPI == EPI_HEAD) KT(0);
   if (EPI == EPI_HEAD) KTC(40);
   if (EPI == EPI_HEAD) KTB(0);
-  headc::EpiPrefetch<BN, BM, 256> hpre;
+  headc::EpiPrefetch<BN, BM, 256 * KW> hpre;
   if constexpr (EPI == EPI_HEAD) {
     hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
     if (g.head_fold > 0) hpre.load_fold(g.A, g.lda, g.a_idx, g.head_fold_c0, g.head_fold, m0, g.M);
@@ -762,7 +771,31 @@ __global__ __launch_bounds__(256, 2) void gemm_glds_kernel(const GemmK g) {
   if (EPI == EPI_HEAD) KT(25);
   if (EPI == EPI_HEAD) KTC(41);
   __syncthreads(); // the LDS is the epilogue's now
-  gemm_epilogue<WM, WN, TM, TN, EPI, 1>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, 0);
+  if constexpr (KW > 1) { // group sums through LDS, in group order (group 0 keeps the result)
+    float *red = lds;
+    static_assert(TM * TN * 16 * 256 <= LDS_F, "k-group reduction buffer");
+    for (int q = 1; q < KW; ++q) {
+      if (kgrp == q) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[((a * TN + b) * 16 + r) * 256 + (threadIdx.x & 255)] = acc[a][b][r];
+      }
+      __syncthreads();
+      if (kgrp == 0) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] += red[((a * TN + b) * 16 + r) * 256 + threadIdx.x];
+      }
+      __syncthreads();
+    }
+  }
+  gemm_epilogue<WM, WN, TM, TN, EPI, KW>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, kgrp);
 }
 
 namespace {
@@ -823,8 +856,9 @@ void launch(hipStream_t s, const GemmDesc &d) {
   static const bool glds_on = env_int("LBF_GEMM_GLDS", 1) != 0;
   if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
     if (fast && glds_on && (AKC || !d.a_idx)) {
-      if (d.a_idx) hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, NS>), grid, dim3(256), 0, s, k);
-      else hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, NS>), grid, dim3(256), 0, s, k);
+      const dim3 gb(256 * KW);
+      if (d.a_idx) hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, NS, KW>), grid, gb, 0, s, k);
+      else hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, KW>), grid, gb, 0, s, k);
       return;
     }
   }
@@ -841,7 +875,8 @@ void launch(hipStream_t s, const GemmDesc &d) {
 template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const GemmDesc &d) {
   static const int pf_big = env_int("LBF_GEMM_PF", 2), pf_small = env_int("LBF_GEMM_PF_SMALL", 2);
   // LDS-DMA stages: as many tile buffers as fit two workgroups per CU (80 KB each)
-  if (d.tile == TILE_32x128) { // 32 x 128 (20 KB per stage)
+  if (d.tile == TILE_32x128) { // 32 x 128 (20 KB per stage), one 8-wave workgroup (two k-groups) per CU
+    // (six stages measured no faster: profiles/r02/small_tile_variants.txt)
     if (pf_small >= 2) launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 2, 4>(s, d);
     else launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 1, 4>(s, d);
   } else if (d.tile == TILE_64x64) { // 64 x 64 (16 KB per stage)

@@ -1,0 +1,17 @@
+# Round 2, run I: quick check of a GEMM change: parity subset, shard / cfg-2 / cfg-4 benches, shard trace.
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r02i
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fold.py tests/test_gpu_dp.py -m gpu -q -x -rf --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+rc=$?
+echo "tests rc=$rc"
+tail -2 $O/gpu_tests.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 120 python -u bench.py --samples 7500 --no-cpu-baseline > $O/bench_7500.json 2> $O/bench_7500.err && \
+timeout -k 10 120 python -u bench.py --no-cpu-baseline > $O/bench_cfg2.json 2> $O/bench_cfg2.err && \
+timeout -k 10 300 python -u bench.py --solver slbfgs --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_cfg4.json 2> $O/bench_cfg4.err && \
+cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt7500 -o run -- python3 $R/bench.py --samples 7500 --no-cpu-baseline --steps 50 > $O/kt7500.json 2> $O/kt7500.err && \
+cd $R && python3 profiles/kstats_live.py $O/kt7500/run_kernel_trace.csv --out $O/kt7500_live.csv > /dev/null
+echo "rc=$?"
