@@ -134,6 +134,7 @@ struct RedAllArgs {
   const float *w = nullptr, *p = nullptr;
   double lambda = 0.0;
   int dots = 0;
+  int l2 = 0;                   // apply g += lambda w here (single rank; data parallel: after the all-reduce)
   double *partials = nullptr;   // [ncg][3] dot partials
   double *colpart = nullptr;    // [ncg][RA_MAXPART][64] split-range partials
   int ncg = 0;

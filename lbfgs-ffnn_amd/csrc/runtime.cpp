@@ -501,7 +501,10 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
   ra.w = P;
   ra.p = pdir;
   ra.lambda = lambda;
-  ra.dots = ctx_->dp() ? 0 : 1;
+  // scal == nullptr (S-LBFGS minibatch / Hessian-batch gradients, whose status nobody reads): the
+  // gradient only, no dot partials and no finishing launch
+  ra.dots = (ctx_->dp() || !scal) ? 0 : 1;
+  ra.l2 = ctx_->dp() ? 0 : 1;
   ra.partials = dots_part_.get();
   ra.colpart = colpart_.get();
   ra.sse_part = loss_part_.get();
@@ -607,7 +610,7 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     ProfScope ps(ctx_, PK_SLAB, 0);
     reduce_all(s, ra);
   }
-  if (ra.dots) {
+  if (!ctx_->dp()) {
     ++evals_;
     rows_ += B;
     return;
@@ -626,7 +629,7 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     ProfScope ps(ctx_, PK_FINAL, 1);
     const int nd = dots_partials_wg(nparams_);
     finalize_grad_dots(s, nparams_, G, P, lambda, pdir, dots_part_.get(), ctx_->abort);
-    eval_tail(s, dots_part_.get(), nd, loss_part_.get(), nloss, hilo, inv_scale, lambda, scal, ctx_->abort);
+    if (scal) eval_tail(s, dots_part_.get(), nd, loss_part_.get(), nloss, hilo, inv_scale, lambda, scal, ctx_->abort);
   }
   ++evals_;
     rows_ += B;

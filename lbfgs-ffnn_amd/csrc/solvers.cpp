@@ -582,15 +582,16 @@ void SlbfgsSolver::eval_pair(const float *wa, float *ga, const float *wb, float 
   const int In = net_->layers().front().in, Out = net_->layers().back().out;
   const float *X = xg_.get() + off * In, *Y = yg_.get() + off * Out;
   const int *idx = nullptr;
+  // gradients only: nobody reads a minibatch evaluation's loss or dots (scal = nullptr skips them)
   if (!tnet_) {
-    net_->loss_grad(wa, ga, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
-    net_->loss_grad(wb, gb, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
+    net_->loss_grad(wa, ga, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, nullptr);
+    net_->loss_grad(wb, gb, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, nullptr);
     return;
   }
   LBF_HIP(hipEventRecord(ev_fork_, ctx_->stream)); // wa, wb, the gathered rows and gb's last reader are done
   LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
-  tnet_->loss_grad(wb, gb, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, tscal_.get());
-  net_->loss_grad(wa, ga, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, hist_.scal());
+  tnet_->loss_grad(wb, gb, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, nullptr);
+  net_->loss_grad(wa, ga, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, nullptr);
   LBF_HIP(hipEventRecord(ev_join_, tctx_->stream));
   LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_join_, 0));
 }

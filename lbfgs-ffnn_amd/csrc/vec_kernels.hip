@@ -215,14 +215,14 @@ __device__ __forceinline__ void ra_column(const RedAllArgs &a, const RedSeg &S, 
   if (live) {
     const long long e = S.goff + col;
     float gv = S.splits > 0 ? float(colsum) : a.G[e];
+    const float wv = (a.w && (a.dots || (a.l2 && a.lambda != 0.0))) ? a.w[e] : 0.0f;
+    if (a.l2 && a.lambda != 0.0) gv = gv + float(a.lambda) * wv; // finalize_kernel's update
     if (a.dots) {
-      const float wv = a.w ? a.w[e] : 0.0f;
-      if (a.lambda != 0.0) gv = gv + float(a.lambda) * wv; // finalize_kernel's update
       d0 = double(gv) * double(gv);
       if (a.p) d1 = double(gv) * double(a.p[e]);
       d2 = double(wv) * double(wv);
     }
-    if (S.splits > 0 || (a.dots && a.lambda != 0.0)) a.G[e] = gv;
+    if (S.splits > 0 || (a.l2 && a.lambda != 0.0)) a.G[e] = gv;
   }
   if (a.dots) {
     d0 = wave_sum(d0);
