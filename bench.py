@@ -9,7 +9,9 @@ iteration (two-loop direction + line-search trials, each a fused loss+grad evalu
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 With N > 1 the 60000 samples are split into contiguous shards (strong scaling; one RCCL all-reduce
-of [grad | loss] per evaluation). Rank 0 prints ONE JSON line.
+of [grad | loss] per evaluation, on the library's own communicator). The torch.distributed group is
+gloo: it carries only the RCCL unique id, the barriers and the max over the ranks' clocks. Rank 0
+prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -170,7 +172,7 @@ def main_slbfgs(a, pkg, ctx, world, rank):
     hist, info = pkg.slbfgs_solve(net, P, X, Y, max_epochs=a.steps, **kw)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    cnt = torch.tensor([elapsed, float(info.n_evals), float(info.n_rows)], device="cuda", dtype=torch.float64)
+    cnt = torch.tensor([elapsed, float(info.n_evals), float(info.n_rows)], dtype=torch.float64)
     if world > 1:
         mx = cnt[:1].clone()
         torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
@@ -230,8 +232,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # control plane only (RCCL unique id, barriers, max of the ranks' clocks): gloo over loopback, so
+        # each process holds exactly one RCCL communicator, the library's own (lbf_comm_init), and the
+        # data path's all-reduce is the only collective on xGMI
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        torch.distributed.init_process_group("gloo")
     pkg = __graft_entry__.load_package()
     dims = [int(x) for x in a.dims.split(",")]
     acts = a.acts.split(",")
@@ -298,7 +303,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     barrier()

@@ -609,7 +609,17 @@ struct GldsPiece {
 // KW = 2 (small tiles that run one workgroup per CU, e.g. 32 x 128 for a rank's shard): eight waves, two
 // per SIMD; k-group q computes steps [8q, 8q+8) of every 32-deep tile from the same LDS stage, group 0
 // alone issues the LDS-DMA pieces, and the groups' accumulators are summed through LDS in group order.
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1>
+// PIPE (small tiles, one or two waves per SIMD): the fragments of k-tile i+1 are read from LDS while the
+// MFMAs of k-tile i run (two register sets), and tile i's buffer is refilled as soon as its fragments are
+// in registers, one k-tile further ahead than the plain loop; the single wave per SIMD then no longer
+// stalls on LDS latency at every k-tile.
+// LDR (KW = 2): the two groups specialise instead of splitting the k-steps: group 1 (waves 4-7) only
+// issues the LDS-DMA pieces, group 0 (waves 0-3) only reads fragments and runs every MFMA. A wave that
+// issues DMA stalls for ~100+ cycles per 1-KiB piece, so loader and MFMA work on the same wave serialise
+// (a 32 x 128 tile then moves ~22 GB/s per CU and its MFMAs idle half the time); on separate waves of the
+// same SIMD they overlap.
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1,
+          bool PIPE = false, bool LDR = false>
 __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(const GemmK g) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32;
   constexpr int ASZ = BM * BK, STG = (BM + BN) * BK;
@@ -682,7 +692,7 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
     pc[i] = q;
   }
   auto issue = [&](int t) {
-    if (KW > 1 && kgrp != 0) return; // wave-uniform
+    if (KW > 1 && kgrp != (LDR ? 1 : 0)) return; // wave-uniform
     float *stage = lds + (t % NS) * STG;
     const int kt = kb + t * BK;
 #pragma unroll
@@ -693,59 +703,66 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
              stage + (j < PA ? j * 256 : ASZ + (j - PA) * 256));
     }
   };
-  auto compute = [&](int buf) {
+  // fragments of one k-tile for this k-group: 16 / KW k-steps of every (tm, tn) operand
+  static_assert(!LDR || (KW == 2 && !PIPE), "LDR: two groups, plain loop");
+  constexpr int KWC = LDR ? 1 : KW; // k-groups sharing the MFMA work
+  const int kq0 = LDR ? 0 : kgrp;
+  constexpr int SK = 16 / KWC;
+  struct Frag {
+    float a[TM][SK], b[TN][SK];
+  };
+  auto lds_frag = [&](int buf, Frag &f) {
     const float *As = lds + buf * STG;
     const float *Bs = As + ASZ;
-    constexpr int QW = 4 / KW; // 16-B quads of the k-contiguous fragments this k-group consumes
-    float af[TM][AKC ? 16 : 1], bf[TN][BKC ? 16 : 1];
-    if constexpr (AKC) {
+    constexpr int QW = 4 / KWC; // 16-B quads of the k-contiguous fragments this k-group consumes
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        const int row = wm * TM * 32 + tm * 32 + li;
+    for (int tm = 0; tm < TM; ++tm) {
+      const int row = wm * TM * 32 + tm * 32 + li;
+      if constexpr (AKC) {
         const int sw = (row >> 1) & 7;
 #pragma unroll
         for (int qq = 0; qq < QW; ++qq) {
-          const int q = kgrp * QW + qq;
+          const int q = kq0 * QW + qq;
           const f32x4 v = *reinterpret_cast<const f32x4 *>(As + row * BK + 4 * ((lh * 4 + q) ^ sw));
 #pragma unroll
-          for (int e = 0; e < 4; ++e) af[tm][qq * 4 + e] = v[e];
+          for (int e = 0; e < 4; ++e) f.a[tm][qq * 4 + e] = v[e];
         }
+      } else {
+#pragma unroll
+        for (int ss = 0; ss < SK; ++ss) f.a[tm][ss] = As[(lh * 16 + kq0 * SK + ss) * BM + (row ^ (lh << 5))];
       }
     }
-    if constexpr (BKC) {
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        const int row = wn * TN * 32 + tn * 32 + li;
+    for (int tn = 0; tn < TN; ++tn) {
+      const int row = wn * TN * 32 + tn * 32 + li;
+      if constexpr (BKC) {
         const int sw = (row >> 1) & 7;
 #pragma unroll
         for (int qq = 0; qq < QW; ++qq) {
-          const int q = kgrp * QW + qq;
+          const int q = kq0 * QW + qq;
           const f32x4 v = *reinterpret_cast<const f32x4 *>(Bs + row * BK + 4 * ((lh * 4 + q) ^ sw));
 #pragma unroll
-          for (int e = 0; e < 4; ++e) bf[tn][qq * 4 + e] = v[e];
+          for (int e = 0; e < 4; ++e) f.b[tn][qq * 4 + e] = v[e];
         }
+      } else {
+#pragma unroll
+        for (int ss = 0; ss < SK; ++ss) f.b[tn][ss] = Bs[(lh * 16 + kq0 * SK + ss) * BN + (row ^ (lh << 5))];
       }
     }
+  };
+  auto mfma_frag = [&](const Frag &f) {
 #pragma unroll
-    for (int ss = 0; ss < 16 / KW; ++ss) {
-      const int s = kgrp * (16 / KW) + ss; // this k-group's steps (uniform)
-      float av[TM], bv[TN];
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        if constexpr (AKC) av[tm] = af[tm][ss];
-        else av[tm] = As[(lh * 16 + s) * BM + ((wm * TM * 32 + tm * 32 + li) ^ (lh << 5))];
-      }
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        if constexpr (BKC) bv[tn] = bf[tn][ss];
-        else bv[tn] = Bs[(lh * 16 + s) * BN + ((wn * TN * 32 + tn * 32 + li) ^ (lh << 5))];
-      }
+    for (int ss = 0; ss < SK; ++ss)
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm], bv[tn], acc[tm][tn], 0, 0, 0);
-    }
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[tm][ss], f.b[tn][ss], acc[tm][tn], 0, 0, 0);
+  };
+  auto compute = [&](int buf) {
+    Frag f;
+    lds_frag(buf, f);
+    mfma_frag(f);
   };
 
   if (EPI == EPI_HEAD) KT(0);
@@ -760,18 +777,58 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
     if (t < nk) issue(t);
-  for (int i = 0; i < nk; ++i) {
-    vm_wait_tiles<P, NS>(min(NS - 2, nk - 1 - i)); // this wave's pieces of k-tile i landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier(); // everyone's pieces landed; buffer (i - 1) % NS no longer read
-    if (EPI == EPI_HEAD && i < 24) KT(1 + i);
-    if (i + NS - 1 < nk) issue(i + NS - 1);
-    compute(i % NS);
+  if constexpr (PIPE) {
+    // f[i & 1] holds k-tile i's fragments. Iteration i: wait until k-tile i+1 has landed and every wave's
+    // reads of k-tile i are complete (vmcnt, lgkmcnt, barrier), refill buffer i % NS with k-tile i + NS,
+    // then k-tile i's MFMAs with the DMA issue and the LDS reads of k-tile i+1 interleaved between them
+    // (sched_group_barrier): the wave's one MFMA chain no longer waits behind that work. The refill is
+    // unconditional (k-tiles past the end read the zero chunk into a buffer nobody reads again), so the
+    // loop body is one basic block and the wait count is the constant NS-2 k-tiles.
+    static_assert(KW == 1, "PIPE: one k-group (the DMA issue must be branch-free)");
+    Frag f[2];
+    if (nk > 0) {
+      for (int t = nk; t < NS - 1; ++t) issue(t); // pad to NS-1 issued k-tiles (zero chunks)
+      vm_wait_tiles<P, NS>(NS - 2); // k-tile 0 landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      issue(NS - 1);
+      lds_frag(0, f[0]);
+    }
+    constexpr int NMF = SK * TM * TN;   // MFMAs per k-tile
+    constexpr int NDS = (TM + TN) * 4;  // LDS read instructions per k-tile (upper bound)
+    for (int i = 0; i < nk; i += 2) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) { // unrolled by two: the register sets are static
+        const int ii = i + u;
+        if (ii >= nk) break;
+        vm_wait_tiles<P, NS>(NS - 2); // k-tile ii+1 landed (NS-2 k-tiles issued after it)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(ii + NS); // buffer ii % NS: its fragments are in f[u]
+        lds_frag((ii + 1) % NS, f[u ^ 1]);
+        mfma_frag(f[u]);
+#pragma unroll
+        for (int j = 0; j < NMF; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); // one MFMA
+          if (j < P) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0); // one DMA piece
+          if (j < NDS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); // one LDS read
+        }
+      }
+    }
+  } else {
+    for (int i = 0; i < nk; ++i) {
+      vm_wait_tiles<P, NS>(min(NS - 2, nk - 1 - i)); // this wave's pieces of k-tile i landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier(); // everyone's pieces landed; buffer (i - 1) % NS no longer read
+      if (EPI == EPI_HEAD && i < 24) KT(1 + i);
+      if (i + NS - 1 < nk) issue(i + NS - 1);
+      if (!LDR || kgrp == 0) compute(i % NS); // wave-uniform
+    }
   }
   if (EPI == EPI_HEAD) KT(25);
   if (EPI == EPI_HEAD) KTC(41);
   __syncthreads(); // the LDS is the epilogue's now
-  if constexpr (KW > 1) { // group sums through LDS, in group order (group 0 keeps the result)
+  if constexpr (KW > 1 && !LDR) { // group sums through LDS, in group order (group 0 keeps the result)
     float *red = lds;
     static_assert(TM * TN * 16 * 256 <= LDS_F, "k-group reduction buffer");
     for (int q = 1; q < KW; ++q) {
@@ -804,7 +861,8 @@ bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 
 // NS > 0: the LDS-DMA kernel with NS tile buffers where the shape allows it (FAST shapes, no gathered
 // mn-contiguous operand); otherwise the register-staged kernel (KW k-groups, PF register sets).
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int KW = 1, int PF = 1, int NS = 0>
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int KW = 1, int PF = 1, int NS = 0,
+          bool PIPE = false, bool LDR = false>
 void launch(hipStream_t s, const GemmDesc &d) {
   // FAST loads: K % 4 == 0, vector-aligned operands, column counts % 4 == 0
   const bool fast = d.K % 4 == 0 && (d.lda % 4 == 0) && (d.ldb % 4 == 0) &&
@@ -857,8 +915,10 @@ void launch(hipStream_t s, const GemmDesc &d) {
   if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
     if (fast && glds_on && (AKC || !d.a_idx)) {
       const dim3 gb(256 * KW);
-      if (d.a_idx) hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, NS, KW>), grid, gb, 0, s, k);
-      else hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, KW>), grid, gb, 0, s, k);
+      if (d.a_idx)
+        hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, NS, KW, PIPE, LDR>), grid, gb, 0, s, k);
+      else
+        hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, KW, PIPE, LDR>), grid, gb, 0, s, k);
       return;
     }
   }
@@ -877,6 +937,8 @@ template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const G
   // LDS-DMA stages: as many tile buffers as fit two workgroups per CU (80 KB each)
   if (d.tile == TILE_32x128) { // 32 x 128 (20 KB per stage), one 8-wave workgroup (two k-groups) per CU
     // (six stages measured no faster: profiles/r02/small_tile_variants.txt)
+    // (PIPE / LDR variants measured no faster: profiles/r02/gemm_small_tiles.txt; these tiles are bound by
+    // the per-CU operand delivery rate, ~22 GB/s per CU, not by the loop's instruction schedule)
     if (pf_small >= 2) launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 2, 4>(s, d);
     else launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 1, 4>(s, d);
   } else if (d.tile == TILE_64x64) { // 64 x 64 (16 KB per stage)
