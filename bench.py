@@ -134,6 +134,25 @@ def slbfgs_cpu_baseline(dims, acts, N, step, epochs=1):
                        f"{dt:.1f} s")
 
 
+_JSON_OUT = None
+
+
+def emit(line: dict):
+    """The one stdout line. Everything else the process prints (RCCL's version banner at communicator
+    init, libdrm notices, C printf from any library) was sent to stderr by isolate_stdout()."""
+    out = _JSON_OUT or sys.stdout
+    out.write(json.dumps(line) + "\n")
+    out.flush()
+
+
+def isolate_stdout():
+    """Keep stdout for the JSON line alone: duplicate fd 1 for emit(), then point fd 1 at stderr."""
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
 def main_slbfgs(a, pkg, ctx, world, rank):
     """BASELINE config 4: S-LBFGS epochs/s (+ grad-evals/s); every rank holds all N rows and evaluates its
     1/world slice of each minibatch, Hessian batch and full-gradient anchor (s_lbfgs.hpp:165-290)."""
@@ -223,11 +242,12 @@ def main_slbfgs(a, pkg, ctx, world, rank):
         }
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = slbfgs_cpu_baseline(dims, acts, N, a.slbfgs_step)
-        print(json.dumps(out), flush=True)
+        emit(out)
 
 
 def main():
     a = parse()
+    isolate_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -372,7 +392,7 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             rows = a.cpu_samples or (N if N <= 60000 else 2000)
             out["cpu_baseline"] = cpu_baseline(dims, acts, N, a.m, a.cpu_iters, a.data, min(rows, N))
-        print(json.dumps(out), flush=True)
+        emit(out)
     run.close()
     if world > 1:
         torch.distributed.destroy_process_group()
