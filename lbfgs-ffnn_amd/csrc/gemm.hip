@@ -941,6 +941,9 @@ template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const G
     // the per-CU operand delivery rate, ~22 GB/s per CU, not by the loop's instruction schedule)
     if (pf_small >= 2) launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 2, 4>(s, d);
     else launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 1, 4>(s, d);
+  } else if (d.tile == TILE_64x128) { // 64 x 128 (24 KB per stage), two workgroups per CU
+    if (pf_small >= 2) launch<2, 2, 1, 2, AKC, BKC, EPI, 1, 2, 3>(s, d);
+    else launch<2, 2, 1, 2, AKC, BKC, EPI, 1, 1, 3>(s, d);
   } else if (d.tile == TILE_64x64) { // 64 x 64 (16 KB per stage)
     if (pf_small >= 2) launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 2, 5>(s, d);
     else launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 1, 5>(s, d);
@@ -964,11 +967,20 @@ void gemm_tile_for(int N, int tile, int *BM, int *BN) {
     *BN = 64;
     return;
   }
+  if (tile == TILE_64x128) {
+    *BM = 64;
+    *BN = 128;
+    return;
+  }
   *BM = 128;
   *BN = N > 64 ? 128 : (N > 32 ? 64 : 32);
 }
 
-int gemm_row_tiles(int M, int tile) { return tile == TILE_32x128 ? (M + 31) / 32 : (M + 127) / 128; }
+int gemm_row_tiles(int M, int tile) {
+  int BM, BN;
+  gemm_tile_for(128, tile, &BM, &BN);
+  return (M + BM - 1) / BM;
+}
 
 void gemm(hipStream_t s, const GemmDesc &d) {
   if (d.M <= 0 || d.N <= 0) return;

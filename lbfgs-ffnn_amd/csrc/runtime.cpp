@@ -137,8 +137,16 @@ void Mlp::plan(long long B) {
     L.fsplits = 1;
     L.fk_chunk = L.in;
     L.ftile = TILE_AUTO;
-    if (fwd_small_ && L.out <= 128 && cdiv(B, 128) < 256) {
-      L.ftile = TILE_32x128; // four times the row tiles, full rows (the head can still fuse), no split
+    // Row-tile height for full-width (out <= 128) layers, where the head can fuse: the smallest tile count
+    // that still fills the chip, since a small tile is bound by its per-CU operand delivery (~22 GB/s per
+    // CU for the LDS-DMA stream; profiles/r02/gemm_small_tiles.txt): 32 x 128 while one workgroup per CU
+    // covers the rows (a rank's 7500-row shard), 64 x 128 while two per CU do (15000 / 30000 rows: 37 / 62
+    // us for the 784 -> 128 main loop against 42 / 79 with 32-row tiles), else 128 x 128.
+    const long long cus = ctx_->cus;
+    if (fwd_small_ && L.out <= 128 && cdiv(B, 32) <= cus) {
+      L.ftile = TILE_32x128; // full rows (the head can still fuse), no split
+    } else if (fwd_small_ && L.out <= 128 && cdiv(B, 64) <= 2 * cus) {
+      L.ftile = TILE_64x128;
     } else if (ftiles < 192 && L.in >= 256) {
       long long fs = std::min(cdiv(384, ftiles), (long long)L.in / 128);
       long long fkc = cdiv(cdiv(L.in, fs), 32) * 32;

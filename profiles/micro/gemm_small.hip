@@ -1,9 +1,9 @@
-// Small-tile GEMM main-loop micro-benchmark (gfx950): what limits the 32 x 128 forward tile of a rank's
-// 7500-row shard (one workgroup per CU) and the 64 x 64 split-K dW tile?
+// Small-tile GEMM main-loop micro-benchmark (gfx950): the forward GEMM's row tile per shard size
+// (32 / 64 / 128 x 128 at 7500 / 15000 / 30000 / 60000 rows of 784 -> 128: Mlp::plan's rule).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../lbfgs-ffnn_amd/csrc gemm_small.hip -o gemm_small
-// Every variant runs the library's own gemm_glds_kernel (EPI_FWD / EPI_STORE epilogue: no head) on
-// synthetic operands; the "A0" / "B0" data modes give an operand a zero row stride, so all its k-tiles
-// hit the same few cache lines (L1/L2 resident): what is left is the in-core cost of the loop.
+// Every variant runs the library's own gemm_glds_kernel (EPI_FWD epilogue: no head) on synthetic
+// operands. Earlier revisions of this file (git history) also timed the PIPE / LDR / register-staged
+// variants and operands with a zero row stride (L1/L2-resident): profiles/r02/gemm_small_tiles.txt.
 #include "gemm.hip"
 
 #include <cstdio>
@@ -80,104 +80,34 @@ int main() {
   CK(hipMemset(W, 0, (long long)In * Out * 4 + 4096));
   CK(hipMemset(D, 0, Mbig * Out * 4));
   const int reps = 200;
-  for (int mode = 0; mode < 3; mode += 2) { // 0: real operands, 1: A0 (X row stride 0), 2: B0 (W row stride 0)
-    const char *mn = mode == 0 ? "" : (mode == 1 ? " A0" : " B0");
-    for (long long M : {7500LL, 60000LL}) {
-      GemmK k{};
-      k.M = int(M);
-      k.N = Out;
-      k.K = In;
-      k.k_chunk = In;
-      k.A = X;
-      k.lda = mode == 1 ? 0 : In;
-      k.a_mvalid = int(M);
-      k.a_ones = -1;
-      k.a_vec = 1;
-      k.B = W;
-      k.ldb = mode == 2 ? 0 : Out;
-      k.b_vec = 1;
-      k.C = C;
-      k.ldc = Out;
-      k.act = ACT_RELU;
-      const double fl = 2.0 * M * In * Out;
-      char nm[96];
-      if (M == 7500) {
-        const dim3 g32(1, unsigned((M + 31) / 32), 1);
-        snprintf(nm, sizeof nm, "fwd 32x128 KW2 NS4%s M=%lld", mn, M);
-        run<1, 4, 1, 1, true, false, EPI_FWD, 4, 2, false>(nm, k, g32, reps, fl);
-        snprintf(nm, sizeof nm, "fwd 32x128 KW1 NS4 PIPE%s M=%lld", mn, M);
-        run<1, 4, 1, 1, true, false, EPI_FWD, 4, 1, true>(nm, k, g32, reps, fl);
-        snprintf(nm, sizeof nm, "fwd 32x128 KW1 NS5 PIPE%s M=%lld", mn, M);
-        run<1, 4, 1, 1, true, false, EPI_FWD, 5, 1, true>(nm, k, g32, reps, fl);
-        snprintf(nm, sizeof nm, "fwd 32x128 KW1 NS4%s M=%lld", mn, M);
-        run<1, 4, 1, 1, true, false, EPI_FWD, 4, 1, false>(nm, k, g32, reps, fl);
-        snprintf(nm, sizeof nm, "fwd 32x128 LDR NS4%s M=%lld", mn, M);
-        run<1, 4, 1, 1, true, false, EPI_FWD, 4, 2, false, true>(nm, k, g32, reps, fl);
-        snprintf(nm, sizeof nm, "fwd 32x128 LDR NS6%s M=%lld", mn, M);
-        run<1, 4, 1, 1, true, false, EPI_FWD, 6, 2, false, true>(nm, k, g32, reps, fl);
-        snprintf(nm, sizeof nm, "fwd 32x128 RS KW1 PF2%s M=%lld", mn, M);
-        run_rs<1, 4, 1, 1, true, false, EPI_FWD, 1, 2>(nm, k, g32, reps, fl);
-        snprintf(nm, sizeof nm, "fwd 32x128 RS KW2 PF2%s M=%lld", mn, M);
-        run_rs<1, 4, 1, 1, true, false, EPI_FWD, 2, 2>(nm, k, g32, reps, fl);
-        snprintf(nm, sizeof nm, "fwd 32x128 RS KW1 PF3%s M=%lld", mn, M);
-        run_rs<1, 4, 1, 1, true, false, EPI_FWD, 1, 3>(nm, k, g32, reps, fl);
-      }
-      const dim3 g128(1, unsigned((M + 127) / 128), 1);
-      snprintf(nm, sizeof nm, "fwd 128x128 NS2%s M=%lld", mn, M);
-      run<2, 2, 2, 2, true, false, EPI_FWD, 2, 1, false>(nm, k, g128, reps, fl);
-      snprintf(nm, sizeof nm, "fwd 128x128 LDR NS2%s M=%lld", mn, M);
-      run<2, 2, 2, 2, true, false, EPI_FWD, 2, 2, false, true>(nm, k, g128, reps, fl);
-      snprintf(nm, sizeof nm, "fwd 128x128 RS PF2%s M=%lld", mn, M);
-      run_rs<2, 2, 2, 2, true, false, EPI_FWD, 1, 2>(nm, k, g128, reps, fl);
-    }
-  }
-  // dW of the shard: [768 x 128] = X^T delta over 7500 rows, 64 x 64 tiles, 20 splits of 384 rows
-  for (int mode = 0; mode < 3; mode += 2) {
-    const char *mn = mode == 0 ? "" : (mode == 1 ? " A0" : " B0");
-    const int B = 7500, splits = 20, kc = 384;
+  // forward GEMM tile per shard size (EPI_FWD, 784 -> 128): rows of a 1/2/4/8-rank shard of N = 60000
+  for (long long M : {7500LL, 15000LL, 30000LL, 60000LL}) {
     GemmK k{};
-    k.M = 768;
+    k.M = int(M);
     k.N = Out;
-    k.K = B;
-    k.k_chunk = kc;
+    k.K = In;
+    k.k_chunk = In;
     k.A = X;
-    k.lda = mode == 1 ? 0 : In;
-    k.a_mvalid = 768;
+    k.lda = In;
+    k.a_mvalid = int(M);
     k.a_ones = -1;
     k.a_vec = 1;
-    k.B = D;
-    k.ldb = mode == 2 ? 0 : Out;
+    k.B = W;
+    k.ldb = Out;
     k.b_vec = 1;
     k.C = C;
     k.ldc = Out;
-    k.slab_stride = 768LL * Out;
-    const double fl = 2.0 * B * 768 * Out;
+    k.act = ACT_RELU;
+    const double fl = 2.0 * M * In * Out;
     char nm[96];
-    snprintf(nm, sizeof nm, "dW 64x64 NS5 s20%s", mn);
-    run<2, 2, 1, 1, false, false, EPI_STORE, 5, 1, false>(nm, k, dim3(2, 12, splits), reps, fl);
-    snprintf(nm, sizeof nm, "dW 64x64 NS5 PIPE s20%s", mn);
-    run<2, 2, 1, 1, false, false, EPI_STORE, 5, 1, true>(nm, k, dim3(2, 12, splits), reps, fl);
-    k.k_chunk = 7500 / 10 / 32 * 32 + 32;
-    snprintf(nm, sizeof nm, "dW 64x64 NS5 s10%s", mn);
-    run<2, 2, 1, 1, false, false, EPI_STORE, 5, 1, false>(nm, k, dim3(2, 12, 10), reps, fl);
-    snprintf(nm, sizeof nm, "dW 64x64 NS5 PIPE s10%s", mn);
-    run<2, 2, 1, 1, false, false, EPI_STORE, 5, 1, true>(nm, k, dim3(2, 12, 10), reps, fl);
-    snprintf(nm, sizeof nm, "dW 64x64 LDR NS5 s10%s", mn);
-    run<2, 2, 1, 1, false, false, EPI_STORE, 5, 2, false, true>(nm, k, dim3(2, 12, 10), reps, fl);
-    snprintf(nm, sizeof nm, "dW 64x64 RS PF2 s10%s", mn);
-    run_rs<2, 2, 1, 1, false, false, EPI_STORE, 1, 2>(nm, k, dim3(2, 12, 10), reps, fl);
-    k.k_chunk = kc;
-    snprintf(nm, sizeof nm, "dW 64x64 RS PF2 s20%s", mn);
-    run_rs<2, 2, 1, 1, false, false, EPI_STORE, 1, 2>(nm, k, dim3(2, 12, 20), reps, fl);
-    k.k_chunk = 7500 / 10 / 32 * 32 + 32;
-    k.k_chunk = kc;
-    snprintf(nm, sizeof nm, "dW 128x128 NS2 s20%s", mn);
-    run<2, 2, 2, 2, false, false, EPI_STORE, 2, 1, false>(nm, k, dim3(1, 6, splits), reps, fl);
-    k.k_chunk = 7500 / 40 / 32 * 32 + 32;
-    snprintf(nm, sizeof nm, "dW 128x128 NS2 s40%s", mn);
-    run<2, 2, 2, 2, false, false, EPI_STORE, 2, 1, false>(nm, k, dim3(1, 6, unsigned((B + k.k_chunk - 1) / k.k_chunk)), reps, fl);
-    snprintf(nm, sizeof nm, "dW 128x128 LDR NS3 s40%s", mn);
-    run<2, 2, 2, 2, false, false, EPI_STORE, 3, 2, false, true>(nm, k, dim3(1, 6, unsigned((B + k.k_chunk - 1) / k.k_chunk)), reps, fl);
+    snprintf(nm, sizeof nm, "fwd 32x128 KW2 NS4 M=%lld", M);
+    run<1, 4, 1, 1, true, false, EPI_FWD, 4, 2, false>(nm, k, dim3(1, unsigned((M + 31) / 32), 1), reps, fl);
+    snprintf(nm, sizeof nm, "fwd 64x128 NS3 M=%lld", M);
+    run<2, 2, 1, 2, true, false, EPI_FWD, 3, 1, false>(nm, k, dim3(1, unsigned((M + 63) / 64), 1), reps, fl);
+    snprintf(nm, sizeof nm, "fwd 64x128 KW2 NS3 M=%lld", M);
+    run<2, 2, 1, 2, true, false, EPI_FWD, 3, 2, false>(nm, k, dim3(1, unsigned((M + 63) / 64), 1), reps, fl);
+    snprintf(nm, sizeof nm, "fwd 128x128 NS2 M=%lld", M);
+    run<2, 2, 2, 2, true, false, EPI_FWD, 2, 1, false>(nm, k, dim3(1, unsigned((M + 127) / 128), 1), reps, fl);
   }
   CK(hipDeviceSynchronize());
   return 0;

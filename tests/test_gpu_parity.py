@@ -93,6 +93,25 @@ def test_loss_grad_gather_and_l2(ctx, pkg, O):
     assert rel(host(g), g_ref) <= GRAD_RTOL
 
 
+@pytest.mark.parametrize("dims,acts", [([784, 128, 10], ["relu", "linear"]),
+                                       ([784, 128, 64, 10], ["relu", "relu", "linear"])])
+@pytest.mark.parametrize("N,gather", [(8192, False), (8200, False), (15000, True), (30000, False),
+                                      (32768, False), (32800, True)])
+def test_forward_tile_routes_match_oracle(ctx, pkg, O, dims, acts, N, gather):
+    """Mlp::plan's forward row tiles at a rank's shard sizes: 32 x 128 up to 32 rows per CU, 64 x 128 up
+    to 128 rows per CU (the 15000 / 30000-row shards of 4 / 2 ranks), 128 x 128 beyond; each with the
+    fused head and the fold, against the oracle (gathered rows: the S-LBFGS anchor path)."""
+    Xh, Yh = pkg.synth_mnist(N, dims[0], dims[-1], 7)
+    idx = np.random.default_rng(N).permutation(N)[: N - 37].astype(np.int64) if gather else None
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    loss, g = net.loss_grad(P, dev(Xh), dev(Yh),
+                            idx=torch.from_numpy(idx.astype(np.int32)).cuda() if gather else None)
+    l_ref, g_ref = O.Net(dims, acts).loss_grad(host(P), Xh.astype(np.float64), Yh.astype(np.float64), idx=idx)
+    assert abs(loss - l_ref) <= LOSS_RTOL * abs(l_ref)
+    assert rel(host(g), g_ref) <= GRAD_RTOL
+
+
 def test_eval_is_deterministic(ctx, pkg):
     """Fixed-order reductions: two evaluations of the same point are bitwise identical (the Wolfe
     line search's cached f / grad reuse relies on it)."""
