@@ -137,16 +137,30 @@ void Mlp::plan(long long B) {
     L.fsplits = 1;
     L.fk_chunk = L.in;
     L.ftile = TILE_AUTO;
-    // Row-tile height for full-width (out <= 128) layers, where the head can fuse: the smallest tile count
-    // that still fills the chip, since a small tile is bound by its per-CU operand delivery (~22 GB/s per
-    // CU for the LDS-DMA stream; profiles/r02/gemm_small_tiles.txt): 32 x 128 while one workgroup per CU
-    // covers the rows (a rank's 7500-row shard), 64 x 128 while two per CU do (15000 / 30000 rows: 37 / 62
-    // us for the 784 -> 128 main loop against 42 / 79 with 32-row tiles), else 128 x 128.
-    const long long cus = ctx_->cus;
-    if (fwd_small_ && L.out <= 128 && cdiv(B, 32) <= cus) {
-      L.ftile = TILE_32x128; // full rows (the head can still fuse), no split
-    } else if (fwd_small_ && L.out <= 128 && cdiv(B, 64) <= 2 * cus) {
-      L.ftile = TILE_64x128;
+    // Row-tile height for layers 65..128 wide (one column tile of 128, where the head can fuse). A small
+    // tile is bound by its per-CU operand delivery (~22 GB/s per CU for the LDS-DMA stream,
+    // profiles/r02/gemm_small_tiles.txt), a 128-row tile by the MFMA issue, so the plan takes the tile
+    // with the shortest estimated launch: n = the most tiles any CU gets, each costing a measured time per
+    // 32-deep k-tile, plus one epilogue per round of co-resident workgroups (one per CU for 32 x 128,
+    // two otherwise). Constants: 784 -> 128 with the fused head on MI355X (profiles/r02/
+    // gemm_fwd_tiles_by_shard.txt, tile64_*.json, tilemodel_*.json): 32 x 128 at 7500 rows (one round),
+    // 64 x 128 at 15000-40000 rows (forward 63.5 -> 48.4 us at 15000, 120.4 -> 77.9 at 30000,
+    // 132.4 -> 112.7 at 40000), 128 x 128 at 60000 (137 against 144.5 with 64-row tiles). Layers up to 64
+    // wide keep the round-1 rule (32-row tiles below 256 row tiles of 128, else 128 x 64 / 128 x 32).
+    const long long cus = ctx_->cus, nkt = cdiv(L.in, 32);
+    auto est_us = [&](long long bm, double per_ktile, long long per_round, double epi) {
+      const long long n = cdiv(cdiv(B, bm), cus);
+      return double(n) * per_ktile * double(nkt) + double(cdiv(n, per_round)) * epi;
+    };
+    if (fwd_small_ && L.out > 64 && L.out <= 128) {
+      const double t32 = est_us(32, 0.93, 1, 8.0), t64 = est_us(64, 1.25, 2, 12.0), t128 = est_us(128, 2.3, 2, 20.0);
+      if (t32 <= t64 && t32 <= t128) L.ftile = TILE_32x128; // full rows (the head can still fuse), no split
+      else if (t64 <= t128) L.ftile = TILE_64x128;
+    } else if (fwd_small_ && L.out <= 64 && cdiv(B, 128) < 256) {
+      L.ftile = TILE_32x128;
+    }
+    if (L.ftile != TILE_AUTO) {
+      // no split: the fused head and the activation need the full K
     } else if (ftiles < 192 && L.in >= 256) {
       long long fs = std::min(cdiv(384, ftiles), (long long)L.in / 128);
       long long fkc = cdiv(cdiv(L.in, fs), 32) * 32;

@@ -98,9 +98,9 @@ def test_loss_grad_gather_and_l2(ctx, pkg, O):
 @pytest.mark.parametrize("N,gather", [(8192, False), (8200, False), (15000, True), (30000, False),
                                       (32768, False), (32800, True)])
 def test_forward_tile_routes_match_oracle(ctx, pkg, O, dims, acts, N, gather):
-    """Mlp::plan's forward row tiles at a rank's shard sizes: 32 x 128 up to 32 rows per CU, 64 x 128 up
-    to 128 rows per CU (the 15000 / 30000-row shards of 4 / 2 ranks), 128 x 128 beyond; each with the
-    fused head and the fold, against the oracle (gathered rows: the S-LBFGS anchor path)."""
+    """Mlp::plan's forward row tiles at a rank's shard sizes (its cost model picks 32 x 128 at 8192 rows,
+    64 x 128 at 8200 / 15000 / 30000 / 32768 / 32800 on 256 CUs; 128 x 128 at 60000 elsewhere); each with
+    the fused head and the fold, against the oracle (gathered rows: the S-LBFGS anchor path)."""
     Xh, Yh = pkg.synth_mnist(N, dims[0], dims[-1], 7)
     idx = np.random.default_rng(N).permutation(N)[: N - 37].astype(np.int64) if gather else None
     net = pkg.Mlp(ctx, dims, acts)
