@@ -162,7 +162,17 @@ void Mlp::plan(long long B) {
     if (L.ftile != TILE_AUTO) {
       // no split: the fused head and the activation need the full K
     } else if (ftiles < 192 && L.in >= 256) {
-      long long fs = std::min(cdiv(384, ftiles), (long long)L.in / 128);
+      // Few rows of a wide layer (S-LBFGS minibatches: 256 x 784 -> 512 is 8 tiles of 128 x 128): split
+      // K. With 32 x 128 tiles the rows make 4x the tiles, so fewer, longer splits fill the chip (one
+      // workgroup per CU) and the slabs are a quarter of the bytes of 128 x 128 tiles at the same count.
+      const long long tiles32 = cdiv(B, 32) * cdiv(L.out, 128);
+      long long fs;
+      if (fwd_small_ && 2 * tiles32 <= cus) {
+        L.ftile = TILE_32x128;
+        fs = std::max(2LL, std::min(cus / tiles32, cdiv(L.in, 64))); // splits of >= 2 k-tiles
+      } else {
+        fs = std::min(cdiv(384, ftiles), (long long)L.in / 128);
+      }
       long long fkc = cdiv(cdiv(L.in, fs), 32) * 32;
       fs = cdiv(L.in, fkc);
       if (fs > 1) {
