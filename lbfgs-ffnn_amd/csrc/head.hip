@@ -30,6 +30,64 @@ using namespace headc;
 
 constexpr int MAX_WG = 512; // 2 workgroups per CU
 
+// One tile's activations, A[b0 .. b0+TB)[0 .. H), in registers: every load issued before the first use
+// (clamped addresses, masked values), so staging a tile is one memory round trip instead of one per
+// 16-B chunk of the thread's share. H % 4 == 0 and 16-B aligned rows (vec); else the scalar path.
+struct TileRegs {
+  static constexpr int QPT = TB * (HMAX / 4) / 256; // 16-B chunks per thread (16 at H = 256)
+  f32x4 v[QPT];
+  __device__ inline void load(const float *A, int H, int Hp, long long b0, int rows) {
+    const int t = threadIdx.x, Hq = H >> 2, hq = Hp >> 2;
+#pragma unroll
+    for (int j = 0; j < QPT; ++j) {
+      const int e = t + j * 256;
+      const int r = e / hq, c4 = e - r * hq;
+      const bool ok = e < TB * hq && r < rows && c4 < Hq;
+      const f32x4 x = *reinterpret_cast<const f32x4 *>(A + (ok ? (b0 + r) * H + 4 * c4 : 0LL));
+      v[j] = ok ? x : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __device__ inline void store(const Smem &sm) const {
+    const int t = threadIdx.x, hq = sm.Hp >> 2;
+#pragma unroll
+    for (int j = 0; j < QPT; ++j) {
+      const int e = t + j * 256;
+      const int r = e / hq, c4 = e - r * hq;
+      if (e < TB * hq) *reinterpret_cast<f32x4 *>(sm.As + r * sm.LDA + 4 * c4) = v[j];
+    }
+  }
+};
+
+// W (H x Out, <= 4096 values) in registers, loaded with the first tile: one round trip for both.
+struct WRegs {
+  static constexpr int PT = HMAX * HMAX_OUT / 256;
+  float w[PT];
+  float bias;
+  __device__ inline void load(const float *P, int H, int Out) {
+    const int t = threadIdx.x, n = H * Out;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int e = t + j * 256;
+      w[j] = P[e < n ? e : 0];
+    }
+    bias = P[(long long)H * Out + (t < Out ? t : 0)];
+  }
+  // Wt [16][LDA] and Wr [Hp][16], zeros outside Out x H (the caller zeroed both and barriered)
+  __device__ inline void store(const Smem &s, int Out) const {
+    const int t = threadIdx.x, n = s.H * Out;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int e = t + j * 256;
+      if (e < n) {
+        const int i = e / Out, o = e - i * Out;
+        s.Wt[o * s.LDA + i] = w[j];
+        s.Wr[i * 16 + o] = w[j];
+      }
+    }
+    if (t < HMAX_OUT) s.bias[t] = t < Out ? bias : 0.0f;
+  }
+};
+
 template <int QM>
 __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const float *P, int Out, const float *Y,
                                                    const int *idx, long long B, int act_out, int act_prev,
@@ -41,8 +99,19 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
   const int t = threadIdx.x, LDA = sm.LDA, Hp = sm.Hp;
   const long long ntiles = (B + TB - 1) / TB;
   const bool vec = (H & 3) == 0 && ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(delta)) & 15) == 0;
-  const int Hq = H >> 2;
-  stage_w(sm, P, Out);
+  TileRegs tr;
+  long long tl = blockIdx.x;
+  if (vec && tl < ntiles) tr.load(A, H, Hp, tl * TB, int(min((long long)TB, B - tl * TB)));
+  if (vec) {
+    WRegs wr; // in flight with the first tile; stage_w's zero fill meanwhile
+    wr.load(P, H, Out);
+    for (int e = t; e < 16 * LDA; e += 256) sm.Wt[e] = 0.0f;
+    for (int e = t; e < Hp * 16; e += 256) sm.Wr[e] = 0.0f;
+    __syncthreads();
+    wr.store(sm, Out);
+  } else {
+    stage_w(sm, P, Out);
+  }
   f32x4 cw[QM];
 #pragma unroll
   for (int q = 0; q < QM; ++q) cw[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -60,16 +129,15 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
   ta.xr = nullptr;
   ta.nfold = 0;
   FoldAcc fa; // unused (no fold in the standalone kernel)
-  for (long long tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+  for (; tl < ntiles; tl += gridDim.x) {
     const long long b0 = tl * TB;
     const int rows = int(min((long long)TB, B - b0));
-    // ---- stage the activation tile ----
+    // ---- stage the activation tile (prefetched in registers on the vector path) ----
     if (vec) {
-      for (int e = t; e < TB * (Hp >> 2); e += 256) {
-        const int r = e / (Hp >> 2), c4 = e - r * (Hp >> 2);
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (r < rows && c4 < Hq) v = *reinterpret_cast<const f32x4 *>(A + (b0 + r) * H + 4 * c4);
-        *reinterpret_cast<f32x4 *>(sm.As + r * LDA + 4 * c4) = v;
+      tr.store(sm);
+      if (tl + gridDim.x < ntiles) { // the block's next tile, in flight during this one's products
+        const long long nb0 = (tl + gridDim.x) * TB;
+        tr.load(A, H, Hp, nb0, int(min((long long)TB, B - nb0)));
       }
     } else {
       for (int e = t; e < TB * Hp; e += 256) {

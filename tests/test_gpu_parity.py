@@ -112,6 +112,23 @@ def test_forward_tile_routes_match_oracle(ctx, pkg, O, dims, acts, N, gather):
     assert rel(host(g), g_ref) <= GRAD_RTOL
 
 
+@pytest.mark.parametrize("H", [132, 200, 255, 256])
+@pytest.mark.parametrize("N", [1, 63, 256, 40000])
+def test_standalone_head_matches_oracle(ctx, pkg, O, H, N):
+    """The standalone head kernel (last hidden layer wider than 128, so not fused into its GEMM): tiles
+    and W prefetched in registers (H % 4 == 0) or the scalar staging path (H = 255); at N = 40000 each
+    workgroup walks two 64-row tiles, the second prefetched during the first."""
+    dims, acts = [48, H, 10], ["relu", "linear"]
+    X, Y = random_problem(dims, N, seed=H + N)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    loss, g = net.loss_grad(P, dev(X), dev(Y))
+    onet = O.Net(dims, acts)
+    l_ref, g_ref = onet.loss_grad(host(P), X, Y)
+    assert abs(loss - l_ref) <= LOSS_RTOL * abs(l_ref)
+    assert rel(host(g), g_ref) <= GRAD_RTOL
+
+
 def test_eval_is_deterministic(ctx, pkg):
     """Fixed-order reductions: two evaluations of the same point are bitwise identical (the Wolfe
     line search's cached f / grad reuse relies on it)."""
