@@ -338,25 +338,36 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
   if (KW > 1 && kgrp != 0) return; // group 0 holds the sums
   // Epilogue: lanes 0-31 own consecutive columns -> each register row is a 128-B coalesced store.
   float *C = g.C + (EPI == EPI_STORE ? (long long)zsplit * g.slab_stride : 0LL);
+  // EPI_DX's act' operand (the previous layer's activations) is loaded for the whole (tm, tn) block before
+  // the first use, from clamped addresses: a load-use-store per element made every element a dependent
+  // memory round trip (64 per lane at 128 x 128; the cfg-3 dX GEMM spent most of its 35 us there).
   with_act(EPI == EPI_FWD ? g.act : (EPI == EPI_DX ? g.aux_act : int(ACT_LINEAR)),
            [&](auto AC) __attribute__((always_inline)) {
     constexpr int A = decltype(AC)::value;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       const int n = n0 + wn * TN * 32 + tn * 32 + li;
-      if (n >= g.N) continue;
+      const bool nok = n < g.N;
       float bn = 0.0f;
-      if constexpr (EPI == EPI_FWD) bn = g.bias ? g.bias[n] : 0.0f;
+      if constexpr (EPI == EPI_FWD) bn = (g.bias && nok) ? g.bias[n] : 0.0f;
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
+        float ax[16];
+        if constexpr (EPI == EPI_DX) {
+          const int nc = nok ? n : 0;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            ax[r] = g.aux[(long long)(m < g.M ? m : 0) * g.ldaux + nc];
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (m >= g.M) continue;
           float v = acc[tm][tn][r];
           if constexpr (EPI == EPI_FWD) v = act_c<A>(v + bn);
-          if constexpr (EPI == EPI_DX) v *= dact_c<A>(g.aux[(long long)m * g.ldaux + n]);
-          C[(long long)m * g.ldc + n] = v;
+          if constexpr (EPI == EPI_DX) v *= dact_c<A>(ax[r]);
+          if (nok && m < g.M) C[(long long)m * g.ldc + n] = v;
         }
       }
     }
