@@ -349,7 +349,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
       const int n = n0 + wn * TN * 32 + tn * 32 + li;
       const bool nok = n < g.N;
       float bn = 0.0f;
-      if constexpr (EPI == EPI_FWD) bn = (g.bias && nok) ? g.bias[n] : 0.0f;
+      if constexpr (EPI == EPI_FWD) bn = g.bias ? g.bias[nok ? n : 0] : 0.0f;
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
         float ax[16];

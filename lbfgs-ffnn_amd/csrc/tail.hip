@@ -226,12 +226,12 @@ __device__ __forceinline__ void tail_cols_body(const TailArgs &a) {
   double s = 0.0;
   for (int r0 = t; r0 < a.nb; r0 += 256 * 8) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 8; ++u) { // unconditional loads from clamped rows: all eight in flight at once
       const int r = r0 + 256 * u;
-      v[u] = r < a.nb ? colp[r] : 0.0;
+      v[u] = colp[r < a.nb ? r : 0];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
+    for (int u = 0; u < 8; ++u) s += (r0 + 256 * u < a.nb) ? v[u] : 0.0;
   }
   s = t_wave_sum(s);
   if ((t & 63) == 0) ws[t >> 6] = s;
