@@ -120,6 +120,9 @@ static long long split_factor(long long tiles, long long K, long long min_chunk,
   return best;
 }
 
+// Batches up to this many rows are "small" for the dW plan (64x64 tiles, k chunks of two k-tiles).
+constexpr long long DW_SMALL_BATCH = 2048;
+
 // Forward plan (split-K for few row tiles), the EPI_HEAD fold, then the split-K plan of every dW GEMM
 // for batch B (workgroup-slot aware, split_factor), k chunks a multiple of the 32-deep LDS tile.
 void Mlp::plan(long long B) {
@@ -182,8 +185,11 @@ void Mlp::plan(long long B) {
       }
     }
     // dW: 64x64 tiles over narrow outputs -> fewer, longer K splits (a third of the slab traffic)
-    // (only for short K: at long K the 128x128 tile's reuse wins over the slab savings)
-    L.dtile = (dw64_ && L.out <= 128 && L.in + 1 <= 1024 && B <= 16384) ? TILE_64x64 : TILE_AUTO;
+    // (only for short K: at long K the 128x128 tile's reuse wins over the slab savings). Small batches
+    // (S-LBFGS minibatches, K = 128 / 256 rows) take 64x64 tiles at any width: four times the tiles of
+    // 128x128 at the same K, where 128x128 tiles filled a fifth of the chip (784 -> 512: 56 workgroups).
+    L.dtile = (dw64_ && ((L.out <= 128 && L.in + 1 <= 1024 && B <= 16384) || B <= DW_SMALL_BATCH)) ? TILE_64x64
+                                                                                                 : TILE_AUTO;
   }
   // The last hidden layer's dW GEMM has in + 1 rows; when they pass a multiple of its tile height by
   // at most 16 input columns + the bias row (784 + 1 = 6 x 128 + 17 at cfg 2), those rows go to the
@@ -209,7 +215,7 @@ void Mlp::plan(long long B) {
     const long long M = (fold_ >= 0 && l == nl - 2) ? fold_c0_ : L.in + 1;
     gemm_tile_for(L.out, L.dtile, &BM, &BN);
     const long long tiles = cdiv(M, BM) * cdiv(L.out, BN);
-    const long long min_chunk = L.dtile == TILE_64x64 ? 256 : 128;
+    const long long min_chunk = L.dtile == TILE_64x64 ? (B <= DW_SMALL_BATCH ? 64 : 256) : 128;
     long long side = 0;
     if (side_reduced(l + 1, fused, 0)) {
       const Layer &N1 = layers_[l + 1];
