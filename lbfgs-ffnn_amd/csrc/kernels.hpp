@@ -124,6 +124,7 @@ struct RedSeg {
   long long stride = 0, count = 0, goff = 0;
   int splits = 0;
   int parts = 1; // blocks per 64-column group, each over a contiguous range of splits
+  int gpb = 1;   // parts == 1: 64-column groups per block (RA_GPB while the splits are few)
   int wg0 = 0;   // first block of the segment (reduce launch)
   int cg0 = 0;   // first column group of the segment (global numbering)
   int fin0 = -1; // parts > 1: first block of the segment in the finishing launch
@@ -147,6 +148,7 @@ struct RedAllArgs {
   const int *abort = nullptr;
 };
 constexpr int RA_COLS = 64;
+constexpr int RA_GPB = 4; // column groups per reduce_all block for single-pass segments
 constexpr int RA_MAXPART = 32;
 constexpr int RA_SPLITS_PER_PART = 64; // 4 stripes x 16 loads per thread
 constexpr int RA_MAXFIN = 128;         // column groups the one-block finishing launch combines

@@ -577,7 +577,10 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       g.fin0 = ra.nfin;
       ra.nfin += ncols;
     }
-    ra.nwg += ncols * g.parts;
+    // few splits: RA_GPB groups per block (a block's loads are few, blocks the cost); many: one group per
+    // block, so the splits' loads spread over four times the blocks (the 20-slab shard gradient)
+    g.gpb = g.parts == 1 && g.splits <= 8 ? RA_GPB : 1;
+    ra.nwg += g.parts > 1 ? ncols * g.parts : int(cdiv(ncols, g.gpb));
     ra.ncg += ncols;
   }
   ra.nseg = nl;

@@ -236,15 +236,127 @@ __device__ __forceinline__ void ra_column(const RedAllArgs &a, const RedSeg &S, 
   }
 }
 
+// Segments reduced in one pass (parts == 1) take RA_GPB column groups per block, four columns per lane:
+// every load of the block (slab values, then the operands of ra_columns) is issued before its first use,
+// and a quarter of the blocks of one group each (a 535,818-parameter gradient was 8,372 blocks, several
+// rounds per CU).
+template <int J>
+__device__ __forceinline__ void ra_columns(const RedAllArgs &a, const RedSeg &S, int cg0, long long cgl0,
+                                           const double (&colsum)[J]) {
+  const int lane = threadIdx.x & 63;
+  const bool need_w = a.w && (a.dots || (a.l2 && a.lambda != 0.0));
+  const bool lam = a.l2 && a.lambda != 0.0;
+  long long e[J];
+  bool live[J];
+  float gv[J], wv[J], pv[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const long long col = (cgl0 + j) * RA_COLS + lane;
+    live[j] = col < S.count;
+    e[j] = S.goff + (live[j] ? col : 0);
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    gv[j] = S.splits > 0 ? float(colsum[j]) : a.G[e[j]];
+    wv[j] = need_w ? a.w[e[j]] : 0.0f;
+    pv[j] = (a.dots && a.p) ? a.p[e[j]] : 0.0f;
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    if ((cgl0 + j) * RA_COLS >= S.count) break; // wave-uniform: past the segment's last group
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+    float g = gv[j];
+    if (live[j]) {
+      if (lam) g = g + float(a.lambda) * wv[j]; // finalize_kernel's update
+      if (a.dots) {
+        d0 = double(g) * double(g);
+        if (a.p) d1 = double(g) * double(pv[j]);
+        d2 = double(wv[j]) * double(wv[j]);
+      }
+      if (S.splits > 0 || lam) a.G[e[j]] = g;
+    }
+    if (a.dots) {
+      d0 = wave_sum(d0);
+      d1 = wave_sum(d1);
+      d2 = wave_sum(d2);
+      if (lane == 0) {
+        const int cg = cg0 + j;
+        a.partials[cg * 3 + 0] = d0;
+        a.partials[cg * 3 + 1] = d1;
+        a.partials[cg * 3 + 2] = d2;
+      }
+    }
+  }
+}
+
+// One block of a single-pass segment: J column groups (J * 64 columns, one per lane per group).
+template <int J>
+__device__ __forceinline__ void ra_block(const RedAllArgs &a, const RedSeg &S, int local, double (*part)[RA_GPB * RA_COLS]) {
+  const int t = threadIdx.x, lane = t & 63, stripe = t >> 6;
+  const long long cgl0 = (long long)local * J;
+  double acc[J];
+  const float *src[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const long long col = (cgl0 + j) * RA_COLS + lane;
+    acc[j] = 0.0;
+    src[j] = S.slab + (col < S.count ? col : 0); // clamped; masked when used
+  }
+  if (S.splits > 0) {
+    // the stripe's splits k = stripe, stripe + 4, ...: rounds of four (4 x J loads in flight), then the
+    // last up-to-three from clamped splits, masked; summed in split order either way
+    int k = stripe;
+    for (; k + 12 < S.splits; k += 16) {
+      float x[4][J];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < J; ++j) x[u][j] = src[j][(long long)(k + 4 * u) * S.stride];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < J; ++j) acc[j] += double(x[u][j]);
+    }
+    float x[3][J];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const long long kk = k + 4 * u < S.splits ? k + 4 * u : 0;
+#pragma unroll
+      for (int j = 0; j < J; ++j) x[u][j] = src[j][kk * S.stride];
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (k + 4 * u < S.splits) // wave-uniform
+#pragma unroll
+        for (int j = 0; j < J; ++j) acc[j] += double(x[u][j]);
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) part[stripe][j * RA_COLS + lane] = acc[j];
+  __syncthreads();
+  if (stripe != 0) return;
+  double colsum[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int q = j * RA_COLS + lane;
+    colsum[j] = ((part[0][q] + part[1][q]) + part[2][q]) + part[3][q];
+  }
+  ra_columns<J>(a, S, S.cg0 + int(cgl0), cgl0, colsum);
+}
+
 __global__ __launch_bounds__(256) void reduce_all_kernel(const RedAllArgs a) {
   if (a.abort && *a.abort) return;
-  __shared__ double part[4][RA_COLS];
+  __shared__ double part[4][RA_GPB * RA_COLS];
   const int t = threadIdx.x, lane = t & 63, stripe = t >> 6;
   const int b = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nseg && a.seg[si + 1].wg0 <= b) ++si;
   const RedSeg S = a.seg[si];
   const int local = b - S.wg0;
+  if (S.parts == 1) { // wave-uniform
+    if (S.gpb == RA_GPB) ra_block<RA_GPB>(a, S, local, part);
+    else ra_block<1>(a, S, local, part);
+    return;
+  }
   const int cgl = local / S.parts, pi = local - cgl * S.parts;
   const int cg = S.cg0 + cgl;
   const long long col = (long long)cgl * RA_COLS + lane;
@@ -269,10 +381,7 @@ __global__ __launch_bounds__(256) void reduce_all_kernel(const RedAllArgs a) {
   __syncthreads();
   if (stripe != 0) return;
   const double colsum = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
-  if (S.parts > 1)
-    a.colpart[((long long)cg * RA_MAXPART + pi) * RA_COLS + lane] = colsum;
-  else
-    ra_column(a, S, cg, col, live, colsum);
+  a.colpart[((long long)cg * RA_MAXPART + pi) * RA_COLS + lane] = colsum;
 }
 
 // One block: combine the split-range partials of the multi-range column groups, then (single rank)
