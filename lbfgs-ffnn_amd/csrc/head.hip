@@ -24,6 +24,8 @@
 
 namespace lbf {
 
+__host__ __device__ int head_hsplit(long long B, int H);
+
 namespace {
 
 using namespace headc;
@@ -99,8 +101,19 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
   const int t = threadIdx.x, LDA = sm.LDA, Hp = sm.Hp;
   const long long ntiles = (B + TB - 1) / TB;
   const bool vec = (H & 3) == 0 && ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(delta)) & 15) == 0;
+  // H split over hsplit workgroups per tile group (few tiles): split hs covers 64 columns of delta and the
+  // matching [dW ; db] row strips (the last one also the bias row)
+  const int hsplit = head_hsplit(B, H), hs = int(blockIdx.x) % hsplit;
+  const int nwt = int(gridDim.x) / hsplit; // workgroups along the tiles
+  HRange hr;
+  if (hsplit > 1) {
+    hr.st0 = 4 * hs;
+    hr.st1 = hs == hsplit - 1 ? (H + 1 + 15) / 16 : 4 * hs + 4;
+    hr.cb0 = 4 * hs;
+    hr.cb1 = 4 * hs + 4;
+  }
   TileRegs tr;
-  long long tl = blockIdx.x;
+  long long tl = int(blockIdx.x) / hsplit;
   if (vec && tl < ntiles) tr.load(A, H, Hp, tl * TB, int(min((long long)TB, B - tl * TB)));
   if (vec) {
     WRegs wr; // in flight with the first tile; stage_w's zero fill meanwhile
@@ -129,14 +142,14 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
   ta.xr = nullptr;
   ta.nfold = 0;
   FoldAcc fa; // unused (no fold in the standalone kernel)
-  for (; tl < ntiles; tl += gridDim.x) {
+  for (; tl < ntiles; tl += nwt) {
     const long long b0 = tl * TB;
     const int rows = int(min((long long)TB, B - b0));
     // ---- stage the activation tile (prefetched in registers on the vector path) ----
     if (vec) {
       tr.store(sm);
-      if (tl + gridDim.x < ntiles) { // the block's next tile, in flight during this one's products
-        const long long nb0 = (tl + gridDim.x) * TB;
+      if (tl + nwt < ntiles) { // the block's next tile, in flight during this one's products
+        const long long nb0 = (tl + nwt) * TB;
         tr.load(A, H, Hp, nb0, int(min((long long)TB, B - nb0)));
       }
     } else {
@@ -146,19 +159,28 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
       }
     }
     __syncthreads();
-    tile<false, QM, false>(sm, ta, b0, rows, cw, sse, fa);
+    tile<false, QM, false>(sm, ta, b0, rows, cw, sse, fa, hr);
   }
-  write_partials(sm, Out, cw, sse, slab + (long long)blockIdx.x * (H + 1) * Out, sse_part + blockIdx.x);
+  if (hs != 0) sse = 0.0; // every split computed the same loss; the first one reports it
+  write_partials(sm, Out, cw, sse, slab + (long long)blockIdx.x * (H + 1) * Out, sse_part + blockIdx.x, hr);
 }
 
 } // namespace
 
 bool head_supported(int H, int Out) { return Out >= 1 && Out <= HMAX_OUT && H >= 1 && H <= HMAX; }
 int head_tile(int) { return TB; }
-// Workgroups (== partial slabs): one per tile up to MAX_WG, then a balanced number of tiles each.
-int head_nwg(long long B, int) {
+// H splits per tile: 64 hidden columns per workgroup while a batch has at most 64 tiles (an S-LBFGS
+// minibatch of 256 rows is 4 tiles: 4 workgroups on a 256-wide layer were 23 us, one CU each)
+__host__ __device__ int head_hsplit(long long B, int H) {
+  const long long nt = ((B > 1 ? B : 1) + TB - 1) / TB;
+  const int hp = (H + 63) / 64;
+  return nt <= 64 && hp > 1 ? hp : 1;
+}
+// Workgroups (== partial slabs): one per tile (x the H splits) up to MAX_WG, then a balanced number of
+// tiles each.
+int head_nwg(long long B, int H) {
   const long long nt = cdiv(std::max(1LL, B), TB);
-  if (nt <= MAX_WG) return int(nt);
+  if (nt <= MAX_WG) return int(nt) * head_hsplit(B, H);
   const long long per = cdiv(nt, MAX_WG);
   return int(cdiv(nt, per));
 }

@@ -189,6 +189,13 @@ struct FoldAcc {
   f32x4 c[2];
   float db[2];
 };
+// The part of the hidden width one workgroup covers (the standalone head splits H over workgroups when a
+// batch has few tiles; the forward Z is then computed by each of them): [dW ; db] row strips [st0, st1)
+// (strip = 16 rows, the bias row included in the last) and delta column strips [cb0, cb1) (cb0 even).
+// Default: everything.
+struct HRange {
+  int st0 = 0, st1 = 1 << 20, cb0 = 0, cb1 = 1 << 20;
+};
 
 // One tile: s.As holds the activations of samples b0..b0+rows-1 (zero-padded to Hp columns), staged
 // and followed by a barrier. Accumulates [dW ; db] into cw and the SSE into sse; writes the tile's
@@ -198,7 +205,7 @@ struct FoldAcc {
 // FOLD: accumulate the fold (TileArgs::xr / nfold) into fa; needs H <= 128 (one pass of column strips).
 template <bool EXTRA_WAVES, int QM, bool FOLD> // EXTRA_WAVES: waves >= 4 only join barriers
 __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int rows, f32x4 (&cw)[QM], double &sse,
-                            FoldAcc &fa) {
+                            FoldAcc &fa, const HRange &hr = HRange()) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int r0 = wave * 16, LDA = s.LDA, H = s.H;
@@ -267,8 +274,8 @@ __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int 
   if (active) {
 #pragma unroll
     for (int q = 0; q < QM; ++q) {
-      const int st = wave + 4 * q;
-      if (st * 16 > H) continue; // wave-uniform
+      const int st = hr.st0 + wave + 4 * q;
+      if (st * 16 > H || st >= hr.st1) continue; // wave-uniform
       const int ic = st * 16 + li;
       const int icc = ic < H ? ic : 0;
       const bool bias_strip = st * 16 + 15 >= H; // wave-uniform
@@ -300,7 +307,7 @@ __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int 
     const int ncs = (H + 15) >> 4;
     with_act(a.act_prev, [&](auto AC) __attribute__((always_inline)) {
       constexpr int A = decltype(AC)::value;
-      for (int cb = 2 * wave; cb < ncs; cb += 8) { // wave-uniform; one pass when H <= 128
+      for (int cb = hr.cb0 + 2 * wave; cb < ncs && cb < hr.cb1; cb += 8) { // wave-uniform; one pass when H <= 128
         const f32x4 wb0 = *reinterpret_cast<const f32x4 *>(s.Wr + (cb * 16 + li) * 16 + g * 4);
         const f32x4 wb1 = *reinterpret_cast<const f32x4 *>(s.Wr + ((cb + 1) * 16 + li) * 16 + g * 4);
         const int col = cb * 16 + li;
@@ -369,16 +376,23 @@ __device__ inline void write_fold(const FoldAcc &fa, int H, int nfold, float *sl
 }
 
 // The workgroup's [dW ; db] partial slab and SSE partial.
+// With an HRange narrower than the whole width, the slab's rows outside [16 st0, 16 st1) are written as
+// zeros (a sibling workgroup owns them), so the fixed-order slab reduction stays bitwise the same.
 template <int QM>
 __device__ inline void write_partials(const Smem &s, int Out, const f32x4 (&cw)[QM], double sse, float *slab,
-                                      double *sse_out) {
+                                      double *sse_out, const HRange &hr = HRange()) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int li = lane & 15, g = lane >> 4, H = s.H;
+  if (hr.st0 > 0 || hr.st1 * 16 < H + 1)
+    for (int e = t; e < (H + 1) * Out; e += blockDim.x) {
+      const int row = e / Out;
+      if (row < hr.st0 * 16 || row >= hr.st1 * 16) slab[e] = 0.0f;
+    }
   if (wave < 4 && li < Out) {
 #pragma unroll
     for (int q = 0; q < QM; ++q) {
-      const int st = wave + 4 * q;
-      if (st * 16 < H + 1) {
+      const int st = hr.st0 + wave + 4 * q;
+      if (st * 16 < H + 1 && st < hr.st1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = st * 16 + g * 4 + r;
