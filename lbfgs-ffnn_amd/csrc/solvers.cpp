@@ -567,12 +567,21 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
     tscal_.resize(SC_N);
     LBF_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     LBF_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    for (int i = 0; i < 2; ++i) {
+      LBF_HIP(hipEventCreateWithFlags(&ev_g2_[i], hipEventDisableTiming));
+      LBF_HIP(hipEventCreateWithFlags(&ev_free_[i], hipEventDisableTiming));
+    }
+    g2b_.resize(ng);
   }
 }
 
 SlbfgsSolver::~SlbfgsSolver() {
   if (ev_fork_) (void)hipEventDestroy(ev_fork_);
   if (ev_join_) (void)hipEventDestroy(ev_join_);
+  for (int i = 0; i < 2; ++i) {
+    if (ev_g2_[i]) (void)hipEventDestroy(ev_g2_[i]);
+    if (ev_free_[i]) (void)hipEventDestroy(ev_free_[i]);
+  }
 }
 
 void SlbfgsSolver::eval_pair(const float *wa, float *ga, const float *wb, float *gb, long long off,
@@ -690,18 +699,41 @@ int SlbfgsSolver::run(lbf_record *rec) {
       LBF_HIP(hipMemcpyAsync(wh_.get() + slot * ld, wt_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice,
                              s));
     }
+    // With the twin stream, the minibatch gradients at the anchor w (fixed for the epoch, and independent
+    // of the iterates) run one step ahead on it, double-buffered: step t's evaluation at w_t and its
+    // direction on the context stream then overlap the twin's gradient of minibatch t + 1 at w, instead of
+    // joining the two evaluations of each step. Same evaluations on the same inputs: bitwise the same.
+    float *g2buf[2] = {g2_.get(), tnet_ ? g2b_.get() : g2_.get()};
+    auto anchor_ahead = [&](int t) { // twin stream: gb of step t into g2buf[t & 1]
+      const long long b = mb[t].second;
+      const long long o = mb[t].first + b * rk / nr, c = b * (rk + 1) / nr - b * rk / nr;
+      LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_free_[t & 1], 0)); // step t - 2's direction read it
+      tnet_->loss_grad(w_.get(), g2buf[t & 1], xg_.get() + o * In, yg_.get() + o * Out, nullptr, c, 1.0 / double(b),
+                       prm_.lambda, nullptr, nullptr);
+      LBF_HIP(hipEventRecord(ev_g2_[t & 1], tctx_->stream));
+    };
+    // the epoch's gathered rows and w are complete (the context stream was synchronised above)
+    if (tnet_) anchor_ahead(0);
     for (int t = 0; t < m_inner; ++t) {
       const long long b = mb[t].second;
       const long long o = mb[t].first + b * rk / nr, c = b * (rk + 1) / nr - b * rk / nr;
-      eval_pair(wt_.get(), g1_.get(), w_.get(), g2_.get(), o, c, 1.0 / double(b));
+      if (tnet_) {
+        if (t + 1 < m_inner) anchor_ahead(t + 1);
+        net_->loss_grad(wt_.get(), g1_.get(), xg_.get() + o * In, yg_.get() + o * Out, nullptr, c, 1.0 / double(b),
+                        prm_.lambda, nullptr, nullptr);
+        LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_g2_[t & 1], 0));
+      } else {
+        eval_pair(wt_.get(), g1_.get(), w_.get(), g2_.get(), o, c, 1.0 / double(b));
+      }
       GramArgs ga;
       ga.policy = POL_SLBFGS;
       ga.has_g = 1;
       ga.ga = g1_.get();
-      ga.gb = g2_.get();
+      ga.gb = g2buf[t & 1];
       ga.gc = mu_.get();
       ga.g_out = v_.get();
       hist_.update(ga, 1, 1, +1.0);
+      if (tnet_) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // g2buf[t & 1] read (v formed)
       const int slot = wh_push_slot();
       // wt = wt - step * r ; w_history.push_back(wt)
       hist_.combine(v_.get(), nullptr, wt_.get(), wt_.get(), wh_.get() + slot * ld, false, -prm_.step);

@@ -180,7 +180,7 @@ private:
   const float *X_, *Y_;
   long long N_, n_;
   History hist_;
-  DevBuf<float> w_, wt_, mu_, g1_, g2_, v_, r_, u_, up_, s_, wp_, wm_, gp_, gm_, wh_;
+  DevBuf<float> w_, wt_, mu_, g1_, g2_, g2b_, v_, r_, u_, up_, s_, wp_, wm_, gp_, gm_, wh_;
   DevBuf<int> idx_;
   PinnedBuf<double> hs_;
   int iters_ = 0;
@@ -194,6 +194,7 @@ private:
   DevBuf<double> tscal_;
   DevBuf<float> xg_, yg_; // the epoch's sampled rows, gathered once (all minibatches and Hessian batches)
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+  hipEvent_t ev_g2_[2] = {nullptr, nullptr}, ev_free_[2] = {nullptr, nullptr}; // anchor gradients ahead (twin)
 };
 
 // CudaGD / CudaSGD (src/cuda/gd.cuh:38-106, sgd.cuh:50-153) on the MLP; return the iterations done.
