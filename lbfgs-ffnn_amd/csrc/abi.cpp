@@ -591,8 +591,11 @@ int lbf_sample_indices(long long N, int b, unsigned seed, int calls, long long *
   return guard([&] {
     LBF_REQUIRE(N >= 0 && b >= 0 && calls >= 0 && h_out, "bad argument");
     std::mt19937 rng(seed);
+    MinibatchSampler smp{size_t(N)}; // one permutation for every call, like the solver's
+    std::vector<int> v;
     for (int c = 0; c < calls; ++c) {
-      auto v = sample_minibatch(size_t(N), size_t(b), rng);
+      v.clear();
+      smp.draw(size_t(b), rng, v);
       for (size_t i = 0; i < v.size(); ++i) h_out[size_t(c) * b + i] = (long long)v[i];
     }
   });

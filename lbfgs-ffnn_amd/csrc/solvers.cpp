@@ -17,19 +17,33 @@ namespace {
 long long round4(long long n) { return cdiv(n, 4) * 4; }
 } // namespace
 
-std::vector<size_t> sample_minibatch(size_t N, size_t b, std::mt19937 &rng) {
+MinibatchSampler::MinibatchSampler(size_t N) : perm_(N) { std::iota(perm_.begin(), perm_.end(), size_t(0)); }
+
+size_t MinibatchSampler::draw(size_t b, std::mt19937 &rng, std::vector<int> &out) {
   // s_lbfgs.hpp:141-160: partial Fisher-Yates over iota(N), uniform_int_distribution<size_t>(i, N-1).
-  if (N == 0 || b == 0) return {};
-  std::vector<size_t> idx(N);
-  std::iota(idx.begin(), idx.end(), 0);
-  if (b >= N) return idx;
+  const size_t N = perm_.size();
+  if (N == 0 || b == 0) return 0;
+  if (b >= N) { // the whole identity, no draws
+    for (size_t i = 0; i < N; ++i) out.push_back(int(i));
+    return N;
+  }
+  touched_.resize(b);
   for (size_t i = 0; i < b; ++i) {
     std::uniform_int_distribution<size_t> dist(i, N - 1);
-    size_t j = dist(rng);
-    std::swap(idx[i], idx[j]);
+    const size_t j = dist(rng);
+    touched_[i] = j;
+    std::swap(perm_[i], perm_[j]);
   }
-  idx.resize(b);
-  return idx;
+  for (size_t i = 0; i < b; ++i) out.push_back(int(perm_[i]));
+  for (size_t i = b; i-- > 0;) std::swap(perm_[i], perm_[touched_[i]]); // undo in reverse: identity again
+  return b;
+}
+
+std::vector<size_t> sample_minibatch(size_t N, size_t b, std::mt19937 &rng) {
+  MinibatchSampler smp(N);
+  std::vector<int> v;
+  smp.draw(b, rng, v);
+  return std::vector<size_t>(v.begin(), v.end());
 }
 
 // ================================================================================================
@@ -636,6 +650,42 @@ int SlbfgsSolver::run(lbf_record *rec) {
     LBF_HIP(hipStreamSynchronize(s));
   };
   bool have_u = false, mu_valid = false;
+  // An epoch's index lists: every minibatch, the Hessian batches (only once a u exists), then the anchor
+  // pick, in the reference's RNG order (s_lbfgs.hpp:212-266). No draw depends on device values, so the next
+  // epoch's lists are drawn on the host while the GPU runs the current epoch.
+  struct EpochDraw {
+    std::vector<int> flat;
+    std::vector<std::pair<long long, long long>> mb, hb;
+    int pick = -1;
+    bool u_seen = false; // have_u after the epoch
+  };
+  MinibatchSampler sampler{size_t(N_)};
+  auto draw_epoch = [&](bool u_seen, EpochDraw &d) {
+    d.flat.clear();
+    d.mb.assign(size_t(m_inner), {0, 0});
+    d.hb.assign(size_t(m_inner), {-1, 0});
+    int whist_size = 1;
+    for (int t = 0; t < m_inner; ++t) {
+      const long long o = (long long)d.flat.size();
+      d.mb[t] = {o, (long long)sampler.draw(size_t(prm_.b), rng, d.flat)};
+      whist_size = std::min(whist_size + 1, L + 1);
+      if (t > 0 && t % L == 0) {
+        if (u_seen) {
+          const long long oh = (long long)d.flat.size();
+          d.hb[t] = {oh, (long long)sampler.draw(size_t(prm_.b_H), rng, d.flat)};
+        }
+        u_seen = true;
+      }
+    }
+    d.pick = -1;
+    if (whist_size >= 2) {
+      std::uniform_int_distribution<size_t> pk(0, size_t(whist_size) - 2); // s_lbfgs.hpp:266
+      d.pick = int(pk(rng));
+    }
+    d.u_seen = u_seen;
+  };
+  EpochDraw cur, next;
+  bool next_ready = false;
   const auto t0 = std::chrono::steady_clock::now();
   int rec_i = rec ? rec->size : 0;
   iters_ = 0;
@@ -645,30 +695,13 @@ int SlbfgsSolver::run(lbf_record *rec) {
       read();
     }
     if (std::sqrt(hs_[SC_TGG]) < prm_.tol) break; // s_lbfgs.hpp:208
-    // --- draw this epoch's samples in reference order -------------------------------------------
-    std::vector<int> flat;
-    std::vector<std::pair<long long, long long>> mb(m_inner), hb(m_inner, {-1, 0});
-    bool u_seen = have_u;
-    int whist_size = 1;
-    for (int t = 0; t < m_inner; ++t) {
-      auto v = sample_minibatch(size_t(N_), size_t(prm_.b), rng);
-      mb[t] = {(long long)flat.size(), (long long)v.size()};
-      for (size_t x : v) flat.push_back(int(x));
-      whist_size = std::min(whist_size + 1, L + 1);
-      if (t > 0 && t % L == 0) {
-        if (u_seen) {
-          auto h = sample_minibatch(size_t(N_), size_t(prm_.b_H), rng);
-          hb[t] = {(long long)flat.size(), (long long)h.size()};
-          for (size_t x : h) flat.push_back(int(x));
-        }
-        u_seen = true;
-      }
-    }
-    int pick = -1;
-    if (whist_size >= 2) {
-      std::uniform_int_distribution<size_t> pk(0, size_t(whist_size) - 2); // s_lbfgs.hpp:266
-      pick = int(pk(rng));
-    }
+    // --- this epoch's samples in reference order (drawn during the previous epoch when it ran) -------
+    if (next_ready) std::swap(cur, next);
+    else draw_epoch(have_u, cur);
+    next_ready = false;
+    const std::vector<int> &flat = cur.flat;
+    const auto &mb = cur.mb, &hb = cur.hb;
+    const int pick = cur.pick;
     idx_.ensure(std::max<size_t>(1, flat.size()));
     if (!flat.empty())
       LBF_HIP(hipMemcpyAsync(idx_.get(), flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
@@ -768,6 +801,11 @@ int SlbfgsSolver::run(lbf_record *rec) {
         LBF_HIP(hipMemcpyAsync(up_.get(), u_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
         have_u = true;
       }
+    }
+    // the next epoch's lists, drawn while the GPU runs this epoch's queued steps
+    if (iters_ + 1 < prm_.max_epochs) {
+      draw_epoch(cur.u_seen, next);
+      next_ready = true;
     }
     // anchor reset (s_lbfgs.hpp:265-270)
     const float *anchor = pick >= 0 ? wh_.get() + wh_slot(pick) * ld : wt_.get();
