@@ -81,6 +81,13 @@ def test_sample_indices_match_oracle(pkg, O):
     assert np.array_equal(pkg.sample_indices(10, 12, 1, 1)[0, :10], np.arange(10))
 
 
+def test_sampler_reuse_matches_oracle(pkg, O):
+    """The library draws every minibatch of an epoch from one reusable permutation (swaps undone after each
+    draw); many draws in a row, b close to N and b = 1 give the oracle's fresh-iota lists (s_lbfgs.hpp:141-160)."""
+    for N, b, seed, calls in [(1000, 999, 7, 40), (1000, 1, 3, 200), (517, 128, 11, 60), (60000, 128, 5, 30)]:
+        assert np.array_equal(pkg.sample_indices(N, b, seed, calls=calls), O.sample_indices(N, b, seed, calls=calls))
+
+
 def test_flop_model():
     import __graft_entry__
     pkg = __graft_entry__.load_package()
