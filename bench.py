@@ -30,9 +30,13 @@ import __graft_entry__  # noqa: E402
 
 METRIC = "L-BFGS iters/sec + grad-eval GFLOP/s, 784-128-10 MLP full-batch"
 REF_GPU_ITERS_PER_S = 139.1      # L-BFGS m=10, 784-128-10, N=60000 (sm_86, fp32 cuBLAS)
+# BASELINE.md's published GPU L-BFGS rates (the reference's CUDA route, N = 60000), by (dims, m)
+REF_GPU = {("784,128,10", 10): 139.1, ("784,128,10", 100): 87.2,
+           ("784,256,128,64,10", 10): 60.7, ("784,256,128,64,10", 100): 51.6}
 FP32_MFMA_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix peak (dense)
 HBM_PEAK_GBS = 8000.0
-PROF_EVERY = 8                   # time every 8th launch of the dominant kernel inside the timed region
+PROF_EVERY = 8                   # time every 8th launch of the dominant kernel inside the timed region ...
+PROF_MIN_LAUNCHES = 40           # ... unless that would time fewer launches than this (then every launch)
 
 
 def parse():
@@ -46,7 +50,12 @@ def parse():
     ap.add_argument("--dims", type=str, default="784,128,10")
     ap.add_argument("--acts", type=str, default="relu,linear")
     ap.add_argument("--m", type=int, default=10)
-    ap.add_argument("--line-search", type=str, default="wolfe")
+    ap.add_argument("--line-search", type=str, default="wolfe",
+                    help="wolfe: the reference's CPU semantics (lbfgs.hpp:38-100); armijo: its CUDA semantics "
+                         "(lbfgs.cuh:39-194), the route its published GPU it/s were measured on")
+    ap.add_argument("--init", choices=["cpu", "cuda"], default="cpu",
+                    help="parameter-init stream: cpu = network.hpp:45-71 (all params N(0, s)), cuda = "
+                         "network.cuh:36-59 (weights N(0, s), zero biases; the reference's GPU drivers)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--comm1", action="store_true",
                     help="at N=1, route evaluations through a 1-rank RCCL communicator (the DP code path)")
@@ -100,6 +109,11 @@ def route_env():
     return {k: v for k, v in sorted(os.environ.items()) if k.startswith("LBF_")}
 
 
+THREADS_NOTE = ("OpenMP threads = OMP_NUM_THREADS as the GPU box sets it (16): one GPU's 1/8 share of the "
+                "host's physical cores, the CPU share a one-GPU job gets on an 8-GPU node; the reference's own "
+                "CPU numbers (BASELINE.md) do not state their thread count")
+
+
 def cpu_baseline(dims, acts, N, m, iters, data, rows):
     """The oracle (fp64 C++/OpenMP restatement of the reference CPU path, literal call pattern incl. its
     redundant f/grad re-evaluations) timed on this host; bounded sample of the same workload: `rows` of
@@ -113,7 +127,7 @@ def cpu_baseline(dims, acts, N, m, iters, data, rows):
     ms = info["ms"]
     scale = rows / N
     return dict(value=round(iters / (ms / 1e3) * scale, 6), unit="iters/s", cores=O.num_threads(), kind="port",
-                host=host_cpu(),
+                host=host_cpu(), threads_note=THREADS_NOTE,
                 sample=f"{iters} L-BFGS iterations (Wolfe, m={m}) of the {'-'.join(map(str, dims))} MLP on "
                        f"{rows} of the N={N} rows{f' (rate scaled by {rows}/{N})' if rows != N else ''}, fp64 "
                        f"oracle (oracle/oracle.hpp) with the reference's f/grad call pattern "
@@ -131,6 +145,7 @@ def slbfgs_cpu_baseline(dims, acts, N, step, epochs=1):
     net.slbfgs(P, X, Y, epochs=epochs, tol=0.0, M=10, L=10, b=256, bH=128, step=step, lam=1e-4)
     dt = time.perf_counter() - t0
     return dict(value=round(epochs / dt, 6), unit="epochs/s", cores=O.num_threads(), kind="port", host=host_cpu(),
+                threads_note=THREADS_NOTE,
                 sample=f"{epochs} S-LBFGS epoch(s) of the {'-'.join(map(str, dims))} MLP on all N={N} rows (b=256, "
                        f"b_H=128, L=M=10), fp64 oracle (oracle/oracle.hpp), {O.num_threads()} OpenMP threads, "
                        f"{dt:.1f} s")
@@ -285,7 +300,7 @@ def main():
     else:  # this rank's shard generated in place
         X, Y = pkg.synth_regression(ctx, hi - lo, dims[0], row0=lo)
     net = pkg.Mlp(ctx, dims, acts)
-    P = net.init_params(123, "cpu")
+    P = net.init_params(123, a.init)
     torch.cuda.synchronize()
 
     run = pkg.LbfgsRun(net, P, X, Y, n_global=N, line_search=a.line_search, m=a.m, max_iters=1 << 30, tol=0.0,
@@ -306,10 +321,14 @@ def main():
         torch.distributed.broadcast_object_list(obj, src=0)
         dominant = obj[0]
     # timed region: only the dominant kernel carries an event pair
-    evals0, lonly0 = run.info.n_evals, run.info.n_loss_only
+    evals0, lonly0, gal0 = run.info.n_evals, run.info.n_loss_only, run.info.n_grad_after_loss
     it0 = run.hist.size
     ctx.prof_select(dominant)
-    ctx.prof_sample(PROF_EVERY)
+    # the dominant section runs about once per evaluation: sample every PROF_EVERY-th launch only when
+    # that still times PROF_MIN_LAUNCHES of them
+    launches = breakdown[dominant][1] / max(bd_steps, 1) * a.steps
+    every = PROF_EVERY if launches / PROF_EVERY >= PROF_MIN_LAUNCHES else 1
+    ctx.prof_sample(every)
     ctx.prof_enable(True)
 
     def barrier():
@@ -335,12 +354,16 @@ def main():
     ctx.prof_sample(1)
     evals = run.info.n_evals - evals0
     lonly = run.info.n_loss_only - lonly0
+    gal = run.info.n_grad_after_loss - gal0
     iters_done = run.hist.size - it0
 
     if rank == 0:
         F = pkg.grad_flops_per_sample(dims) * N            # algorithmic flops per full-batch evaluation
-        Ffwd = sum(2 * dims[l] * dims[l + 1] for l in range(len(dims) - 1)) * N  # loss-only trial (forward)
-        gflops = (evals * F + lonly * Ffwd) / elapsed / 1e9
+        Ffwd = sum(2 * dims[l] * dims[l + 1] for l in range(len(dims) - 1)) * N  # forward pass
+        # forward passes: full evaluations + loss-only trials, minus the backward halves that reused a
+        # loss-only trial's forward (each counted in n_evals too); backward passes: n_evals
+        fwd_passes = evals - gal + lonly
+        gflops = (fwd_passes * Ffwd + evals * (F - Ffwd)) / elapsed / 1e9
         # dominant kernel: largest total time in the timed region (HIP events on the library stream)
         name, (ms, cnt) = dominant, prof[dominant]
         avg_s = ms / 1e3 / cnt
@@ -357,6 +380,7 @@ def main():
         roof["kernel"] = name
         roof["avg_launch_us"] = round(avg_s * 1e6, 2)
         roof["timed_launches"] = cnt
+        roof["sampled_every"] = every
         roof["traffic"] = None
         if os.path.exists(a.pmc_json):
             try:
@@ -377,16 +401,20 @@ def main():
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": round(value / REF_GPU_ITERS_PER_S, 3),
+            "vs_baseline": (round(value / REF_GPU[(a.dims, a.m)], 3)
+                            if N == 60000 and (a.dims, a.m) in REF_GPU else None),
             "dtype": "fp32",
             "data": "synthetic" if a.data == "mnist" else "synthetic (config-5 regression stream, device-generated)",
             "config": {"workload": f"{a.dims} MLP ({a.acts}), full-batch L-BFGS m={a.m} "
-                                   f"({a.line_search} line search, CPU-reference semantics), N={N}",
+                                   f"({a.line_search} line search, "
+                                   f"{'CPU' if a.line_search == 'wolfe' else 'CUDA'}-reference semantics, "
+                                   f"{a.init} init stream), N={N}",
                        "global_batch": N,
                        "parallelism": f"dp{world}" + ("+rccl1" if a.comm1 and world == 1 else "")},
             "grad_eval_gflops": round(gflops, 1),
             "evals_per_iter": round(evals / max(iters_done, 1), 3),
             "loss_only_trials_per_iter": round(lonly / max(iters_done, 1), 3),
+            "forward_passes_per_iter": round(fwd_passes / max(iters_done, 1), 3),
             "roofline": roof,
             "kernel_ms_per_step": {k: round(v[0] / bd_steps, 4) for k, v in sorted(breakdown.items())},
             "route_env": route_env(),

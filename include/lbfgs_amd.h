@@ -49,8 +49,16 @@ typedef struct lbf_ctx lbf_ctx;
 typedef struct lbf_mlp lbf_mlp;
 typedef struct lbf_lbfgs lbf_lbfgs;
 
+/* ABI revision of this header. Structs only ever grow at their end; a caller checks
+ * lbf_abi_version() >= the LBF_ABI_VERSION it was compiled with before passing a struct the library
+ * writes (lbf_solve_info), so an older library never writes past a newer caller's struct and a newer
+ * library is never handed an older, smaller struct by a caller that did not check.
+ * 2: lbf_solve_info.n_grad_after_loss; lbf_comm_init_local (in-process rank group). */
+#define LBF_ABI_VERSION 2
+
 const char *lbf_last_error(void);
 const char *lbf_version(void);
+int lbf_abi_version(void);
 
 /* ---- context: device, stream, workspace, optional communicator --------------------------------
  * Replaces CublasHandle (src/cuda/cublas_handle.cuh:22-39) + the implicit legacy stream. */
@@ -63,6 +71,14 @@ void *lbf_ctx_stream(lbf_ctx *ctx);
  * collective. One all-reduce of [grad | loss] per loss+grad evaluation. */
 int lbf_comm_unique_id(char out[128]);
 int lbf_comm_init(lbf_ctx *ctx, int nranks, int rank, const char id[128]);
+/* In-process rank group: ctxs[r] becomes rank r of an nranks-rank group whose all-reduce sums every rank's
+ * buffer on the device in rank order (HIP events + a host barrier; no RCCL). All contexts must live on one
+ * device and each rank must then be driven by its own host thread, calling the same sequence of
+ * evaluations as the others (exactly as one process per GPU would). RCCL refuses two ranks on one GPU,
+ * so this is how the multi-rank path (shard offsets, n_global scaling, minibatch slices, replicated
+ * line-search decisions over summed data) runs on a single GPU; the product route is lbf_comm_init.
+ * ABI 2. */
+int lbf_comm_init_local(lbf_ctx **ctxs, int nranks);
 int lbf_comm_rank(lbf_ctx *ctx, int *rank, int *nranks);
 int lbf_allreduce_sum(lbf_ctx *ctx, float *d_buf, size_t count);
 
@@ -170,6 +186,10 @@ typedef struct lbf_solve_info {
   double final_loss, final_grad_norm;
   long long n_rows;   /* batch rows those evaluations covered on this rank (0 for callback objectives) */
   long long n_loss_only; /* line-search trials evaluated forward + loss only (rejected by Armijo) */
+  /* ABI 2: backward passes run on the forward state of a loss-only trial (it passed Armijo). Each is
+   * counted in n_evals too, so forward passes = n_evals - n_grad_after_loss + n_loss_only and
+   * backward passes = n_evals. */
+  long long n_grad_after_loss;
 } lbf_solve_info;
 
 void lbf_lbfgs_default_params(lbf_lbfgs_params *p, int line_search);

@@ -16,6 +16,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LBF_LIB_PATH") or os.path.join(_HERE, "build", "liblbfgs_amd.so")
 
+ABI_VERSION = 2  # include/lbfgs_amd.h LBF_ABI_VERSION
 LS_WOLFE, LS_ARMIJO = 0, 1
 INIT_CPU, INIT_CUDA = 0, 1
 ACTS = {"linear": 0, "tanh": 1, "relu": 2, "sigmoid": 3}
@@ -54,7 +55,8 @@ class Record(C.Structure):
 
 class SolveInfo(C.Structure):
     _fields_ = [("iterations", C.c_int), ("n_evals", C.c_longlong), ("final_loss", C.c_double),
-                ("final_grad_norm", C.c_double), ("n_rows", C.c_longlong), ("n_loss_only", C.c_longlong)]
+                ("final_grad_norm", C.c_double), ("n_rows", C.c_longlong), ("n_loss_only", C.c_longlong),
+                ("n_grad_after_loss", C.c_longlong)]
 
 
 _lib = None
@@ -73,12 +75,14 @@ def lib():
     sig = {
         "lbf_last_error": (C.c_char_p, []),
         "lbf_version": (C.c_char_p, []),
+        "lbf_abi_version": (C.c_int, []),
         "lbf_ctx_create": (C.c_int, [C.c_int, _vp, C.POINTER(_vp)]),
         "lbf_ctx_destroy": (C.c_int, [_vp]),
         "lbf_ctx_sync": (C.c_int, [_vp]),
         "lbf_ctx_stream": (_vp, [_vp]),
         "lbf_comm_unique_id": (C.c_int, [C.c_char_p]),
         "lbf_comm_init": (C.c_int, [_vp, C.c_int, C.c_int, C.c_char_p]),
+        "lbf_comm_init_local": (C.c_int, [C.POINTER(_vp), C.c_int]),
         "lbf_comm_rank": (C.c_int, [_vp, _ip, _ip]),
         "lbf_allreduce_sum": (C.c_int, [_vp, _vp, C.c_size_t]),
         "lbf_mlp_create": (C.c_int, [_vp, C.c_int, _ip, _ip, C.POINTER(_vp)]),
@@ -132,12 +136,14 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    if L.lbf_abi_version() < ABI_VERSION:
+        raise LbfError(f"{LIB_PATH} implements ABI {L.lbf_abi_version()}, this binding needs {ABI_VERSION}: rebuild it")
     _lib = L
     return L
 
 
-EXPORTS = ("lbf_last_error lbf_version lbf_ctx_create lbf_ctx_destroy lbf_ctx_sync lbf_ctx_stream "
-           "lbf_comm_unique_id lbf_comm_init lbf_comm_rank lbf_allreduce_sum lbf_mlp_create lbf_mlp_destroy "
+EXPORTS = ("lbf_last_error lbf_version lbf_abi_version lbf_ctx_create lbf_ctx_destroy lbf_ctx_sync lbf_ctx_stream "
+           "lbf_comm_unique_id lbf_comm_init lbf_comm_init_local lbf_comm_rank lbf_allreduce_sum lbf_mlp_create lbf_mlp_destroy "
            "lbf_mlp_param_count lbf_mlp_init_params lbf_init_params_host lbf_mlp_forward lbf_mlp_loss_grad lbf_two_loop lbf_dot "
            "lbf_nrm2 lbf_axpy lbf_scal lbf_lbfgs_default_params lbf_slbfgs_default_params lbf_lbfgs_solve "
            "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_prof_enable lbf_prof_select lbf_prof_sample lbf_prof_read lbf_synth_mnist "

@@ -6,6 +6,8 @@
 #include "runtime.hpp"
 #include "solvers.hpp"
 
+#include <rccl/rccl.h>
+
 #include <cstring>
 #include <memory>
 #include <string>
@@ -53,7 +55,8 @@ void check_comm(ncclResult_t r, const char *what) {
 extern "C" {
 
 const char *lbf_last_error(void) { return g_err.c_str(); }
-const char *lbf_version(void) { return "lbfgs_amd 0.1 (gfx950)"; }
+const char *lbf_version(void) { return "lbfgs_amd 0.3 (gfx950, abi 2)"; }
+int lbf_abi_version(void) { return LBF_ABI_VERSION; }
 
 int lbf_ctx_create(int device, void *stream, lbf_ctx **out) {
   return guard([&] {
@@ -107,18 +110,31 @@ int lbf_comm_unique_id(char out[128]) {
 int lbf_comm_init(lbf_ctx *ctx, int nranks, int rank, const char id[128]) {
   return guard([&] {
     LBF_REQUIRE(ctx && nranks >= 1 && rank >= 0 && rank < nranks, "comm args");
+    LBF_REQUIRE(id, "unique id");
     ctx->c.set_device();
-    if (ctx->c.comm) {
-      (void)ncclCommDestroy(ctx->c.comm);
-      ctx->c.comm = nullptr;
-    }
+    ctx->c.comm.reset();
     // a 1-rank communicator is created too: it routes evaluations through the data-parallel path
     // (local reduce -> ncclAllReduce -> tail), the single-GPU test of that path
-    ncclUniqueId uid;
-    std::memcpy(&uid, id, sizeof(uid));
-    check_comm(ncclCommInitRank(&ctx->c.comm, nranks, uid, rank), "ncclCommInitRank");
+    ctx->c.comm = make_rccl_comm(nranks, rank, id);
     ctx->c.rank = rank;
     ctx->c.nranks = nranks;
+  });
+}
+
+int lbf_comm_init_local(lbf_ctx **ctxs, int nranks) {
+  return guard([&] {
+    LBF_REQUIRE(ctxs && nranks >= 1 && nranks <= kMaxLocalRanks, "comm_init_local: 1..16 contexts");
+    for (int r = 0; r < nranks; ++r) {
+      LBF_REQUIRE(ctxs[r], "comm_init_local: null context");
+      LBF_REQUIRE(ctxs[r]->c.device == ctxs[0]->c.device, "comm_init_local: every context on one device");
+      for (int q = 0; q < r; ++q) LBF_REQUIRE(ctxs[q] != ctxs[r], "comm_init_local: a context twice");
+    }
+    auto group = make_local_group(nranks, ctxs[0]->c.device);
+    for (int r = 0; r < nranks; ++r) {
+      ctxs[r]->c.comm = std::move(group[size_t(r)]);
+      ctxs[r]->c.rank = r;
+      ctxs[r]->c.nranks = nranks;
+    }
   });
 }
 

@@ -202,6 +202,14 @@ void lincomb(hipStream_t s, long long n, const float *a, double c, const float *
 void gather_rows(hipStream_t s, const float *src, long long ld, const int *idx, long long count, int cols,
                  float *dst);
 void diff_scale(hipStream_t s, long long n, const float *a, const float *b, float scale, float *out);
+void zero_fill(hipStream_t s, long long n, float *x, const int *abort = nullptr);
+// dst = sum_i src[i] over the ranks of an in-process group, in rank order (comm.cpp LocalComm)
+constexpr int kMaxLocalRanks = 16;
+struct RankSrcs {
+  int n = 0;
+  const float *p[kMaxLocalRanks] = {};
+};
+void sum_ranks(hipStream_t s, const RankSrcs &r, long long count, float *dst);
 
 // ------------------------------------------------------------------------------------------------
 // Device-resident L-BFGS history ("vector-free" two-loop: Chen, Wang & Zhou, NIPS 2014).

@@ -12,7 +12,7 @@ namespace lbf {
 // Ctx
 // ------------------------------------------------------------------------------------------------
 Ctx::~Ctx() {
-  if (comm) (void)ncclCommDestroy(comm);
+  comm.reset();
   if (own_stream && stream) (void)hipStreamDestroy(stream);
 }
 
@@ -65,8 +65,7 @@ void Ctx::set_device() const { LBF_HIP(hipSetDevice(device)); }
 
 void Ctx::allreduce(float *buf, size_t count) {
   if (!comm) return;
-  ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat, ncclSum, comm, stream);
-  if (r != ncclSuccess) throw Error(3, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  comm->allreduce(buf, count, stream);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -416,43 +415,63 @@ void Mlp::forward_phase(const float *P, const float *X, const float *Y, const in
 // grad_after_loss. lambda must be 0 (the L-BFGS objectives).
 void Mlp::loss_only(const float *P, const float *X, const float *Y, const int *idx, long long B, double inv_scale,
                     double *scal) {
-  forward_phase(P, X, Y, idx, B, inv_scale);
+  LBF_REQUIRE(B >= 0, "negative batch");
   hipStream_t s = ctx_->stream;
   const float *hilo = nullptr;
-  if (ctx_->dp()) {
+  if (B > 0) forward_phase(P, X, Y, idx, B, inv_scale);
+  if (ctx_->dp() || B == 0) {
     hilo_.ensure(4);
-    sse_pack(s, loss_part_.get(), fs_.nloss, hilo_.get(), ctx_->abort);
-    ProfScope ps(ctx_, PK_ALLREDUCE);
-    ctx_->allreduce(hilo_.get(), 2);
+    if (B > 0) sse_pack(s, loss_part_.get(), fs_.nloss, hilo_.get(), ctx_->abort);
+    else zero_fill(s, 2, hilo_.get(), ctx_->abort);
+    if (ctx_->dp()) {
+      ProfScope ps(ctx_, PK_ALLREDUCE);
+      ctx_->allreduce(hilo_.get(), 2);
+    }
     hilo = hilo_.get();
   }
   ProfScope ps(ctx_, PK_FINAL, 2);
-  sse_loss(s, loss_part_.get(), fs_.nloss, hilo, inv_scale, scal, ctx_->abort);
+  sse_loss(s, loss_part_.get(), B > 0 ? fs_.nloss : 0, hilo, inv_scale, scal, ctx_->abort);
   ++loss_only_;
 }
 
 void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
                     double inv_scale, double lambda, const float *pdir, double *scal, const TailFuse *tf) {
-  forward_phase(P, X, Y, idx, B, inv_scale);
-  backward_phase(P, G, X, idx, B, inv_scale, lambda, pdir, scal, tf);
+  LBF_REQUIRE(B >= 0, "negative batch");
+  if (B > 0) forward_phase(P, X, Y, idx, B, inv_scale);
+  backward_phase(P, G, X, idx, B, inv_scale, lambda, pdir, scal, tf, false, nullptr);
+}
+
+void Mlp::loss_grad_local(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
+                          double inv_scale) {
+  LBF_REQUIRE(B >= 0, "negative batch");
+  if (B > 0) forward_phase(P, X, Y, idx, B, inv_scale);
+  backward_phase(P, G, X, idx, B, inv_scale, 0.0, nullptr, nullptr, nullptr, true, nullptr);
 }
 
 void Mlp::grad_after_loss(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
                           double lambda, const float *pdir, double *scal) {
-  LBF_REQUIRE(fs_.B == B, "grad_after_loss: no forward phase of this batch");
-  backward_phase(P, G, X, idx, B, inv_scale, lambda, pdir, scal, nullptr);
+  LBF_REQUIRE(B == 0 || fs_.B == B, "grad_after_loss: no forward phase of this batch");
+  ++gal_;
+  // the reduced route reports the loss of the loss-only trial's own all-reduced words, so the Armijo
+  // decision and the recorded loss are one value whatever order the collective sums the two buffers in
+  const bool reduced = ctx_->dp() || B == 0;
+  backward_phase(P, G, X, idx, B, inv_scale, lambda, pdir, scal, nullptr, false, reduced ? hilo_.get() : nullptr);
 }
 
 // Backward phase: the dW / dX GEMMs below the head, every layer's slab reduction, the gradient
 // finish (+ all-reduce, dots, status block) or the fused optimizer tail.
 void Mlp::backward_phase(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
-                         double lambda, const float *pdir, double *scal, const TailFuse *tf) {
+                         double lambda, const float *pdir, double *scal, const TailFuse *tf, bool local,
+                         const float *hilo_in) {
   hipStream_t s = ctx_->stream;
   const int nl = int(layers_.size());
   const Layer &Lo = layers_[nl - 1];
+  const bool empty = B == 0; // a data-parallel rank whose share of a small batch is empty
+  const bool reduced = ctx_->dp() || empty || local;
   const bool fused = fs_.fused;
-  const int fold = fs_.fold, nloss = fs_.nloss, lstart = fs_.lstart;
+  const int fold = empty ? -1 : fs_.fold, nloss = empty ? 0 : fs_.nloss, lstart = empty ? -1 : fs_.lstart;
   const long long nfold = fold >= 0 ? (long long)(fold + 1) * Lo.in : 0; // fold rows in the head slab
+  if (empty) zero_fill(s, (long long)nparams_ + 2, G, ctx_->abort);
   for (int l = lstart; l >= 0; --l) {
     const Layer &L = layers_[l];
     const float *Ain = (l == 0) ? X : A_[l - 1].get();
@@ -540,13 +559,14 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
   ra.p = pdir;
   ra.lambda = lambda;
   // scal == nullptr (S-LBFGS minibatch / Hessian-batch gradients, whose status nobody reads): the
-  // gradient only, no dot partials and no finishing launch
-  ra.dots = (ctx_->dp() || !scal) ? 0 : 1;
-  ra.l2 = ctx_->dp() ? 0 : 1;
+  // gradient only, no dot partials and no finishing launch. The reduced route (data parallel, an empty
+  // share, or a packed local evaluation) finishes the gradient from [G | hi | lo] after the all-reduce.
+  ra.dots = (reduced || !scal) ? 0 : 1;
+  ra.l2 = reduced ? 0 : 1;
   ra.partials = dots_part_.get();
   ra.colpart = colpart_.get();
   ra.sse_part = loss_part_.get();
-  ra.nsse = nloss;
+  ra.nsse = empty ? 0 : nloss;
   ra.inv_scale = inv_scale;
   ra.scal = scal;
   ra.abort = ctx_->abort;
@@ -561,8 +581,8 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       g.goff -= nfold;
     }
     g.stride = g.count;
-    if (side_reduced(l, fused, nloss)) {
-      // finished by the side blocks of the next dW launch: as written
+    if (empty || side_reduced(l, fused, nloss)) {
+      // zero-filled (an empty share) / finished by the side blocks of the next dW launch: as written
     } else if (L.splits > 1) {
       g.slab = slab_.get() + L.slab_off;
       g.splits = L.splits;
@@ -584,25 +604,28 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     ra.ncg += ncols;
   }
   ra.nseg = nl;
-  bool tail_ok = tf != nullptr;
+  // this rank's gradient (no lambda w) and its SSE as an fp32 (hi, lo) pair: [G | hi | lo]
+  auto local_words = [&]() {
+    if (empty) return; // zero-filled at entry
+    RedAllArgs loc = ra;
+    loc.dots = 0;
+    ProfScope ps(ctx_, PK_SLAB, 0);
+    reduce_all(s, loc);
+    sse_pack(s, loss_part_.get(), nloss, G + nparams_, ctx_->abort);
+  };
+  bool tail_ok = tf != nullptr && !local;
   for (int l = 0; l < nl && tail_ok; ++l) tail_ok = ra.seg[l].parts == 1;
   if (tail_ok) {
     // fused optimizer tail (tail.hip); data parallel: local reduce -> all-reduce -> tail over G
     TailArgs ta;
     const float *hilo = nullptr;
-    if (ctx_->dp()) {
-      RedAllArgs loc = ra;
-      loc.dots = 0;
-      {
-        ProfScope ps(ctx_, PK_SLAB, 0);
-        reduce_all(s, loc);
-        sse_pack(s, loss_part_.get(), nloss, G + nparams_, ctx_->abort);
-      }
-      {
+    if (reduced) {
+      local_words();
+      if (ctx_->dp()) {
         ProfScope ps(ctx_, PK_ALLREDUCE);
         ctx_->allreduce(G, nparams_ + 2);
       }
-      hilo = G + nparams_;
+      hilo = hilo_in ? hilo_in : G + nparams_;
       for (int l = 0; l < nl; ++l) {
         ra.seg[l].slab = nullptr;
         ra.seg[l].splits = 0;
@@ -647,33 +670,34 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     rows_ += B;
     return;
   }
-  {
+  ++evals_;
+  rows_ += B;
+  if (!reduced) {
     ProfScope ps(ctx_, PK_SLAB, 0);
     reduce_all(s, ra);
-  }
-  if (!ctx_->dp()) {
-    ++evals_;
-    rows_ += B;
     return;
   }
-  const float *hilo = nullptr;
+  local_words();
+  if (local) return; // the caller all-reduces [G | hi | lo] (with other blocks) and calls finish_reduced
   if (ctx_->dp()) {
-    {
-      ProfScope ps(ctx_, PK_FINAL, 0);
-      sse_pack(s, loss_part_.get(), nloss, G + nparams_, ctx_->abort);
-    }
     ProfScope ps(ctx_, PK_ALLREDUCE);
     ctx_->allreduce(G, nparams_ + 2); // one RCCL all-reduce of [grad | sse_hi | sse_lo]
-    hilo = G + nparams_;
   }
-  {
-    ProfScope ps(ctx_, PK_FINAL, 1);
-    const int nd = dots_partials_wg(nparams_);
-    finalize_grad_dots(s, nparams_, G, P, lambda, pdir, dots_part_.get(), ctx_->abort);
-    if (scal) eval_tail(s, dots_part_.get(), nd, loss_part_.get(), nloss, hilo, inv_scale, lambda, scal, ctx_->abort);
-  }
-  ++evals_;
-    rows_ += B;
+  finish_reduced(P, G, inv_scale, lambda, pdir, scal, hilo_in);
+}
+
+// The gradient and status of an all-reduced [G | hi | lo] block: G += lambda w, the dots of the status
+// block, and the loss from the (hi, lo) words (or from hilo_in: a loss-only trial's reduced words).
+void Mlp::finish_reduced(const float *P, float *G, double inv_scale, double lambda, const float *pdir, double *scal,
+                         const float *hilo_in) {
+  hipStream_t s = ctx_->stream;
+  ProfScope ps(ctx_, PK_FINAL, 1);
+  const int nd = dots_partials_wg(nparams_);
+  dots_part_.ensure(size_t(nd) * 3);
+  finalize_grad_dots(s, nparams_, G, P, lambda, pdir, dots_part_.get(), ctx_->abort);
+  if (scal)
+    eval_tail(s, dots_part_.get(), nd, loss_part_.get(), 0, hilo_in ? hilo_in : G + nparams_, inv_scale, lambda, scal,
+              ctx_->abort);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -3,9 +3,8 @@
 #pragma once
 
 #include "internal.hpp"
+#include "comm.hpp"
 #include "kernels.hpp"
-
-#include <rccl/rccl.h>
 
 #include <memory>
 #include <vector>
@@ -42,7 +41,7 @@ struct Ctx {
   Profiler prof;
   hipStream_t stream = nullptr;
   bool own_stream = false;
-  ncclComm_t comm = nullptr;
+  std::unique_ptr<Comm> comm; // RCCL (lbf_comm_init) or an in-process rank group (lbf_comm_init_local)
   int rank = 0, nranks = 1;
   const int *abort = nullptr; // set by a solver while it runs speculatively (see LbfgsSolver)
   // scratch for the BLAS-1 ABI helpers
@@ -118,7 +117,16 @@ public:
                  double *scal);
   void grad_after_loss(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
                        double lambda, const float *pdir, double *scal);
+  // Packed data-parallel evaluation in two halves: loss_grad_local stops before the all-reduce, leaving
+  // this rank's gradient (no lambda w) and its SSE as fp32 (hi, lo) words in G[0 .. n+2); the caller
+  // all-reduces one or more such blocks in a single collective and then finishes each with
+  // finish_reduced (+ lambda w, status block). Together bitwise equal to loss_grad on the same rank.
+  void loss_grad_local(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
+                       double inv_scale);
+  void finish_reduced(const float *P, float *G, double inv_scale, double lambda, const float *pdir, double *scal,
+                      const float *hilo_in = nullptr);
   long long loss_only_evals() const { return loss_only_; }
+  long long grad_after_loss_evals() const { return gal_; } // backward phases run after a loss_only
   // Exact Hessian-vector product Hv = H(P) V of the same batch loss (+ lambda V), Pearlmutter's
   // R-operator (hvp.hip); with a communicator the shards' products are all-reduced. Hv: nparams().
   void hvp(const float *P, const float *V, const float *X, const float *Y, const int *idx, long long B,
@@ -133,14 +141,15 @@ public:
 private:
   void forward_phase(const float *P, const float *X, const float *Y, const int *idx, long long B, double inv_scale);
   void backward_phase(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
-                      double lambda, const float *pdir, double *scal, const TailFuse *tf);
+                      double lambda, const float *pdir, double *scal, const TailFuse *tf, bool local,
+                      const float *hilo_in);
   struct FwdState {
     long long B = -1;
     bool fused = false;
     int fold = -1, nloss = 0, lstart = 0;
   } fs_;
   DevBuf<float> hilo_;
-  long long loss_only_ = 0;
+  long long loss_only_ = 0, gal_ = 0;
   void ensure(long long B);
   bool side_reduced(int l, bool fused, int nloss) const;
   GemmDesc fwd_desc(size_t l, const float *P, const float *in, const int *idx, long long B) const;

@@ -97,6 +97,7 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
   evals0_ = obj_->evals();
   rows0_ = obj_->rows();
   lonly0_ = obj_->loss_only_evals();
+  gal0_ = obj_->grad_after_loss_evals();
   // initial evaluation (lbfgs.hpp:44 / lbfgs.cuh:147)
   eval(x_, g_, nullptr);
   read_status();
@@ -515,10 +516,12 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
 
 void LbfgsSolver::info(lbf_solve_info *out) const {
   if (!out) return;
+  std::memset(out, 0, sizeof(*out));
   out->iterations = iter_;
   out->n_evals = obj_->evals() - evals0_;
   out->n_rows = obj_->rows() - rows0_;
   out->n_loss_only = obj_->loss_only_evals() - lonly0_;
+  out->n_grad_after_loss = obj_->grad_after_loss_evals() - gal0_;
   out->final_loss = loss_;
   out->final_grad_norm = std::sqrt(gg_);
 }
@@ -554,15 +557,17 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
   wp_.resize(nv);
   wm_.resize(nv);
   mu_.resize(ng);
-  g1_.resize(ng);
-  g2_.resize(ng);
-  gp_.resize(ng);
-  gm_.resize(ng);
+  ng_ = (long long)ng;
+  // zeroed once: the pads between the two halves of a block are summed by the all-reduce too
+  for (auto *b : {&gpair_[0], &gpair_[1], &fdpair_}) {
+    b->resize(2 * ng);
+    LBF_HIP(hipMemsetAsync(b->get(), 0, 2 * ng * sizeof(float), ctx_->stream));
+  }
   wh_.resize(nv * size_t(prm.L + 1));
   hs_.ensure(SC_N);
   evals0_ = net->evals();
   rows0_ = net->rows();
-  if (!ctx_->dp() && env_int("LBF_SLBFGS_TWIN", 1)) {
+  if (env_int("LBF_SLBFGS_TWIN", 1)) {
     tctx_.reset(new Ctx());
     tctx_->device = ctx_->device;
     tctx_->cus = ctx_->cus;
@@ -578,14 +583,12 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
     }
     dims.push_back(net->layers().back().out);
     tnet_.reset(new Mlp(tctx_.get(), int(acts.size()), dims.data(), acts.data()));
-    tscal_.resize(SC_N);
     LBF_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     LBF_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     for (int i = 0; i < 2; ++i) {
       LBF_HIP(hipEventCreateWithFlags(&ev_g2_[i], hipEventDisableTiming));
       LBF_HIP(hipEventCreateWithFlags(&ev_free_[i], hipEventDisableTiming));
     }
-    g2b_.resize(ng);
   }
 }
 
@@ -598,30 +601,40 @@ SlbfgsSolver::~SlbfgsSolver() {
   }
 }
 
-void SlbfgsSolver::eval_pair(const float *wa, float *ga, const float *wb, float *gb, long long off,
-                             long long count, double inv_scale) {
+void SlbfgsSolver::reduce_pair(const float *wa, const float *wb, float *gab, double inv_scale) {
+  {
+    ProfScope ps(ctx_, PK_ALLREDUCE);
+    ctx_->allreduce(gab, size_t(2 * ng_)); // [ga | hi | lo | pad | gb | hi | lo | pad]
+  }
+  net_->finish_reduced(wa, gab, inv_scale, prm_.lambda, nullptr, nullptr);
+  net_->finish_reduced(wb, gab + ng_, inv_scale, prm_.lambda, nullptr, nullptr);
+}
+
+void SlbfgsSolver::eval_pair(const float *wa, const float *wb, float *gab, long long off, long long count,
+                             double inv_scale) {
   // the step's rows were gathered for the whole epoch (contiguous slices, same values in the same order
   // as the gathering GEMMs would read), which also lets the dW GEMM of layer 0 take the LDS-DMA path
   const int In = net_->layers().front().in, Out = net_->layers().back().out;
   const float *X = xg_.get() + off * In, *Y = yg_.get() + off * Out;
-  const int *idx = nullptr;
+  float *ga = gab, *gb = gab + ng_;
+  const bool dp = ctx_->dp();
   // gradients only: nobody reads a minibatch evaluation's loss or dots (scal = nullptr skips them)
+  auto one = [&](Mlp *m, const float *w, float *g) {
+    if (dp) m->loss_grad_local(w, g, X, Y, nullptr, count, inv_scale);
+    else m->loss_grad(w, g, X, Y, nullptr, count, inv_scale, prm_.lambda, nullptr, nullptr);
+  };
   if (!tnet_) {
-    net_->loss_grad(wa, ga, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, nullptr);
-    net_->loss_grad(wb, gb, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, nullptr);
-    return;
+    one(net_, wa, ga);
+    one(net_, wb, gb);
+  } else {
+    LBF_HIP(hipEventRecord(ev_fork_, ctx_->stream)); // wa, wb, the gathered rows and gb's last reader are done
+    LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
+    one(tnet_.get(), wb, gb);
+    one(net_, wa, ga);
+    LBF_HIP(hipEventRecord(ev_join_, tctx_->stream));
+    LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_join_, 0));
   }
-  LBF_HIP(hipEventRecord(ev_fork_, ctx_->stream)); // wa, wb, the gathered rows and gb's last reader are done
-  LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
-  tnet_->loss_grad(wb, gb, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, nullptr);
-  net_->loss_grad(wa, ga, X, Y, idx, count, inv_scale, prm_.lambda, nullptr, nullptr);
-  LBF_HIP(hipEventRecord(ev_join_, tctx_->stream));
-  LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_join_, 0));
-}
-
-void SlbfgsSolver::eval_batch(const float *w, float *g, const int *d_idx, long long count, const float *pdir) {
-  (void)pdir;
-  net_->loss_grad(w, g, X_, Y_, d_idx, count, 1.0, prm_.lambda, nullptr, hist_.scal());
+  if (dp) reduce_pair(wa, wb, gab, inv_scale);
 }
 
 // SLBFGS::stochastic_solve (s_lbfgs.hpp:165-290) with the UnifiedSLBFGS_CPU closures
@@ -652,28 +665,36 @@ int SlbfgsSolver::run(lbf_record *rec) {
   bool have_u = false, mu_valid = false;
   // An epoch's index lists: every minibatch, the Hessian batches (only once a u exists), then the anchor
   // pick, in the reference's RNG order (s_lbfgs.hpp:212-266). No draw depends on device values, so the next
-  // epoch's lists are drawn on the host while the GPU runs the current epoch.
+  // epoch's lists are drawn on the host while the GPU runs the current epoch. Every rank draws the same
+  // lists and keeps only its slice [b*rk/nr, b*(rk+1)/nr) of each batch: `flat` holds those slices.
+  struct Slice {
+    long long off = 0, cnt = 0, total = 0; // offset / count in this rank's flat list, whole batch size
+  };
   struct EpochDraw {
-    std::vector<int> flat;
-    std::vector<std::pair<long long, long long>> mb, hb;
+    std::vector<int> flat, batch;
+    std::vector<Slice> mb, hb;
     int pick = -1;
     bool u_seen = false; // have_u after the epoch
   };
   MinibatchSampler sampler{size_t(N_)};
   auto draw_epoch = [&](bool u_seen, EpochDraw &d) {
     d.flat.clear();
-    d.mb.assign(size_t(m_inner), {0, 0});
-    d.hb.assign(size_t(m_inner), {-1, 0});
+    d.mb.assign(size_t(m_inner), Slice{});
+    d.hb.assign(size_t(m_inner), Slice{-1, 0, 0});
+    auto take = [&](size_t bsz) {
+      d.batch.clear();
+      const long long tot = (long long)sampler.draw(bsz, rng, d.batch);
+      const long long a0 = tot * rk / nr, a1 = tot * (rk + 1) / nr;
+      Slice sl{(long long)d.flat.size(), a1 - a0, tot};
+      d.flat.insert(d.flat.end(), d.batch.begin() + a0, d.batch.begin() + a1);
+      return sl;
+    };
     int whist_size = 1;
     for (int t = 0; t < m_inner; ++t) {
-      const long long o = (long long)d.flat.size();
-      d.mb[t] = {o, (long long)sampler.draw(size_t(prm_.b), rng, d.flat)};
+      d.mb[t] = take(size_t(prm_.b));
       whist_size = std::min(whist_size + 1, L + 1);
       if (t > 0 && t % L == 0) {
-        if (u_seen) {
-          const long long oh = (long long)d.flat.size();
-          d.hb[t] = {oh, (long long)sampler.draw(size_t(prm_.b_H), rng, d.flat)};
-        }
+        if (u_seen) d.hb[t] = take(size_t(prm_.b_H));
         u_seen = true;
       }
     }
@@ -689,6 +710,7 @@ int SlbfgsSolver::run(lbf_record *rec) {
   const auto t0 = std::chrono::steady_clock::now();
   int rec_i = rec ? rec->size : 0;
   iters_ = 0;
+  const bool dp = ctx_->dp();
   while (iters_ < prm_.max_epochs) {
     if (!mu_valid) {
       eval_full(w_.get(), mu_.get());
@@ -705,8 +727,8 @@ int SlbfgsSolver::run(lbf_record *rec) {
     idx_.ensure(std::max<size_t>(1, flat.size()));
     if (!flat.empty())
       LBF_HIP(hipMemcpyAsync(idx_.get(), flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
-    // every sampled row of the epoch gathered once, in sampling order: step t's minibatch (and its
-    // Hessian batch) is then a contiguous slice (batch_g's column gather, unified_optimization.hpp:361-364)
+    // this rank's sampled rows of the epoch gathered once, in sampling order: step t's minibatch slice (and
+    // its Hessian batch slice) is then contiguous (batch_g's column gather, unified_optimization.hpp:361-364)
     xg_.ensure(std::max<size_t>(1, flat.size()) * size_t(In));
     yg_.ensure(std::max<size_t>(1, flat.size()) * size_t(Out));
     gather_rows(s, X_, In, idx_.get(), (long long)flat.size(), int(In), xg_.get());
@@ -733,40 +755,51 @@ int SlbfgsSolver::run(lbf_record *rec) {
                              s));
     }
     // With the twin stream, the minibatch gradients at the anchor w (fixed for the epoch, and independent
-    // of the iterates) run one step ahead on it, double-buffered: step t's evaluation at w_t and its
-    // direction on the context stream then overlap the twin's gradient of minibatch t + 1 at w, instead of
-    // joining the two evaluations of each step. Same evaluations on the same inputs: bitwise the same.
-    float *g2buf[2] = {g2_.get(), tnet_ ? g2b_.get() : g2_.get()};
-    auto anchor_ahead = [&](int t) { // twin stream: gb of step t into g2buf[t & 1]
-      const long long b = mb[t].second;
-      const long long o = mb[t].first + b * rk / nr, c = b * (rk + 1) / nr - b * rk / nr;
+    // of the iterates) run one step ahead on it, double-buffered in the second half of gpair_[t & 1]: step
+    // t's evaluation at w_t and its direction on the context stream then overlap the twin's gradient of
+    // minibatch t + 1 at w, instead of joining the two evaluations of each step. Same evaluations on the
+    // same inputs: bitwise the same. Data parallel: both halves are this rank's partial sums until the
+    // step's one all-reduce of the whole block.
+    auto g1 = [&](int t) { return gpair_[t & 1].get(); };
+    auto g2 = [&](int t) { return gpair_[t & 1].get() + ng_; };
+    auto rows_x = [&](const Slice &sl) { return xg_.get() + sl.off * In; };
+    auto rows_y = [&](const Slice &sl) { return yg_.get() + sl.off * Out; };
+    auto anchor_ahead = [&](int t) { // twin stream: the anchor half of step t's block
+      const Slice &sl = mb[t];
       LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_free_[t & 1], 0)); // step t - 2's direction read it
-      tnet_->loss_grad(w_.get(), g2buf[t & 1], xg_.get() + o * In, yg_.get() + o * Out, nullptr, c, 1.0 / double(b),
-                       prm_.lambda, nullptr, nullptr);
+      if (dp)
+        tnet_->loss_grad_local(w_.get(), g2(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, 1.0 / double(sl.total));
+      else
+        tnet_->loss_grad(w_.get(), g2(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, 1.0 / double(sl.total),
+                         prm_.lambda, nullptr, nullptr);
       LBF_HIP(hipEventRecord(ev_g2_[t & 1], tctx_->stream));
     };
     // the epoch's gathered rows and w are complete (the context stream was synchronised above)
     if (tnet_) anchor_ahead(0);
     for (int t = 0; t < m_inner; ++t) {
-      const long long b = mb[t].second;
-      const long long o = mb[t].first + b * rk / nr, c = b * (rk + 1) / nr - b * rk / nr;
+      const Slice &sl = mb[t];
+      const double inv_b = 1.0 / double(sl.total);
       if (tnet_) {
         if (t + 1 < m_inner) anchor_ahead(t + 1);
-        net_->loss_grad(wt_.get(), g1_.get(), xg_.get() + o * In, yg_.get() + o * Out, nullptr, c, 1.0 / double(b),
-                        prm_.lambda, nullptr, nullptr);
+        if (dp)
+          net_->loss_grad_local(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b);
+        else
+          net_->loss_grad(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda, nullptr,
+                          nullptr);
         LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_g2_[t & 1], 0));
+        if (dp) reduce_pair(wt_.get(), w_.get(), g1(t), inv_b);
       } else {
-        eval_pair(wt_.get(), g1_.get(), w_.get(), g2_.get(), o, c, 1.0 / double(b));
+        eval_pair(wt_.get(), w_.get(), g1(t), sl.off, sl.cnt, inv_b);
       }
       GramArgs ga;
       ga.policy = POL_SLBFGS;
       ga.has_g = 1;
-      ga.ga = g1_.get();
-      ga.gb = g2buf[t & 1];
+      ga.ga = g1(t);
+      ga.gb = g2(t);
       ga.gc = mu_.get();
       ga.g_out = v_.get();
       hist_.update(ga, 1, 1, +1.0);
-      if (tnet_) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // g2buf[t & 1] read (v formed)
+      if (tnet_) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
       const int slot = wh_push_slot();
       // wt = wt - step * r ; w_history.push_back(wt)
       hist_.combine(v_.get(), nullptr, wt_.get(), wt_.get(), wh_.get() + slot * ld, false, -prm_.step);
@@ -775,8 +808,7 @@ int SlbfgsSolver::run(lbf_record *rec) {
         for (int i = 0; i < wh_count; ++i) slots[i] = wh_slot(i);
         average_slots(s, n_, wh_.get(), ld, slots, wh_count, u_.get());
         if (have_u) {
-          const long long hbn = hb[t].second;
-          const long long ho = hb[t].first + hbn * rk / nr, hc = hbn * (rk + 1) / nr - hbn * rk / nr;
+          const Slice &hs = hb[t];
           const double eps = prm_.fd_eps;
           lincomb(s, n_, u_.get(), -1.0, up_.get(), s_.get()); // s = u - u_prev
           GramArgs pa;
@@ -784,18 +816,20 @@ int SlbfgsSolver::run(lbf_record *rec) {
           pa.has_pair = 1;
           pa.sa = u_.get();
           pa.sb = up_.get();
+          float *gp = fdpair_.get(), *gm = fdpair_.get() + ng_;
           if (prm_.hvp_exact) { // y = H(u) s on the b_H batch, R-operator (hvp.hip)
-            net_->hvp(u_.get(), s_.get(), X_, Y_, idx_.get() + ho, hc, 1.0 / double(hbn), prm_.lambda, gp_.get());
-            LBF_HIP(hipMemsetAsync(gm_.get(), 0, size_t(n_) * sizeof(float), s));
+            net_->hvp(u_.get(), s_.get(), X_, Y_, idx_.get() + hs.off, hs.cnt, 1.0 / double(hs.total), prm_.lambda,
+                      gp);
+            LBF_HIP(hipMemsetAsync(gm, 0, size_t(n_) * sizeof(float), s));
             pa.yscale = 1.0;
           } else { // s_lbfgs.hpp:88-101: central difference of two batch gradients
             lincomb(s, n_, u_.get(), eps, s_.get(), wp_.get()); // fd_hvp_grads, the two evaluations paired
             lincomb(s, n_, u_.get(), -eps, s_.get(), wm_.get());
-            eval_pair(wp_.get(), gp_.get(), wm_.get(), gm_.get(), ho, hc, 1.0 / double(hbn));
+            eval_pair(wp_.get(), wm_.get(), fdpair_.get(), hs.off, hs.cnt, 1.0 / double(hs.total));
             pa.yscale = 1.0 / (2.0 * eps);
           }
-          pa.ya = gp_.get();
-          pa.yb = gm_.get();
+          pa.ya = gp;
+          pa.yb = gm;
           hist_.update(pa, 0, 1, +1.0);
         }
         LBF_HIP(hipMemcpyAsync(up_.get(), u_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -839,6 +873,7 @@ int SlbfgsSolver::run(lbf_record *rec) {
 
 void SlbfgsSolver::info(lbf_solve_info *out) const {
   if (!out) return;
+  std::memset(out, 0, sizeof(*out));
   out->iterations = iters_;
   out->n_evals = net_->evals() - evals0_ + (tnet_ ? tnet_->evals() : 0);
   out->n_rows = net_->rows() - rows0_ + (tnet_ ? tnet_->rows() : 0);
@@ -895,6 +930,7 @@ int run_gd(Mlp *net, const lbf_gd_params &prm, float *d_params, const float *X, 
     ++done;
   }
   if (info) {
+    std::memset(info, 0, sizeof(*info));
     info->iterations = done;
     info->n_evals = net->evals() - evals0;
     info->n_rows = net->rows() - rows0;
@@ -966,6 +1002,7 @@ int run_sgd(Mlp *net, const lbf_sgd_params &prm, float *d_params, const float *X
     ++done;
   }
   if (info) {
+    std::memset(info, 0, sizeof(*info));
     info->iterations = done;
     info->n_evals = net->evals() - evals0;
     info->n_rows = net->rows() - rows0;

@@ -29,6 +29,7 @@ struct Objective {
   virtual void eval_loss(const float *, double *) {}
   virtual void eval_grad_after_loss(const float *, float *, const float *, double *) {}
   virtual long long loss_only_evals() const { return 0; }
+  virtual long long grad_after_loss_evals() const { return 0; }
   // Evaluation followed by the fused optimizer tail (tail.hip); only when fused_tail() is true.
   virtual bool fused_tail() const { return false; }
   virtual void eval_fused(const float *, float *, const float *, double *, const TailFuse &) {}
@@ -58,6 +59,7 @@ struct MlpObjective : Objective {
     net->grad_after_loss(x, g, X, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal);
   }
   long long loss_only_evals() const override { return net->loss_only_evals(); }
+  long long grad_after_loss_evals() const override { return net->grad_after_loss_evals(); }
   bool fused_tail() const override { return true; }
   void eval_fused(const float *x, float *g, const float *pdir, double *scal, const TailFuse &tf) override {
     net->loss_grad(x, g, X, Y, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal, &tf);
@@ -155,7 +157,7 @@ private:
   int iter_ = 0;
   bool pending_pair_ = false, pending_reset_ = false, converged_ = false;
   int rec_idx_ = 0;
-  long long evals0_ = 0, rows0_ = 0, lonly0_ = 0; // the objective's counters when this solve began
+  long long evals0_ = 0, rows0_ = 0, lonly0_ = 0, gal0_ = 0; // the objective's counters when this solve began
   std::chrono::steady_clock::time_point t0_;
 };
 
@@ -168,11 +170,13 @@ public:
   void info(lbf_solve_info *out) const;
 
 private:
-  void eval_batch(const float *w, float *g, const int *d_idx, long long count, const float *pdir);
-  // Two independent batch gradients of one step (minibatch at w_t and at the anchor w; the FD pair at
-  // u +- eps s): the second on the twin's stream when there is one, joined before the next launch.
-  void eval_pair(const float *wa, float *ga, const float *wb, float *gb, long long off, long long count,
-                 double inv_scale); // rows off .. off+count-1 of the epoch's gathered block
+  // Two independent batch gradients of one step (the FD pair at u +- eps s) into one [ga | gb] block
+  // (gb = gab + ng_): the second on the twin's stream when there is one, joined before the next launch.
+  // Data parallel: both evaluations stop before the all-reduce and ONE collective sums the block.
+  void eval_pair(const float *wa, const float *wb, float *gab, long long off, long long count,
+                 double inv_scale); // rows off .. off+count-1 of this rank's gathered block
+  // Data parallel: all-reduce a [ga | gb] block once, then finish both gradients (+ lambda w).
+  void reduce_pair(const float *wa, const float *wb, float *gab, double inv_scale);
   Mlp *net_;
   Ctx *ctx_;
   lbf_slbfgs_params prm_;
@@ -180,19 +184,24 @@ private:
   const float *X_, *Y_;
   long long N_, n_;
   History hist_;
-  DevBuf<float> w_, wt_, mu_, g1_, g2_, g2b_, v_, r_, u_, up_, s_, wp_, wm_, gp_, gm_, wh_;
+  DevBuf<float> w_, wt_, mu_, v_, r_, u_, up_, s_, wp_, wm_, wh_;
+  // [g(w_t) | g(w)] of an inner step, double-buffered (the twin fills the anchor half one step ahead),
+  // and [g(u + eps s) | g(u - eps s)] of a Hessian step: one all-reduce per block under data parallelism
+  DevBuf<float> gpair_[2], fdpair_;
+  long long ng_ = 0; // floats per gradient in a block (n + 2 loss words, rounded to 4)
   DevBuf<int> idx_;
   PinnedBuf<double> hs_;
   int iters_ = 0;
   double last_loss_ = 0, last_gnorm_ = 0;
   long long evals0_ = 0, rows0_ = 0; // the net's counters when this solve began
-  // Twin evaluator (single rank): a second workspace of the same network on its own stream, so the
-  // two latency-bound minibatch evaluations of a step run concurrently (results unchanged: each is
-  // the same launch sequence on its own buffers). Data parallel: off (one communicator, one order).
+  // Twin evaluator: a second workspace of the same network on its own stream, so the two latency-bound
+  // minibatch evaluations of a step run concurrently (results unchanged: each is the same launch
+  // sequence on its own buffers). Data parallel: the twin's evaluations stop before the all-reduce
+  // (it has no communicator) and the context stream's one collective per block sums both.
   std::unique_ptr<Ctx> tctx_;
   std::unique_ptr<Mlp> tnet_;
-  DevBuf<double> tscal_;
-  DevBuf<float> xg_, yg_; // the epoch's sampled rows, gathered once (all minibatches and Hessian batches)
+  // this rank's slices of the epoch's sampled rows, gathered once (all minibatches and Hessian batches)
+  DevBuf<float> xg_, yg_;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   hipEvent_t ev_g2_[2] = {nullptr, nullptr}, ev_free_[2] = {nullptr, nullptr}; // anchor gradients ahead (twin)
 };

@@ -642,11 +642,12 @@ void lincomb(hipStream_t s, long long n, const float *a, double c, const float *
 }
 
 // Minibatch rows gathered into a contiguous block (S-LBFGS: both evaluations of an inner step read the
-// same rows; batch_g's column gather, unified_optimization.hpp:361-364). 16-B lanes when cols % 4 == 0.
+// same rows; batch_g's column gather, unified_optimization.hpp:361-364). 16-B lanes when cols % 4 == 0,
+// ld % 4 == 0 and both base pointers are 16-B aligned (the caller's X may be any float pointer).
 __global__ __launch_bounds__(256) void gather_rows_kernel(const float *src, long long ld, const int *idx,
-                                                          long long count, int cols, float *dst) {
+                                                          long long count, int cols, int vec, float *dst) {
   const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if ((cols & 3) == 0 && (ld & 3) == 0) {
+  if (vec) {
     const int c4 = cols >> 2;
     if (q >= count * c4) return;
     const long long r = q / c4, c = (q - r * c4) * 4;
@@ -660,9 +661,39 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float *src, long
 void gather_rows(hipStream_t s, const float *src, long long ld, const int *idx, long long count, int cols,
                  float *dst) {
   if (count <= 0) return;
-  const long long per = (cols & 3) == 0 && (ld & 3) == 0 ? cols / 4 : cols;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+  const int vec = (cols & 3) == 0 && (ld & 3) == 0 && aligned ? 1 : 0;
+  const long long per = vec ? cols / 4 : cols;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(unsigned(cdiv(count * per, 256))), dim3(256), 0, s, src, ld, idx, count,
-                     cols, dst);
+                     cols, vec, dst);
+  LBF_KERNEL_CHECK();
+}
+
+// x[0 .. n) = 0 unless the speculative chain was aborted (a data-parallel rank's empty share)
+__global__ __launch_bounds__(256) void zero_fill_kernel(long long n, float *x, const int *abort) {
+  if (abort && *abort) return;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) x[e] = 0.0f;
+}
+void zero_fill(hipStream_t s, long long n, float *x, const int *abort) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(zero_fill_kernel, dim3(unsigned(cdiv(n, 256))), dim3(256), 0, s, n, x, abort);
+  LBF_KERNEL_CHECK();
+}
+
+// In-process rank group (comm.cpp LocalComm): dst = src[0] + src[1] + ... in rank order, fp32, so
+// every rank of the group computes the same bits.
+__global__ __launch_bounds__(256) void sum_ranks_kernel(RankSrcs r, long long count, float *dst) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  float acc = r.p[0][e];
+  for (int i = 1; i < r.n; ++i) acc += r.p[i][e];
+  dst[e] = acc;
+}
+void sum_ranks(hipStream_t s, const RankSrcs &r, long long count, float *dst) {
+  LBF_REQUIRE(r.n >= 1 && r.n <= kMaxLocalRanks, "sum_ranks: 1..16 ranks");
+  if (count <= 0) return;
+  hipLaunchKernelGGL(sum_ranks_kernel, dim3(unsigned(cdiv(count, 256))), dim3(256), 0, s, r, count, dst);
   LBF_KERNEL_CHECK();
 }
 

@@ -44,6 +44,15 @@ class Context:
         check(lib().lbf_comm_init(self.h, world, rank, uid), "lbf_comm_init")
         self.rank, self.world = rank, world
 
+    @staticmethod
+    def comm_init_local(ctxs: Sequence["Context"]):
+        """In-process rank group (lbf_comm_init_local): ctxs[r] becomes rank r. The contexts share one device
+        and each must then be driven by its own thread with the same call sequence."""
+        arr = (C.c_void_p * len(ctxs))(*[c.h.value for c in ctxs])
+        check(lib().lbf_comm_init_local(arr, len(ctxs)), "lbf_comm_init_local")
+        for r, c in enumerate(ctxs):
+            c.rank, c.world = r, len(ctxs)
+
     def allreduce_(self, t: torch.Tensor):
         check(lib().lbf_allreduce_sum(self.h, ptr(t), t.numel()), "lbf_allreduce_sum")
         return t

@@ -26,6 +26,15 @@ __global__ void onesum_k(const double *p, long long n, double *out) {
   }
 }
 
+// one link of a dependent chain: every block reads the value the previous launch wrote and writes
+// its successor (a true data dependency, as between the kernels of an evaluation)
+__global__ void chain_k(double *p, int nb) {
+  const double v = p[0];
+  __syncthreads();
+  if (threadIdx.x == 0) p[1 + blockIdx.x % 64] = v + 1.0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) p[0] = v + 1.0;
+}
+
 int main() {
   double *buf, *out;
   const long long N = 1 << 22;
@@ -70,5 +79,37 @@ int main() {
     hipLaunchKernelGGL(write_k, (unsigned)(N / 256), 256, 0, s, buf, N);
     hipLaunchKernelGGL(onesum_k, 1, 1024, 0, s, buf, 8192LL, out);
   });
+  // dependent chains of 10 launches at several grid sizes: eager, and the same chain as one hipGraph
+  for (int nb : {1, 16, 64, 256, 1024}) {
+    char nm[128];
+    snprintf(nm, sizeof nm, "chain of 10 x chain_k<<<%d,256>>> (eager), per launch", nb);
+    auto body = [&] {
+      for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(chain_k, nb, 256, 0, s, buf, nb);
+    };
+    for (int i = 0; i < 20; ++i) body();
+    hipEventRecord(a, s);
+    for (int i = 0; i < R; ++i) body();
+    hipEventRecord(b, s);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    printf("%-58s %8.2f us\n", nm, ms * 1e3f / (R * 10));
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+    body();
+    CK(hipStreamEndCapture(s, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    for (int i = 0; i < 20; ++i) CK(hipGraphLaunch(ge, s));
+    hipEventRecord(a, s);
+    for (int i = 0; i < R; ++i) CK(hipGraphLaunch(ge, s));
+    hipEventRecord(b, s);
+    hipEventSynchronize(b);
+    hipEventElapsedTime(&ms, a, b);
+    snprintf(nm, sizeof nm, "chain of 10 x chain_k<<<%d,256>>> (hipGraph), per launch", nb);
+    printf("%-58s %8.2f us\n", nm, ms * 1e3f / (R * 10));
+    CK(hipGraphExecDestroy(ge));
+    CK(hipGraphDestroy(g));
+  }
   return 0;
 }

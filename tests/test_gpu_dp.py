@@ -102,3 +102,25 @@ def test_dp_slbfgs_equals_single(ctx, dp_ctx, pkg):
     assert np.array_equal(h1["accepted"], hd["accepted"])
     assert np.allclose(h1["loss"], hd["loss"], rtol=1e-9, atol=0)
     assert np.linalg.norm(P1 - Pd) <= 1e-6 * np.linalg.norm(P1)
+
+
+def test_dp_slbfgs_cfg4_bitwise(ctx, dp_ctx, pkg):
+    """BASELINE cfg 4's shape (784-512-256-10, b = 256, b_H = 128, L = M = 10) for one epoch over 12800 rows:
+    the data-parallel route (both minibatch gradients of a step in one [g(w_t) | g(w)] all-reduce, the
+    twin's anchor gradients one step ahead, the FD pair in one [g(u+eps s) | g(u-eps s)] all-reduce) against
+    the single route: the same parameters bit for bit (s_lbfgs.hpp:218-262)."""
+    dims, acts = [784, 512, 256, 10], ["relu", "relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(12800)
+    X, Y = dev(Xh), dev(Yh)
+    kw = dict(M=10, L=10, b=256, b_H=128, step=0.005, max_epochs=1, tol=0.0, lam=1e-4)
+    out = []
+    for c in (ctx, dp_ctx):
+        net = pkg.Mlp(c, dims, acts)
+        P = net.init_params(123, "cpu")
+        hist, info = pkg.slbfgs_solve(net, P, X, Y, **kw)
+        out.append((hist, P, info))
+    (h1, P1, i1), (hd, Pd, idd) = out
+    assert torch.equal(P1, Pd)
+    assert np.array_equal(h1["accepted"], hd["accepted"])
+    assert i1.n_evals == idd.n_evals and i1.n_rows == idd.n_rows
+    assert abs(h1["loss"][0] - hd["loss"][0]) <= 1e-12 * abs(h1["loss"][0])

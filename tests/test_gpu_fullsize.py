@@ -23,6 +23,9 @@ N_FULL = 60000
 CFG2 = ([784, 128, 10], ["relu", "linear"])
 CFG3 = ([784, 128, 64, 10], ["relu", "relu", "linear"])
 CFG4 = ([784, 512, 256, 10], ["relu", "relu", "linear"])
+# the reference's only deep GPU workload: tests/fashion-mnist/main_gpu_deep.cpp:14-17 (784-256-128-64-10,
+# ReLU x 3, Linear; L-BFGS m = 100 and m = 10 on N = 60000, :78, :92; CUDA route and init)
+DEEP = ([784, 256, 128, 64, 10], ["relu", "relu", "relu", "linear"])
 
 
 def dev(a):
@@ -55,7 +58,7 @@ def test_cfg2_loss_grad_full_size(ctx, pkg, O, mnist):
     assert rel(host(g), g_ref) <= 1e-4
 
 
-@pytest.mark.parametrize("dims,acts,m", [(*CFG2, 10), (*CFG3, 20)], ids=["cfg2_m10", "cfg3_m20"])
+@pytest.mark.parametrize("dims,acts,m", [(*CFG2, 10), (*CFG3, 20), (*DEEP, 10)], ids=["cfg2_m10", "cfg3_m20", "deep_m10"])
 def test_wolfe_first10_full_size(ctx, pkg, O, mnist, dims, acts, m):
     """The headline trajectory: 10 L-BFGS iterations (CPU semantics) over all 60000 rows."""
     _, _, X64, Y64, X, Y = mnist
@@ -71,6 +74,40 @@ def test_wolfe_first10_full_size(ctx, pkg, O, mnist, dims, acts, m):
     assert np.array_equal(hist["accepted"][:9], rec[:9, 3].astype(int))
     g = np.abs(hist["grad_norm"][:5] - rec[:5, 1]) / np.abs(rec[:5, 1])
     assert g.max() <= 1e-3, g
+
+
+@pytest.mark.parametrize("init", ["cpu", "cuda"])
+def test_deep_loss_grad_full_size(ctx, pkg, O, mnist, init):
+    """784-256-128-64-10 at N = 60000: three hidden layers, a 256-wide first layer (two 128-wide column tiles
+    in the forward GEMM, no fused head on layer 0) and the fold on the 128 -> 64 layer's dW; both init streams
+    (network.hpp:45-71 and the zero-bias network.cuh:36-59 the reference's GPU drivers use)."""
+    _, _, X64, Y64, X, Y = mnist
+    dims, acts = DEEP
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, init)
+    loss, g = net.loss_grad(P, X, Y)
+    l_ref, g_ref = O.Net(dims, acts).loss_grad(host(P), X64, Y64)
+    assert abs(loss - l_ref) <= 1e-5 * abs(l_ref), (loss, l_ref)
+    assert rel(host(g), g_ref) <= 1e-4
+
+
+@pytest.mark.parametrize("m", [10, 100])
+def test_deep_armijo_first10_full_size(ctx, pkg, O, mnist, m):
+    """The deep config as the reference's GPU driver runs it (CudaLBFGS::solve, lbfgs.cuh:39-194: Armijo
+    backtracking with quadratic interpolation, fp32 host scalars; CUDA init stream), 10 iterations over all
+    60000 rows against the oracle's fp32 Armijo restatement: the same trial counts, losses within 1e-3."""
+    Xh, Yh, _, _, X, Y = mnist
+    dims, acts = DEEP
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cuda")
+    P0 = host(P)
+    hist, _ = pkg.lbfgs_solve(net, P, X, Y, line_search="armijo", m=m, max_iters=10, tol=0.0)
+    _, rec = O.Net(dims, acts).lbfgs_armijo(P0, Xh.astype(np.float64), Yh.astype(np.float64), m=m, max_iters=10,
+                                            fp32=True)
+    assert len(hist["loss"]) == 10 and len(rec) == 10
+    r = np.abs(hist["loss"] - rec[:, 0]) / np.abs(rec[:, 0])
+    assert r.max() <= 1e-3, r
+    assert np.array_equal(hist["ls_trials"], rec[:, 4].astype(int)), (hist["ls_trials"], rec[:, 4])
 
 
 @pytest.mark.parametrize("N,gather", [(20000, False), (40000, False), (40000, True)])

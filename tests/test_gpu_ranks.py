@@ -1,0 +1,280 @@
+"""The product's multi-rank path (nranks > 1) on ONE GPU, through an in-process rank group.
+
+RCCL refuses two ranks on one device, so `lbf_comm_init_local` (csrc/comm.cpp) makes 2-4 contexts on
+GPU 0 the ranks of one group: each rank is driven by its own host thread (as one process per GPU would
+drive it), evaluates its contiguous shard / minibatch slice, and the group's all-reduce sums every
+rank's [grad | sse_hi | sse_lo] buffer on the device in rank order. Everything the driver's 8-GPU run
+executes with nranks > 1 runs here: rank > 0 shard offsets, the n_global scaling, the S-LBFGS slices
+b*rk/nr .. b*(rk+1)/nr of every minibatch, Hessian batch and anchor, empty shares (b < world), the
+(hi, lo) loss words of different shards summed, and line-search decisions replicated on summed data.
+
+The reference has no collective; the split rests on the loss being a sum over samples
+(src/unified_optimization.hpp:101-120, src/cuda/network.cuh:105-107) and on S-LBFGS's batch_g
+(unified_optimization.hpp:343-400, s_lbfgs.hpp:218-262). Tolerances ("1-GPU vs 8-GPU:
+per-call rel <= 1e-5"): the shard sums are added in another order than one GPU's split-K slabs, so
+results agree to fp32 rounding, not bitwise; ranks of one group agree bitwise with each other.
+"""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
+
+
+def host(t):
+    return t.double().cpu().numpy()
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def run_ranks(pkg, world, body, timeout=240):
+    """body(rank, ctx) on `world` threads, each rank of one in-process group on GPU 0."""
+    ctxs = [pkg.Context(0, use_torch_stream=False) for _ in range(world)]
+    pkg.Context.comm_init_local(ctxs)
+    torch.cuda.synchronize()
+    out, err = [None] * world, [None] * world
+
+    def th(r):
+        try:
+            torch.cuda.set_device(0)
+            out[r] = body(r, ctxs[r])
+            torch.cuda.synchronize()
+        except BaseException as e:  # noqa: BLE001 (re-raised below)
+            err[r] = e
+
+    ts = [threading.Thread(target=th, args=(r,), daemon=True) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout)
+    assert not any(t.is_alive() for t in ts), "a rank thread did not finish"
+    for e in err:
+        if e is not None:
+            raise e
+    return out
+
+
+def shard(N, world, r):
+    return N * r // world, N * (r + 1) // world
+
+
+def test_local_group_allreduce(pkg):
+    """Rank-order device sum, identical on every rank; counts up to 16 ranks' worth of data."""
+    world = 3
+    base = [torch.randn(100003, device="cuda") for _ in range(world)]
+    bufs = [b.clone() for b in base]
+
+    def body(r, c):
+        c.allreduce_(bufs[r])
+        c.allreduce_(bufs[r])  # twice: the group's events and barrier are reused
+        return None
+
+    run_ranks(pkg, world, body)
+    s1 = (base[0] + base[1]) + base[2]
+    s2 = (s1 + s1) + s1
+    for r in range(world):
+        assert torch.equal(bufs[r], s2)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("dims,acts,N", [([784, 128, 10], ["relu", "linear"], 7501),
+                                         ([784, 128, 64, 10], ["relu", "relu", "linear"], 3000),
+                                         ([784, 300, 20], ["tanh", "linear"], 1001)])
+def test_ranks_loss_grad_equals_single(ctx, pkg, world, dims, acts, N):
+    Xh, Yh = pkg.synth_mnist(N, dims[0], dims[-1])
+    net1 = pkg.Mlp(ctx, dims, acts)
+    P = net1.init_params(123, "cpu")
+    l1, g1 = net1.loss_grad(P, dev(Xh), dev(Yh), inv_scale=1.0 / N)
+    shards = [shard(N, world, r) for r in range(world)]
+    Xs = [dev(Xh[lo:hi]) for lo, hi in shards]
+    Ys = [dev(Yh[lo:hi]) for lo, hi in shards]
+
+    def body(r, c):
+        net = pkg.Mlp(c, dims, acts)
+        return net.loss_grad(P, Xs[r], Ys[r], inv_scale=1.0 / N)
+
+    res = run_ranks(pkg, world, body)
+    for lr, gr in res:
+        assert lr == res[0][0] and torch.equal(gr, res[0][1])  # replicated, bitwise
+    assert abs(res[0][0] - l1) <= 1e-6 * abs(l1)
+    assert rel(host(res[0][1]), host(g1)) <= 1e-5
+
+
+def test_ranks_minibatch_slices_equal_single(ctx, pkg):
+    """S-LBFGS batch_g on a sampled minibatch: each rank evaluates its slice of the index list with the
+    whole batch's 1/b scale and lambda; the group sum equals the single evaluation of the whole list."""
+    dims, acts = [784, 512, 256, 10], ["relu", "relu", "linear"]
+    N, b, world = 60000, 256, 2
+    Xh, Yh = pkg.synth_mnist(N)
+    X, Y = dev(Xh), dev(Yh)
+    idx = torch.from_numpy(pkg.sample_indices(N, b, 123)[0].astype(np.int32)).cuda()
+    net1 = pkg.Mlp(ctx, dims, acts)
+    P = net1.init_params(123, "cpu")
+    l1, g1 = net1.loss_grad(P, X, Y, idx=idx, inv_scale=1.0 / b, l2=1e-4)
+
+    def body(r, c):
+        lo, hi = shard(b, world, r)
+        net = pkg.Mlp(c, dims, acts)
+        return net.loss_grad(P, X, Y, idx=idx[lo:hi].contiguous(), inv_scale=1.0 / b, l2=1e-4)
+
+    res = run_ranks(pkg, world, body)
+    assert torch.equal(res[0][1], res[1][1])
+    assert abs(res[0][0] - l1) <= 1e-6 * abs(l1)
+    assert rel(host(res[0][1]), host(g1)) <= 1e-5
+
+
+@pytest.mark.parametrize("line_search", ["wolfe", "armijo"])
+def test_ranks_cfg2_full_size_trajectory(ctx, pkg, line_search):
+    """BASELINE cfg 2 at N = 60000 split 30000 / 30000: 10 L-BFGS iterations with the same line-search
+    trial counts and pair acceptances as the single route, losses within 1e-5, ranks bitwise identical."""
+    dims, acts, N, world = [784, 128, 10], ["relu", "linear"], 60000, 2
+    Xh, Yh = pkg.synth_mnist(N)
+    net1 = pkg.Mlp(ctx, dims, acts)
+    P0 = net1.init_params(123, "cpu")
+    P1 = P0.clone()
+    h1, _ = pkg.lbfgs_solve(net1, P1, dev(Xh), dev(Yh), line_search=line_search, m=10, max_iters=10, tol=0.0)
+    shards = [shard(N, world, r) for r in range(world)]
+    Xs = [dev(Xh[lo:hi]) for lo, hi in shards]
+    Ys = [dev(Yh[lo:hi]) for lo, hi in shards]
+
+    def body(r, c):
+        net = pkg.Mlp(c, dims, acts)
+        P = P0.clone()
+        h, info = pkg.lbfgs_solve(net, P, Xs[r], Ys[r], n_global=N, line_search=line_search, m=10, max_iters=10,
+                                  tol=0.0)
+        return h, P, info.n_rows
+
+    res = run_ranks(pkg, world, body)
+    for h, P, _ in res[1:]:
+        assert np.array_equal(h["loss"], res[0][0]["loss"]) and torch.equal(P, res[0][1])
+    assert res[0][2] == res[1][2] > 0  # 30000 rows per evaluation on each rank
+    h = res[0][0]
+    assert np.array_equal(h["ls_trials"], h1["ls_trials"]), (h["ls_trials"], h1["ls_trials"])
+    assert np.array_equal(h["accepted"], h1["accepted"])
+    assert np.max(np.abs(h["loss"] - h1["loss"]) / np.abs(h1["loss"])) <= 1e-5
+    assert rel(host(res[0][1]), host(P1)) <= 1e-4
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_ranks_ragged_lbfgs(ctx, pkg, world):
+    """Ragged shards (N = 2049 over 3 / 4 ranks), Wolfe and the speculative pipeline with rejections:
+    ranks bitwise identical, the first 10 iterations as the single route's."""
+    dims, acts, N = [784, 64, 10], ["relu", "linear"], 2049
+    Xh, Yh = pkg.synth_mnist(N)
+    net1 = pkg.Mlp(ctx, dims, acts)
+    P0 = net1.init_params(7, "cpu")
+    P1 = P0.clone()
+    h1, _ = pkg.lbfgs_solve(net1, P1, dev(Xh), dev(Yh), m=10, max_iters=25, tol=0.0)
+    shards = [shard(N, world, r) for r in range(world)]
+    Xs = [dev(Xh[lo:hi]) for lo, hi in shards]
+    Ys = [dev(Yh[lo:hi]) for lo, hi in shards]
+
+    def body(r, c):
+        net = pkg.Mlp(c, dims, acts)
+        P = P0.clone()
+        h, _ = pkg.lbfgs_solve(net, P, Xs[r], Ys[r], n_global=N, m=10, max_iters=25, tol=0.0)
+        return h, P
+
+    res = run_ranks(pkg, world, body)
+    for h, P in res[1:]:
+        assert np.array_equal(h["loss"], res[0][0]["loss"]) and torch.equal(P, res[0][1])
+    h = res[0][0]
+    assert np.array_equal(h["ls_trials"][:10], h1["ls_trials"][:10])
+    assert np.max(np.abs(h["loss"][:10] - h1["loss"][:10]) / np.abs(h1["loss"][:10])) <= 1e-4
+
+
+def test_ranks_empty_share_lbfgs(ctx, pkg):
+    """N = 3 rows over 4 ranks: one rank evaluates nothing and still joins every all-reduce."""
+    dims, acts, N, world = [784, 16, 10], ["relu", "linear"], 3, 4
+    Xh, Yh = pkg.synth_mnist(N)
+    net1 = pkg.Mlp(ctx, dims, acts)
+    P0 = net1.init_params(3, "cpu")
+    P1 = P0.clone()
+    h1, _ = pkg.lbfgs_solve(net1, P1, dev(Xh), dev(Yh), m=5, max_iters=8, tol=0.0)
+    shards = [shard(N, world, r) for r in range(world)]
+    Xs = [dev(Xh[lo:hi]) if hi > lo else dev(np.zeros((1, 784))) for lo, hi in shards]
+    Ys = [dev(Yh[lo:hi]) if hi > lo else dev(np.zeros((1, 10))) for lo, hi in shards]
+
+    def body(r, c):
+        net = pkg.Mlp(c, dims, acts)
+        P = P0.clone()
+        lo, hi = shards[r]
+        h, _ = pkg.lbfgs_solve(net, P, Xs[r][: hi - lo], Ys[r][: hi - lo], n_global=N, m=5, max_iters=8, tol=0.0)
+        return h, P
+
+    res = run_ranks(pkg, world, body)
+    for h, P in res[1:]:
+        assert torch.equal(P, res[0][1])
+    h = res[0][0]
+    assert np.array_equal(h["ls_trials"], h1["ls_trials"])
+    assert np.max(np.abs(h["loss"] - h1["loss"]) / np.abs(h1["loss"])) <= 1e-4
+
+
+@pytest.mark.parametrize("world,kw", [
+    (2, dict(M=5, L=4, b=32, b_H=16)),
+    (3, dict(M=5, L=4, b=32, b_H=16)),
+    (2, dict(M=5, L=4, b=1, b_H=1)),            # b < world: a rank's minibatch slice is empty
+    (2, dict(M=5, L=4, b=32, b_H=1, hvp_exact=1)),  # exact HVP with b_H < world
+])
+def test_ranks_slbfgs_equals_single(ctx, pkg, world, kw):
+    dims, acts, N = [784, 16, 10], ["relu", "linear"], 512 if kw["b"] > 1 else 64
+    Xh, Yh = pkg.synth_mnist(N)
+    X, Y = dev(Xh), dev(Yh)
+    args = dict(step=0.02, max_epochs=2, tol=0.0, lam=1e-4, **kw)
+    net1 = pkg.Mlp(ctx, dims, acts)
+    P0 = net1.init_params(123, "cpu")
+    P1 = P0.clone()
+    h1, _ = pkg.slbfgs_solve(net1, P1, X, Y, **args)
+
+    def body(r, c):
+        net = pkg.Mlp(c, dims, acts)
+        P = P0.clone()
+        h, _ = pkg.slbfgs_solve(net, P, X, Y, **args)
+        return h, P
+
+    res = run_ranks(pkg, world, body)
+    for h, P in res[1:]:
+        assert np.array_equal(h["loss"], res[0][0]["loss"]) and torch.equal(P, res[0][1])
+    h = res[0][0]
+    assert np.all(np.isfinite(h["loss"]))
+    assert np.array_equal(h["accepted"], h1["accepted"])
+    assert np.max(np.abs(h["loss"] - h1["loss"]) / np.abs(h1["loss"])) <= 1e-4, (h["loss"], h1["loss"])
+    assert rel(host(res[0][1]), host(P1)) <= 1e-3
+
+
+def test_ranks_cfg4_epoch(ctx, pkg):
+    """BASELINE cfg 4 (784-512-256-10, N = 60000, b = 256, b_H = 128, L = M = 10) for one epoch at world 2
+    against the single route: the twin's anchor gradients ahead and ONE all-reduce per [g(w_t) | g(w)]
+    block; same number of live curvature pairs, epoch loss within 5 % (234 SVRG steps with FD pairs are
+    chaotic at the rounding level: tests/test_gpu_fullsize.py), ranks bitwise identical."""
+    dims, acts, N, world = [784, 512, 256, 10], ["relu", "relu", "linear"], 60000, 2
+    Xh, Yh = pkg.synth_mnist(N)
+    X, Y = dev(Xh), dev(Yh)
+    args = dict(M=10, L=10, b=256, b_H=128, step=0.005, max_epochs=1, tol=0.0, lam=1e-4)
+    net1 = pkg.Mlp(ctx, dims, acts)
+    P0 = net1.init_params(123, "cpu")
+    P1 = P0.clone()
+    h1, i1 = pkg.slbfgs_solve(net1, P1, X, Y, **args)
+
+    def body(r, c):
+        net = pkg.Mlp(c, dims, acts)
+        P = P0.clone()
+        h, info = pkg.slbfgs_solve(net, P, X, Y, **args)
+        return h, P, info.n_rows
+
+    res = run_ranks(pkg, world, body)
+    assert torch.equal(res[0][1], res[1][1])
+    h = res[0][0]
+    assert np.isfinite(h["loss"][0])
+    assert h["accepted"][0] == h1["accepted"][0]
+    assert abs(h["loss"][0] - h1["loss"][0]) <= 0.05 * abs(h1["loss"][0])
+    assert res[0][2] + res[1][2] == i1.n_rows  # the ranks' slices partition the single route's rows
