@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--solver", choices=["lbfgs", "slbfgs"], default="lbfgs",
                     help="slbfgs: BASELINE config 4 (S-LBFGS 784-512-256-10, b=256, b_H=128, L=M=10); a step "
                          "is one epoch")
+    ap.add_argument("--slbfgs-b", type=int, default=256, help="S-LBFGS minibatch b (config 4: 256)")
+    ap.add_argument("--slbfgs-bh", type=int, default=128, help="S-LBFGS Hessian batch b_H (config 4: 128)")
     ap.add_argument("--slbfgs-step", type=float, default=0.005,
                     help="S-LBFGS step (config 4 names 0.02, which diverges to NaN on the synthetic data in the "
                          "fp64 oracle too; the work per epoch does not depend on it)")
@@ -181,7 +183,7 @@ def main_slbfgs(a, pkg, ctx, world, rank):
     del Xh, Yh
     net = pkg.Mlp(ctx, dims, acts)
     P = net.init_params(123, "cpu")
-    kw = dict(M=10, L=10, b=256, b_H=128, step=a.slbfgs_step, lam=1e-4, tol=0.0)
+    kw = dict(M=10, L=10, b=a.slbfgs_b, b_H=a.slbfgs_bh, step=a.slbfgs_step, lam=1e-4, tol=0.0)
     # warmup epoch(s) with every kernel section timed: the breakdown and the dominant section
     ctx.prof_select(None)
     ctx.prof_sample(1)
@@ -246,9 +248,9 @@ def main_slbfgs(a, pkg, ctx, world, rank):
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic",
-            "config": {"workload": f"{a.dims} MLP ({a.acts}), S-LBFGS b=256 b_H=128 L=M=10 step {a.slbfgs_step} "
-                                   f"lambda 1e-4, N={N}; a step = one epoch ({N // 256} inner steps) incl. the "
-                                   f"call's one-time full-gradient anchor",
+            "config": {"workload": f"{a.dims} MLP ({a.acts}), S-LBFGS b={a.slbfgs_b} b_H={a.slbfgs_bh} L=M=10 step "
+                                   f"{a.slbfgs_step} lambda 1e-4, N={N}; a step = one epoch ({N // a.slbfgs_b} inner "
+                                   f"steps) incl. the call's one-time full-gradient anchor",
                        "global_batch": N, "parallelism": f"dp{world}"},
             "grad_evals_per_s": round(evals_all / elapsed, 1),
             "grad_eval_gflops": round(rows_all * F / elapsed / 1e9, 1),

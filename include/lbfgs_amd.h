@@ -151,7 +151,13 @@ typedef struct lbf_slbfgs_params {
   double fd_eps;      /* finite-difference HVP epsilon, 1e-4 (s_lbfgs.hpp:90)        */
   int hvp_exact;      /* 0: the reference's central-difference HVP (s_lbfgs.hpp:88-101); 1: the
                          exact R-operator product (lbf_mlp_hvp), SURVEY §8(f) rank 4          */
+  /* ABI 2, diagnostics (NULL / 0: off): one row of LBF_PAIR_TRACE_COLS doubles per curvature-pair
+   * candidate (s_lbfgs.hpp:245-256): epoch, inner step t, y.s, s.s, y.y, accepted (|y.s| > 1e-10), live
+   * pairs after it, 0. Reading each row back synchronises the stream: not for timed runs. */
+  double *pair_trace;
+  int pair_trace_cap;
 } lbf_slbfgs_params;
+#define LBF_PAIR_TRACE_COLS 8
 
 /* Gradient descent with momentum == cuda_mlp::CudaGD (src/cuda/gd.cuh:38-106; setters :22-25). */
 typedef struct lbf_gd_params {

@@ -34,7 +34,8 @@ class LbfgsParams(C.Structure):
 class SlbfgsParams(C.Structure):
     _fields_ = [("max_epochs", C.c_int), ("tol", C.c_double), ("M", C.c_int), ("L", C.c_int), ("b", C.c_int),
                 ("b_H", C.c_int), ("step", C.c_double), ("reg", C.c_double), ("seed", C.c_uint),
-                ("fd_eps", C.c_double), ("hvp_exact", C.c_int)]
+                ("fd_eps", C.c_double), ("hvp_exact", C.c_int), ("pair_trace", C.POINTER(C.c_double)),
+                ("pair_trace_cap", C.c_int)]
 
 
 class GdParams(C.Structure):

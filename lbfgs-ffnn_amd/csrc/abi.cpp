@@ -425,6 +425,8 @@ void lbf_slbfgs_default_params(lbf_slbfgs_params *p) {
   p->seed = 123;
   p->fd_eps = 1e-4;
   p->hvp_exact = 0;
+  p->pair_trace = nullptr;
+  p->pair_trace_cap = 0;
 }
 
 int lbf_lbfgs_begin(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, const float *d_X,

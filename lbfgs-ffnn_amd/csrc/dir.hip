@@ -1,0 +1,268 @@
+// History update of the S-LBFGS inner step in two launches (the L-BFGS fused tail's pattern, tail.hip,
+// with the operands of GramArgs instead of split-K slabs):
+//   dir_sweep    one block per 64*C-column group: the new vectors s = sa - sb, y = (ya - yb)*yscale,
+//                g = ga - gb + gc of the group (s, y into the ring's write slot, g into g_out), the group's
+//                values of every live history vector, all loaded up front (one round trip), then every
+//                Gram column of the group reduced out of LDS by four lanes -> one partial row per block,
+//                stored transposed ([nc][nb]);
+//   dir_cols_fin one block per Gram column: its fixed-order sum; the last block to arrive (arrival
+//                counter) runs the history step (hist_core.hpp: push / evict, the two-loop recurrences on
+//                coefficients) from those sums.
+// The linear-combination sweep (combine_small) follows. Replaces gram_kernel -> fold_rows -> hist_step
+// (three launches, the step reading a folded partial table) for S-LBFGS's directions (s_lbfgs.hpp:
+// 106-136 two-loop with the VR gradient of :228) and curvature pairs (:245-256).
+#include "hist_core.hpp"
+#include "internal.hpp"
+#include "kernels.hpp"
+#include "wave.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+namespace lbf {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// C columns per lane (64*C per block); VPW history vectors per wave (v = wave + 4j).
+template <int C, int VPW>
+__global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
+  constexpr int TC = 64 * C;
+  const GramArgs &g = a.g;
+  const HistView &h = g.h;
+  if (h.abort && *h.abort) return;
+  __shared__ float xs[4 * VPW][TC]; // this group's values of the live history vectors
+  __shared__ float ops[3][TC];      // s, y, g
+  __shared__ int ist[IST_ORDER + DIR_MAXM];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (t < IST_ORDER + h.m) ist[t] = h.ist[t];
+  lds_barrier();
+  const int count0 = __builtin_amdgcn_readfirstlane(g.reset ? 0 : ist[IST_COUNT]);
+  const int w = __builtin_amdgcn_readfirstlane(hist_write_slot(ist, h.m, g.policy, g.reset));
+  if (blockIdx.x == 0 && t == 0) h.ist[IST_WSLOT] = w;
+  const int nvec = 2 * count0;
+  // every load below is unconditional from a clamped address and masked after (tail.hip's discipline)
+  long long e[C];
+  bool live[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const long long col = (long long)blockIdx.x * TC + lane + 64 * c;
+    live[c] = col < h.n;
+    e[c] = live[c] ? col : h.n - 1;
+  }
+  float vv[VPW][C];
+  unsigned zero_mask = 0; // bit j: vector j of this wave is not live (or is the slot being overwritten)
+#pragma unroll
+  for (int j = 0; j < VPW; ++j) {
+    const int v = wave + 4 * j;
+    const int vi = v < nvec ? v : 0;
+    const int slot = __builtin_amdgcn_readfirstlane(ist[IST_ORDER + (vi < count0 ? vi : vi - count0)]);
+    const float *base = (vi < count0 ? h.S : h.Y) + (long long)slot * h.ld;
+#pragma unroll
+    for (int c = 0; c < C; ++c) vv[j][c] = base[e[c]];
+    if (v >= nvec || (g.has_pair && slot == w)) zero_mask |= 1u << j;
+  }
+  if (wave == 0) { // the new vectors of the group (null operands read ga / sa and are masked)
+    const float *dflt = g.has_g ? g.ga : g.sa;
+    float sa[C], sb[C], ya[C], yb[C], ga[C], gb[C], gc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      sa[c] = (g.sa ? g.sa : dflt)[e[c]];
+      sb[c] = (g.sb ? g.sb : dflt)[e[c]];
+      ya[c] = (g.ya ? g.ya : dflt)[e[c]];
+      yb[c] = (g.yb ? g.yb : dflt)[e[c]];
+      ga[c] = (g.ga ? g.ga : dflt)[e[c]];
+      gb[c] = (g.gb ? g.gb : dflt)[e[c]];
+      gc[c] = (g.gc ? g.gc : dflt)[e[c]];
+    }
+    const float ysc = float(g.yscale);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int q = lane + 64 * c;
+      float sv = 0.f, yv = 0.f, gv = 0.f;
+      if (live[c]) {
+        if (g.has_pair) { // gram_kernel's arithmetic
+          sv = sa[c] - sb[c];
+          yv = (ya[c] - yb[c]) * ysc;
+          h.S[(long long)w * h.ld + e[c]] = sv;
+          h.Y[(long long)w * h.ld + e[c]] = yv;
+        }
+        if (g.has_g) {
+          gv = ga[c];
+          if (g.gb) gv = gv - gb[c];
+          if (g.gc) gv = gv + gc[c];
+          if (g.g_out) g.g_out[e[c]] = gv;
+        }
+      }
+      ops[0][q] = sv;
+      ops[1][q] = yv;
+      ops[2][q] = gv;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < VPW; ++j) {
+    const int v = wave + 4 * j;
+    if (v < nvec)
+#pragma unroll
+      for (int c = 0; c < C; ++c) xs[v][lane + 64 * c] = ((zero_mask >> j) & 1u) || !live[c] ? 0.0f : vv[j][c];
+  }
+  lds_barrier();
+  // ---- dot columns: 4 lanes per column, TC/4 exact fp64 products each, fixed order ----
+  // history columns 6i + {0..5}: S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g ; self 6m + {s.s s.y y.y g.s g.y g.g}
+  const int nh = 6 * count0, ncu = nh + 6;
+  const int q = t & 3;
+  for (int base = 0; base < 4 * ncu; base += 256) {
+    const int u = (base + t) >> 2;
+    double d = 0.0;
+    int c = -1;
+    if (u < ncu) {
+      const float *A, *B;
+      if (u < nh) {
+        const int i = u / 6, r = u - 6 * i;
+        A = xs[(r & 1) ? count0 + i : i];
+        B = ops[r >> 1];
+        c = u;
+      } else {
+        const int z = u - nh; // (s,s) (s,y) (y,y) (g,s) (g,y) (g,g)
+        const int ia = (0x222100 >> (4 * z)) & 0xF, ib = (0x210110 >> (4 * z)) & 0xF;
+        A = ops[ia];
+        B = ops[ib];
+        c = 6 * h.m + z;
+      }
+      const f32x4 *A4 = reinterpret_cast<const f32x4 *>(A + (TC / 4) * q);
+      const f32x4 *B4 = reinterpret_cast<const f32x4 *>(B + (TC / 4) * q);
+#pragma unroll
+      for (int k = 0; k < TC / 16; ++k) {
+        const f32x4 x = A4[k], y = B4[k];
+        d += double(x[0]) * double(y[0]);
+        d += double(x[1]) * double(y[1]);
+        d += double(x[2]) * double(y[2]);
+        d += double(x[3]) * double(y[3]);
+      }
+    }
+    d += dpp_f64<0xB1, 0xF>(d); // quad_perm [1,0,3,2]
+    d += dpp_f64<0x4E, 0xF>(d); // quad_perm [2,3,0,1]
+    if (c >= 0 && q == 0) a.rows[(long long)c * a.nb + blockIdx.x] = d;
+  }
+}
+
+constexpr int DF_THREADS = 256;
+
+// Column sums, then the last block runs the history step. Release: each block's column store, fence,
+// arrival; acquire: the last arrival fences before reading the other blocks' sums (agent scope).
+__global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs a) {
+  const HistView &h = a.g.h;
+  if (h.abort && *h.abort) return; // uniform for the launch: nobody arrives, the counter stays 0
+  extern __shared__ double dyn[]; // sy [2*m*m] (SY and its transpose) | yy [m*m] | SY, YY [S*S] | rho [S]
+  __shared__ HistSmem sm;
+  __shared__ double ws[4];
+  __shared__ int s_last;
+  __shared__ int ist_l[IST_ORDER + DIR_MAXM + 4];
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int count0 = a.g.reset ? 0 : h.ist[IST_COUNT];
+  if (!(c < 6 * h.m && c >= 6 * count0)) { // only the columns in use (live pairs and the self block)
+    const double *colp = a.rows + (long long)c * a.nb;
+    double v[8];
+    double s = 0.0;
+    for (int r0 = t; r0 < a.nb; r0 += DF_THREADS * 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { // unconditional loads from clamped rows: all eight in flight at once
+        const int r = r0 + DF_THREADS * u;
+        v[u] = colp[r < a.nb ? r : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (r0 + DF_THREADS * u < a.nb) ? v[u] : 0.0;
+    }
+    s = wave_sum_f64(s);
+    if ((t & 63) == 0) ws[t >> 6] = s;
+    lds_barrier();
+    if (t == 0) a.dots[c] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+  }
+  if (t == 0) {
+    __threadfence();
+    s_last = atomicAdd(a.cols_done, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (t == 0) *a.cols_done = 0u; // ready for the next launch (stream-ordered)
+  // ---- the history step, from LDS: dots, ring header, and (fused) SY, YY, rho ----
+  const int m = h.m, S_ = h.slots;
+  double *SYp = dyn + 3 * m * m, *YYp = SYp + S_ * S_, *rhop = YYp + S_ * S_;
+  for (int q = t; q < 6 * m + 6; q += DF_THREADS) sm.dots[q] = a.dots[q];
+  if (t < IST_ORDER + m) ist_l[t] = h.ist[t];
+  const bool fused = a.want_dir == 1 && !a.g.reset;
+  if (fused) {
+    for (int i = t; i < S_ * S_; i += DF_THREADS) {
+      SYp[i] = h.SY[i];
+      YYp[i] = h.YY[i];
+    }
+    if (t < S_) rhop[t] = h.rho[t];
+  }
+  lds_barrier();
+  HistStep st;
+  st.h = h;
+  st.has_pair = a.g.has_pair;
+  st.has_g = a.g.has_g;
+  st.reset = a.g.reset;
+  st.policy = a.g.policy;
+  st.want_dir = a.want_dir;
+  st.iter = a.iter;
+  st.dsign = a.dsign;
+  if (fused) {
+    st.ist = ist_l;
+    st.rho = rhop;
+    st.SY = SYp;
+    st.YY = YYp;
+    hist_prologue<true>(st, sm, ist_l[IST_WSLOT]);
+    hist_core<true>(st, sm, dyn, 2 * m * m, dyn + 2 * m * m, m * m);
+  } else {
+    hist_prologue<false>(st, sm, ist_l[IST_WSLOT]);
+    hist_core<false>(st, sm, dyn, 2 * m * m, dyn + 2 * m * m, m * m);
+  }
+}
+
+template <int C>
+void launch_sweep(hipStream_t s, const DirArgs &a, int vpw) {
+  switch (vpw) {
+  case 2: hipLaunchKernelGGL((dir_sweep_kernel<C, 2>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 4: hipLaunchKernelGGL((dir_sweep_kernel<C, 4>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 8: hipLaunchKernelGGL((dir_sweep_kernel<C, 8>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 16: hipLaunchKernelGGL((dir_sweep_kernel<C, 16>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  default: throw Error(2, "dir_sweep: history size not supported");
+  }
+}
+
+} // namespace
+
+static int dir_vpw(int m) {
+  const int per_wave = (2 * m + 3) / 4;
+  return per_wave <= 2 ? 2 : per_wave <= 4 ? 4 : per_wave <= 8 ? 8 : 16;
+}
+bool dir_supported(int m, long long n) { return m >= 0 && m <= DIR_MAXM && n > 0 && n <= DIR_MAXN; }
+// 256 columns per block for long vectors (half the partial rows), except with 16 vectors per wave, whose
+// LDS copy of the group would then pass 64 KB
+int dir_cols_per_block(int m, long long n) { return (n > (1LL << 18) && dir_vpw(m) < 16) ? 256 : 128; }
+int dir_ncols(int m) { return 6 * m + 6; }
+
+void dir_sweep(hipStream_t s, const DirArgs &a) {
+  LBF_REQUIRE(dir_supported(a.g.h.m, a.g.h.n), "dir_sweep: history size / vector length");
+  LBF_REQUIRE(a.want_dir == 0 || a.want_dir == 1, "dir_sweep: want_dir 0 / 1");
+  LBF_REQUIRE(a.nb == int(cdiv(a.g.h.n, dir_cols_per_block(a.g.h.m, a.g.h.n))), "dir_sweep: block count");
+  const int vpw = dir_vpw(a.g.h.m);
+  if (dir_cols_per_block(a.g.h.m, a.g.h.n) == 256) launch_sweep<4>(s, a, vpw);
+  else launch_sweep<2>(s, a, vpw);
+  LBF_KERNEL_CHECK();
+}
+
+void dir_fin(hipStream_t s, const DirArgs &a) {
+  const int m = a.g.h.m;
+  const size_t shmem = (size_t(3) * m * m + 2 * size_t(a.g.h.slots) * a.g.h.slots + a.g.h.slots) * sizeof(double);
+  hipLaunchKernelGGL(dir_cols_fin_kernel, dim3(unsigned(dir_ncols(m))), dim3(DF_THREADS), shmem, s, a);
+  LBF_KERNEL_CHECK();
+}
+
+} // namespace lbf

@@ -344,6 +344,27 @@ void tail_reduce(hipStream_t s, const TailArgs &a); // tail_reduce + tail_cols (
 void tail_fin(hipStream_t s, const TailArgs &a);    // one block
 int tail_vpw(int m);                                // vectors per wave of the Gram sweep (0: unsupported)
 
+// S-LBFGS history update in two launches (dir.hip): a one-round-trip Gram sweep of the new s / y / g
+// against the live history (one block per 64*C columns, a partial row each, stored [nc][nb]), then one
+// block per Gram column whose last arrival runs the history step (hist_core.hpp) from the column sums.
+constexpr int DIR_MAXM = 32;
+constexpr long long DIR_MAXN = 1LL << 22;
+struct DirArgs {
+  GramArgs g;               // operands, policy, has_pair / has_g, reset; g.h carries the abort flag
+  int want_dir = 1;         // 0 (pair only) or 1
+  int iter = 1;
+  double dsign = 1.0;
+  double *rows = nullptr;   // [dir_ncols(m)][nb]
+  double *dots = nullptr;   // [dir_ncols(m)]
+  int nb = 0;               // cdiv(n, dir_cols_per_block(m, n))
+  unsigned *cols_done = nullptr; // arrival counter, zero between launches
+};
+bool dir_supported(int m, long long n);
+int dir_cols_per_block(int m, long long n);
+int dir_ncols(int m);
+void dir_sweep(hipStream_t s, const DirArgs &a);
+void dir_fin(hipStream_t s, const DirArgs &a);
+
 struct CombineArgs {
   HistView h;
   const float *g = nullptr; // the vector the direction was built for

@@ -901,6 +901,14 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
   // the ring vectors are only ever read for live slots, but keep them defined
   LBF_HIP(hipMemsetAsync(S_.get(), 0, S_.size() * sizeof(float), ctx_->stream));
   LBF_HIP(hipMemsetAsync(Y_.get(), 0, Y_.size() * sizeof(float), ctx_->stream));
+  dir_on_ = dir_supported(m, n) && env_int("LBF_DIR_FUSED", 1) != 0;
+  if (dir_on_) {
+    const int nb = int(cdiv(n, dir_cols_per_block(m, n)));
+    drows_.resize(size_t(dir_ncols(m)) * size_t(nb));
+    ddots_.resize(size_t(dir_ncols(m)));
+    dcount_.resize(1);
+    LBF_HIP(hipMemsetAsync(dcount_.get(), 0, sizeof(unsigned), ctx_->stream));
+  }
 }
 
 void History::reset() { hist_reset(ctx_->stream, v_); }
@@ -910,6 +918,26 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
   g.h = v_;
   g.h.abort = ctx_->abort;
   hipStream_t s = ctx_->stream;
+  if (dir_on_ && g.policy == POL_SLBFGS && (want_dir == 0 || want_dir == 1)) {
+    // S-LBFGS: sweep + column sums whose last block runs the step (dir.hip), two launches instead of
+    // gram -> fold -> hist_step
+    DirArgs d;
+    d.g = g;
+    d.want_dir = want_dir;
+    d.iter = iter;
+    d.dsign = dsign;
+    d.rows = drows_.get();
+    d.dots = ddots_.get();
+    d.nb = int(cdiv(v_.n, dir_cols_per_block(v_.m, v_.n)));
+    d.cols_done = dcount_.get();
+    {
+      ProfScope ps(ctx_, PK_GRAM);
+      dir_sweep(s, d);
+    }
+    ProfScope ps(ctx_, PK_COEF);
+    dir_fin(s, d);
+    return;
+  }
   {
     ProfScope ps(ctx_, PK_GRAM);
     gram_update(s, g, part_.get());

@@ -203,6 +203,10 @@ private:
   DevBuf<float> S_, Y_;
   DevBuf<int> ist_;
   DevBuf<double> dstate_, part_, red_;
+  // two-launch S-LBFGS update (dir.hip): partial rows, column sums, arrival counter
+  DevBuf<double> drows_, ddots_;
+  DevBuf<unsigned> dcount_;
+  bool dir_on_ = false;
 };
 
 struct LbfgsRecordRow {

@@ -831,6 +831,7 @@ int SlbfgsSolver::run(lbf_record *rec) {
           pa.ya = gp;
           pa.yb = gm;
           hist_.update(pa, 0, 1, +1.0);
+          if (prm_.pair_trace && npairs_ < prm_.pair_trace_cap) trace_pair(iters_, t);
         }
         LBF_HIP(hipMemcpyAsync(up_.get(), u_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
         have_u = true;
@@ -869,6 +870,25 @@ int SlbfgsSolver::run(lbf_record *rec) {
     tctx_->prof.merge_into(ctx_->prof);
   }
   return iters_;
+}
+
+// Diagnostics row of the pair just offered to the ring (lbf_slbfgs_params.pair_trace): synchronous.
+void SlbfgsSolver::trace_pair(int epoch, int t) {
+  hipStream_t s = ctx_->stream;
+  const HistView v = hist_.view();
+  LBF_HIP(hipMemcpyAsync(hs_.get(), v.scal, SC_N * sizeof(double), hipMemcpyDeviceToHost, s));
+  int wslot = 0;
+  LBF_HIP(hipMemcpyAsync(&wslot, v.ist + IST_WSLOT, sizeof(int), hipMemcpyDeviceToHost, s));
+  LBF_HIP(hipStreamSynchronize(s));
+  double ss = 0.0, yy = 0.0;
+  const size_t d = size_t(wslot) * size_t(v.slots) + size_t(wslot);
+  LBF_HIP(hipMemcpyAsync(&ss, v.SS + d, sizeof(double), hipMemcpyDeviceToHost, s));
+  LBF_HIP(hipMemcpyAsync(&yy, v.YY + d, sizeof(double), hipMemcpyDeviceToHost, s));
+  LBF_HIP(hipStreamSynchronize(s));
+  double *row = prm_.pair_trace + size_t(npairs_++) * LBF_PAIR_TRACE_COLS;
+  const double vals[LBF_PAIR_TRACE_COLS] = {double(epoch), double(t), hs_[SC_YS], ss, yy, hs_[SC_ACCEPT],
+                                            hs_[SC_COUNT], 0.0};
+  for (int i = 0; i < LBF_PAIR_TRACE_COLS; ++i) row[i] = vals[i];
 }
 
 void SlbfgsSolver::info(lbf_solve_info *out) const {

@@ -177,6 +177,8 @@ private:
                  double inv_scale); // rows off .. off+count-1 of this rank's gathered block
   // Data parallel: all-reduce a [ga | gb] block once, then finish both gradients (+ lambda w).
   void reduce_pair(const float *wa, const float *wb, float *gab, double inv_scale);
+  void trace_pair(int epoch, int t);
+  int npairs_ = 0;
   Mlp *net_;
   Ctx *ctx_;
   lbf_slbfgs_params prm_;

@@ -317,14 +317,24 @@ class LbfgsRun:
             pass
 
 
-def slbfgs_solve(net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, **kw):
-    """S-LBFGS (SVRG + FD-HVP curvature pairs); X/Y hold all N rows on every rank."""
+def slbfgs_solve(net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, pair_trace: int = 0, **kw):
+    """S-LBFGS (SVRG + FD-HVP curvature pairs); X/Y hold all N rows on every rank. pair_trace > 0 records up
+    to that many curvature-pair candidates (diagnostics, synchronous) into hist["pairs"]: rows of (epoch, t,
+    y.s, s.s, y.y, accepted, live pairs, 0)."""
     p = slbfgs_params(**kw)
+    trace = None
+    if pair_trace > 0:
+        trace = np.full((int(pair_trace), 8), np.nan)
+        p.pair_trace = trace.ctypes.data_as(C.POINTER(C.c_double))
+        p.pair_trace_cap = int(pair_trace)
     hist = History(p.max_epochs)
     info = SolveInfo()
     check(lib().lbf_slbfgs_solve(net.h, C.byref(p), ptr(params), ptr(X), ptr(Y), int(X.shape[0]),
                                  C.byref(hist.rec), C.byref(info)), "lbf_slbfgs_solve")
-    return hist.as_dict(), info
+    out = hist.as_dict()
+    if trace is not None:
+        out["pairs"] = trace[~np.isnan(trace[:, 0])]
+    return out, info
 
 
 def gd_solve(net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, n_global: Optional[int] = None,

@@ -15,6 +15,7 @@
 #pragma once
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -649,7 +650,8 @@ struct SlbfgsParams {
 // BG(w, idx, g): batch gradient; BF(w, idx) -> batch loss.
 template <class T, class BG, class BF>
 Vec<T> slbfgs(Vec<T> weights, BG &&batch_g, BF &&batch_f, const SlbfgsParams &prm, std::vector<IterRecord> *rec,
-              int *iters_out, std::vector<std::vector<size_t>> *sampled = nullptr) {
+              int *iters_out, std::vector<std::vector<size_t>> *sampled = nullptr,
+              std::vector<std::array<double, 8>> *pairs = nullptr) {
   const size_t n = weights.size();
   const int M = prm.M;
   Ring<Vec<T>> u_list(M > 0 ? M + 1 : 0), s_list(M > 0 ? M : 0), y_list(M > 0 ? M : 0);
@@ -692,11 +694,16 @@ Vec<T> slbfgs(Vec<T> weights, BG &&batch_g, BF &&batch_f, const SlbfgsParams &pr
           if (sampled) sampled->push_back(hb);
           Vec<T> y = finite_difference_hvp_batch<T>(batch_g, u, s, hb, 1e-4);
           double ys = double(dot(y, s));
-          if (std::abs(ys) > 1e-10) {
+          const bool acc = std::abs(ys) > 1e-10;
+          if (acc) {
             s_list.push_back(s);
             y_list.push_back(y);
             rho_list.push_back(1.0 / ys);
           }
+          // diagnostics row (the device's lbf_slbfgs_params.pair_trace): epoch, t, y.s, s.s, y.y, accepted, live
+          if (pairs)
+            pairs->push_back({double(it), double(t), ys, double(dot(s, s)), double(dot(y, y)), acc ? 1.0 : 0.0,
+                              double(s_list.size()), 0.0});
         }
         u_list.push_back(u);
       }

@@ -60,7 +60,8 @@ def lib():
                                               C.POINTER(C.c_int)]
         L.oracle_slbfgs_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_int, C.c_double,
                                         C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, _dp,
-                                        C.POINTER(C.c_int), C.c_void_p, C.c_longlong]
+                                        C.POINTER(C.c_int), C.c_void_p, C.c_longlong, C.c_void_p, C.c_int,
+                                        C.POINTER(C.c_int)]
         L.oracle_gd_mlp.restype = C.c_int
         L.oracle_gd_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_double, C.c_double, C.c_int,
                                     C.c_double, C.c_int, _dp]
@@ -178,7 +179,9 @@ class Net:
         return P, rec[:n]
 
     def slbfgs(self, P, X, Y, epochs=2, tol=0.0, M=10, L=10, b=32, bH=16, step=0.02, lam=1e-4, fp32=False,
-               want_idx=False):
+               want_idx=False, pair_trace=0):
+        """Returns (params, rec, idx) or, with pair_trace > 0, (params, rec, idx, pairs): one row per curvature
+        pair candidate (epoch, t, y.s, s.s, y.y, accepted, live pairs, 0), as the device's pair trace."""
         P = np.array(P, np.float64, copy=True)
         rec = np.zeros((epochs, 6), np.float64)
         it = C.c_int(0)
@@ -189,11 +192,16 @@ class Net:
             m = max(1, N // b)
             cap = epochs * (m * b + (m // max(L, 1) + 1) * bH)
             idx = np.full(cap, -1, np.int64)
+        pairs = np.zeros((max(int(pair_trace), 1), 8), np.float64)
+        npairs = C.c_int(0)
         lib().oracle_slbfgs_mlp(self.nl, self.dims, self.acts, P, np.ascontiguousarray(X, np.float64),
                                 np.ascontiguousarray(Y, np.float64), N, epochs, tol, M, L, b, bH, step, lam, int(fp32),
-                                rec, C.byref(it), idx.ctypes.data if want_idx else None, cap)
+                                rec, C.byref(it), idx.ctypes.data if want_idx else None, cap,
+                                pairs.ctypes.data if pair_trace > 0 else None, int(pair_trace), C.byref(npairs))
         if want_idx:
             idx = idx[idx >= 0]
+        if pair_trace > 0:
+            return P, rec[: it.value], idx, pairs[: npairs.value]
         return P, rec[: it.value], idx
 
 

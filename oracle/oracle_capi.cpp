@@ -130,7 +130,7 @@ int run_armijo_mlp(const Net &net, double *params, const double *X, const double
 template <class T>
 int run_slbfgs_mlp(const Net &net, double *params, const double *X, const double *Y, int64_t N, int epochs,
                    double tol, int M, int L, int b, int bH, double step, double lambda, double *rec_out, int *iters,
-                   int64_t *idx_out, int64_t idx_cap) {
+                   int64_t *idx_out, int64_t idx_cap, double *pair_out, int pair_cap, int *npairs) {
   std::vector<T> Xt = to_vec<T>(X, size_t(N) * net.dims[0]);
   std::vector<T> Yt = to_vec<T>(Y, size_t(N) * net.dims.back());
   MLPObjective<T> obj{&net, Xt.data(), Yt.data(), N, {}, 0, 0};
@@ -163,7 +163,18 @@ int run_slbfgs_mlp(const Net &net, double *params, const double *X, const double
   prm.m = int(N / b) > 0 ? int(N / b) : 1; // unified_optimization.hpp:326-327
   std::vector<IterRecord> rec;
   std::vector<std::vector<size_t>> sampled;
-  Vec<T> w = slbfgs<T>(to_vec<T>(params, net.nparams), bg, bf, prm, &rec, iters, idx_out ? &sampled : nullptr);
+  std::vector<std::array<double, 8>> pairs;
+  Vec<T> w = slbfgs<T>(to_vec<T>(params, net.nparams), bg, bf, prm, &rec, iters, idx_out ? &sampled : nullptr,
+                       pair_out ? &pairs : nullptr);
+  if (pair_out) {
+    int k = 0;
+    for (auto &r : pairs)
+      if (k < pair_cap) {
+        for (int j = 0; j < 8; ++j) pair_out[size_t(k) * 8 + j] = r[size_t(j)];
+        ++k;
+      }
+    if (npairs) *npairs = k;
+  }
   from_vec(w, params);
   write_rec(rec, rec_out, epochs);
   if (idx_out) {
@@ -288,13 +299,14 @@ int oracle_lbfgs_armijo_mlp(int nl, const int *dims, const int *acts, double *pa
 // S-LBFGS on the MLP (CPU semantics, fp64). idx_out (optional) receives every sampled index list in order.
 int oracle_slbfgs_mlp(int nl, const int *dims, const int *acts, double *params, const double *X, const double *Y,
                       long long N, int epochs, double tol, int M, int L, int b, int bH, double step, double lambda,
-                      int fp32, double *rec, int *iters, long long *idx_out, long long idx_cap) {
+                      int fp32, double *rec, int *iters, long long *idx_out, long long idx_cap, double *pair_out,
+                      int pair_cap, int *npairs) {
   Net net(dims, acts, nl);
   if (fp32)
     return run_slbfgs_mlp<float>(net, params, X, Y, N, epochs, tol, M, L, b, bH, step, lambda, rec, iters,
-                                 reinterpret_cast<int64_t *>(idx_out), idx_cap);
+                                 reinterpret_cast<int64_t *>(idx_out), idx_cap, pair_out, pair_cap, npairs);
   return run_slbfgs_mlp<double>(net, params, X, Y, N, epochs, tol, M, L, b, bH, step, lambda, rec, iters,
-                                reinterpret_cast<int64_t *>(idx_out), idx_cap);
+                                reinterpret_cast<int64_t *>(idx_out), idx_cap, pair_out, pair_cap, npairs);
 }
 
 // GD (gd.cuh:38-106) / SGD (sgd.cuh:50-153) with momentum on the MLP. rec: 2 doubles per record.
