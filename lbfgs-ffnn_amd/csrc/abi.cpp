@@ -435,7 +435,8 @@ int lbf_lbfgs_begin(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, 
     LBF_REQUIRE(net && prm && out, "null argument");
     LBF_REQUIRE(prm->m >= 0 && prm->m <= 128, "m in [0, 128]");
     net->ctx->c.set_device();
-    LBF_REQUIRE(d_params && d_X && d_Y, "null pointer");
+    // a data-parallel rank with an empty shard (n_local == 0) has no data pointers
+    LBF_REQUIRE(d_params && (n_local == 0 || (d_X && d_Y)), "null pointer");
     LBF_REQUIRE(n_local >= 0 && n_global > 0, "batch sizes");
     auto *s = new lbf_lbfgs();
     try {

@@ -44,16 +44,16 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(hist_write_slot(ist, h.m, g.policy, g.reset));
   if (blockIdx.x == 0 && t == 0) h.ist[IST_WSLOT] = w;
   const int nvec = 2 * count0;
-  // every load below is unconditional from a clamped address and masked after (tail.hip's discipline)
-  long long e[C];
+  // Lane l owns columns 4l .. 4l+3 of the group (C == 4: 16-B loads; every vector the sweep touches is
+  // 16-B aligned and padded to a multiple of 4 floats, History::update checks). Every load is
+  // unconditional from a clamped address and masked after (tail.hip's discipline).
+  static_assert(C == 4, "dir_sweep: four columns per lane");
+  const long long col0 = (long long)blockIdx.x * TC + 4 * lane;
+  const long long e4 = col0 < h.n ? col0 : ((h.n - 1) & ~3LL); // clamped quad start (inside the padding)
   bool live[C];
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const long long col = (long long)blockIdx.x * TC + lane + 64 * c;
-    live[c] = col < h.n;
-    e[c] = live[c] ? col : h.n - 1;
-  }
-  float vv[VPW][C];
+  for (int c = 0; c < C; ++c) live[c] = col0 + c < h.n;
+  f32x4 vv[VPW];
   unsigned zero_mask = 0; // bit j: vector j of this wave is not live (or is the slot being overwritten)
 #pragma unroll
   for (int j = 0; j < VPW; ++j) {
@@ -61,40 +61,32 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
     const int vi = v < nvec ? v : 0;
     const int slot = __builtin_amdgcn_readfirstlane(ist[IST_ORDER + (vi < count0 ? vi : vi - count0)]);
     const float *base = (vi < count0 ? h.S : h.Y) + (long long)slot * h.ld;
-#pragma unroll
-    for (int c = 0; c < C; ++c) vv[j][c] = base[e[c]];
+    vv[j] = *reinterpret_cast<const f32x4 *>(base + e4);
     if (v >= nvec || (g.has_pair && slot == w)) zero_mask |= 1u << j;
   }
   if (wave == 0) { // the new vectors of the group (null operands read ga / sa and are masked)
     const float *dflt = g.has_g ? g.ga : g.sa;
-    float sa[C], sb[C], ya[C], yb[C], ga[C], gb[C], gc[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      sa[c] = (g.sa ? g.sa : dflt)[e[c]];
-      sb[c] = (g.sb ? g.sb : dflt)[e[c]];
-      ya[c] = (g.ya ? g.ya : dflt)[e[c]];
-      yb[c] = (g.yb ? g.yb : dflt)[e[c]];
-      ga[c] = (g.ga ? g.ga : dflt)[e[c]];
-      gb[c] = (g.gb ? g.gb : dflt)[e[c]];
-      gc[c] = (g.gc ? g.gc : dflt)[e[c]];
-    }
+    auto ld4 = [&](const float *p) { return *reinterpret_cast<const f32x4 *>((p ? p : dflt) + e4); };
+    const f32x4 sa = ld4(g.sa), sb = ld4(g.sb), ya = ld4(g.ya), yb = ld4(g.yb);
+    const f32x4 ga = ld4(g.ga), gb = ld4(g.gb), gc = ld4(g.gc);
     const float ysc = float(g.yscale);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      const int q = lane + 64 * c;
+      const int q = 4 * lane + c;
+      const long long e = col0 + c;
       float sv = 0.f, yv = 0.f, gv = 0.f;
       if (live[c]) {
         if (g.has_pair) { // gram_kernel's arithmetic
           sv = sa[c] - sb[c];
           yv = (ya[c] - yb[c]) * ysc;
-          h.S[(long long)w * h.ld + e[c]] = sv;
-          h.Y[(long long)w * h.ld + e[c]] = yv;
+          h.S[(long long)w * h.ld + e] = sv;
+          h.Y[(long long)w * h.ld + e] = yv;
         }
         if (g.has_g) {
           gv = ga[c];
           if (g.gb) gv = gv - gb[c];
           if (g.gc) gv = gv + gc[c];
-          if (g.g_out) g.g_out[e[c]] = gv;
+          if (g.g_out) g.g_out[e] = gv;
         }
       }
       ops[0][q] = sv;
@@ -105,9 +97,12 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
 #pragma unroll
   for (int j = 0; j < VPW; ++j) {
     const int v = wave + 4 * j;
-    if (v < nvec)
+    if (v < nvec) {
+      f32x4 x;
 #pragma unroll
-      for (int c = 0; c < C; ++c) xs[v][lane + 64 * c] = ((zero_mask >> j) & 1u) || !live[c] ? 0.0f : vv[j][c];
+      for (int c = 0; c < C; ++c) x[c] = ((zero_mask >> j) & 1u) || !live[c] ? 0.0f : vv[j][c];
+      *reinterpret_cast<f32x4 *>(&xs[v][4 * lane]) = x;
+    }
   }
   lds_barrier();
   // ---- dot columns: 4 lanes per column, TC/4 exact fp64 products each, fixed order ----
@@ -231,7 +226,6 @@ void launch_sweep(hipStream_t s, const DirArgs &a, int vpw) {
   case 2: hipLaunchKernelGGL((dir_sweep_kernel<C, 2>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
   case 4: hipLaunchKernelGGL((dir_sweep_kernel<C, 4>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
   case 8: hipLaunchKernelGGL((dir_sweep_kernel<C, 8>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
-  case 16: hipLaunchKernelGGL((dir_sweep_kernel<C, 16>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
   default: throw Error(2, "dir_sweep: history size not supported");
   }
 }
@@ -242,19 +236,21 @@ static int dir_vpw(int m) {
   const int per_wave = (2 * m + 3) / 4;
   return per_wave <= 2 ? 2 : per_wave <= 4 ? 4 : per_wave <= 8 ? 8 : 16;
 }
+// 256 columns per block (16-B loads, four columns per lane); the LDS copy of a group holds 4 * VPW vectors,
+// so m <= 16 (VPW 8: 32 KB)
 bool dir_supported(int m, long long n) { return m >= 0 && m <= DIR_MAXM && n > 0 && n <= DIR_MAXN; }
-// 256 columns per block for long vectors (half the partial rows), except with 16 vectors per wave, whose
-// LDS copy of the group would then pass 64 KB
-int dir_cols_per_block(int m, long long n) { return (n > (1LL << 18) && dir_vpw(m) < 16) ? 256 : 128; }
+int dir_cols_per_block(int m, long long n) {
+  (void)m;
+  (void)n;
+  return 256;
+}
 int dir_ncols(int m) { return 6 * m + 6; }
 
 void dir_sweep(hipStream_t s, const DirArgs &a) {
   LBF_REQUIRE(dir_supported(a.g.h.m, a.g.h.n), "dir_sweep: history size / vector length");
   LBF_REQUIRE(a.want_dir == 0 || a.want_dir == 1, "dir_sweep: want_dir 0 / 1");
   LBF_REQUIRE(a.nb == int(cdiv(a.g.h.n, dir_cols_per_block(a.g.h.m, a.g.h.n))), "dir_sweep: block count");
-  const int vpw = dir_vpw(a.g.h.m);
-  if (dir_cols_per_block(a.g.h.m, a.g.h.n) == 256) launch_sweep<4>(s, a, vpw);
-  else launch_sweep<2>(s, a, vpw);
+  launch_sweep<4>(s, a, dir_vpw(a.g.h.m));
   LBF_KERNEL_CHECK();
 }
 

@@ -167,7 +167,7 @@ void synth_regression(hipStream_t s, long long row0, long long N, int In, unsign
                       float *Y);
 
 void finalize_grad_dots(hipStream_t s, long long n, float *g, const float *w, double lambda, const float *p,
-                        double *partials, const int *abort = nullptr);
+                        double *partials, const int *abort = nullptr, const float *g_in = nullptr);
 // generic: per-WG partials of x.y -> partials[wg]
 void dot_partials(hipStream_t s, long long n, const float *x, const float *y, double *partials);
 
@@ -326,6 +326,10 @@ constexpr int TAIL_COLS = 128; // columns per tail_reduce block
 struct TailArgs {
   RedAllArgs ra;                // every segment with parts == 1; ra.w = x_t, ra.p = direction
   const float *hilo = nullptr;  // data parallel: all-reduced SSE (hi, lo) behind the gradient
+  // data parallel: the all-reduced gradient words to read the columns from (segments taken as written);
+  // the tail then writes ra.G. Never ra.G itself: an aborted speculative iteration's collective still
+  // runs, so it must not land in a buffer that may hold the live gradient.
+  const float *g_src = nullptr;
   HistView h;
   int has_pair = 0;
   const float *x_prev = nullptr, *g_prev = nullptr;
@@ -347,7 +351,7 @@ int tail_vpw(int m);                                // vectors per wave of the G
 // S-LBFGS history update in two launches (dir.hip): a one-round-trip Gram sweep of the new s / y / g
 // against the live history (one block per 64*C columns, a partial row each, stored [nc][nb]), then one
 // block per Gram column whose last arrival runs the history step (hist_core.hpp) from the column sums.
-constexpr int DIR_MAXM = 32;
+constexpr int DIR_MAXM = 16;
 constexpr long long DIR_MAXN = 1LL << 22;
 struct DirArgs {
   GramArgs g;               // operands, policy, has_pair / has_g, reset; g.h carries the abort flag

@@ -471,7 +471,17 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
   const bool fused = fs_.fused;
   const int fold = empty ? -1 : fs_.fold, nloss = empty ? 0 : fs_.nloss, lstart = empty ? -1 : fs_.lstart;
   const long long nfold = fold >= 0 ? (long long)(fold + 1) * Lo.in : 0; // fold rows in the head slab
-  if (empty) zero_fill(s, (long long)nparams_ + 2, G, ctx_->abort);
+  // Where this rank's gradient lands before the collective: G itself on a single rank and for a packed
+  // local evaluation (its caller reduces the block), else the private words buffer. The collective of a
+  // speculative iteration that was aborted still runs (RCCL cannot skip it; every rank aborts alike), and
+  // G of a queued iteration can be the buffer of the live gradient: only abort-aware kernels (the tail,
+  // finalize) may write G from the reduced words.
+  float *Gl = G;
+  if (reduced && !local) {
+    words_.ensure(size_t(cdiv((long long)nparams_ + 2, 4) * 4));
+    Gl = words_.get();
+  }
+  if (empty) zero_fill(s, (long long)nparams_ + 2, Gl, ctx_->abort);
   for (int l = lstart; l >= 0; --l) {
     const Layer &L = layers_[l];
     const float *Ain = (l == 0) ? X : A_[l - 1].get();
@@ -514,7 +524,7 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       d.side_splits = head ? nloss : N1.splits;
       d.side_stride = nseg;
       d.side_count = nseg;
-      d.side_dst = G + N1.off - (head ? nfold : 0);
+      d.side_dst = Gl + N1.off - (head ? nfold : 0);
     }
     const long long seg = (long long)d.M * L.out;
     if (L.splits > 1) {
@@ -523,7 +533,7 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       ProfScope ps(ctx_, PK_DW, l);
       gemm(s, d);
     } else {
-      d.C = G + L.off;
+      d.C = Gl + L.off;
       ProfScope ps(ctx_, PK_DW, l);
       gemm(s, d);
     }
@@ -554,7 +564,7 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
   }
   // every layer's partial slabs -> gradient (+ dots and the status block on a single rank)
   RedAllArgs ra;
-  ra.G = G;
+  ra.G = Gl;
   ra.w = P;
   ra.p = pdir;
   ra.lambda = lambda;
@@ -611,7 +621,7 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     loc.dots = 0;
     ProfScope ps(ctx_, PK_SLAB, 0);
     reduce_all(s, loc);
-    sse_pack(s, loss_part_.get(), nloss, G + nparams_, ctx_->abort);
+    sse_pack(s, loss_part_.get(), nloss, Gl + nparams_, ctx_->abort);
   };
   bool tail_ok = tf != nullptr && !local;
   for (int l = 0; l < nl && tail_ok; ++l) tail_ok = ra.seg[l].parts == 1;
@@ -623,15 +633,17 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       local_words();
       if (ctx_->dp()) {
         ProfScope ps(ctx_, PK_ALLREDUCE);
-        ctx_->allreduce(G, nparams_ + 2);
+        ctx_->allreduce(Gl, nparams_ + 2);
       }
-      hilo = hilo_in ? hilo_in : G + nparams_;
+      hilo = hilo_in ? hilo_in : Gl + nparams_;
       for (int l = 0; l < nl; ++l) {
         ra.seg[l].slab = nullptr;
         ra.seg[l].splits = 0;
       }
     }
     ta.ra = ra;
+    ta.ra.G = G;
+    ta.g_src = Gl != G ? Gl : nullptr;
     ta.hilo = hilo;
     ta.h = tf->h;
     ta.h.abort = ctx_->abort;
@@ -681,23 +693,23 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
   if (local) return; // the caller all-reduces [G | hi | lo] (with other blocks) and calls finish_reduced
   if (ctx_->dp()) {
     ProfScope ps(ctx_, PK_ALLREDUCE);
-    ctx_->allreduce(G, nparams_ + 2); // one RCCL all-reduce of [grad | sse_hi | sse_lo]
+    ctx_->allreduce(Gl, nparams_ + 2); // one RCCL all-reduce of [grad | sse_hi | sse_lo]
   }
-  finish_reduced(P, G, inv_scale, lambda, pdir, scal, hilo_in);
+  finish_reduced(P, G, inv_scale, lambda, pdir, scal, hilo_in, Gl != G ? Gl : nullptr);
 }
 
 // The gradient and status of an all-reduced [G | hi | lo] block: G += lambda w, the dots of the status
 // block, and the loss from the (hi, lo) words (or from hilo_in: a loss-only trial's reduced words).
 void Mlp::finish_reduced(const float *P, float *G, double inv_scale, double lambda, const float *pdir, double *scal,
-                         const float *hilo_in) {
+                         const float *hilo_in, const float *g_src) {
   hipStream_t s = ctx_->stream;
   ProfScope ps(ctx_, PK_FINAL, 1);
   const int nd = dots_partials_wg(nparams_);
   dots_part_.ensure(size_t(nd) * 3);
-  finalize_grad_dots(s, nparams_, G, P, lambda, pdir, dots_part_.get(), ctx_->abort);
+  finalize_grad_dots(s, nparams_, G, P, lambda, pdir, dots_part_.get(), ctx_->abort, g_src);
   if (scal)
-    eval_tail(s, dots_part_.get(), nd, loss_part_.get(), 0, hilo_in ? hilo_in : G + nparams_, inv_scale, lambda, scal,
-              ctx_->abort);
+    eval_tail(s, dots_part_.get(), nd, loss_part_.get(), 0, hilo_in ? hilo_in : (g_src ? g_src : G) + nparams_,
+              inv_scale, lambda, scal, ctx_->abort);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -918,7 +930,10 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
   g.h = v_;
   g.h.abort = ctx_->abort;
   hipStream_t s = ctx_->stream;
-  if (dir_on_ && g.policy == POL_SLBFGS && (want_dir == 0 || want_dir == 1)) {
+  auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+  const bool aligned = al16(g.sa) && al16(g.sb) && al16(g.ya) && al16(g.yb) && al16(g.ga) && al16(g.gb) &&
+                       al16(g.gc) && al16(g.g_out); // 16-B lanes in dir_sweep (null pointers pass)
+  if (dir_on_ && aligned && g.policy == POL_SLBFGS && (want_dir == 0 || want_dir == 1)) {
     // S-LBFGS: sweep + column sums whose last block runs the step (dir.hip), two launches instead of
     // gram -> fold -> hist_step
     DirArgs d;

@@ -123,8 +123,9 @@ public:
   // finish_reduced (+ lambda w, status block). Together bitwise equal to loss_grad on the same rank.
   void loss_grad_local(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
                        double inv_scale);
+  // g_src (nullable): the reduced words are there and the finished gradient is written to G
   void finish_reduced(const float *P, float *G, double inv_scale, double lambda, const float *pdir, double *scal,
-                      const float *hilo_in = nullptr);
+                      const float *hilo_in = nullptr, const float *g_src = nullptr);
   long long loss_only_evals() const { return loss_only_; }
   long long grad_after_loss_evals() const { return gal_; } // backward phases run after a loss_only
   // Exact Hessian-vector product Hv = H(P) V of the same batch loss (+ lambda V), Pearlmutter's
@@ -148,7 +149,7 @@ private:
     bool fused = false;
     int fold = -1, nloss = 0, lstart = 0;
   } fs_;
-  DevBuf<float> hilo_;
+  DevBuf<float> hilo_, words_; // loss-only (hi, lo); data parallel: this rank's [grad | hi | lo] for the collective
   long long loss_only_ = 0, gal_ = 0;
   void ensure(long long B);
   bool side_reduced(int l, bool fused, int nloss) const;

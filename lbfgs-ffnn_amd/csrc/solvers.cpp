@@ -2,6 +2,7 @@
 #include "solvers.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -775,6 +776,8 @@ int SlbfgsSolver::run(lbf_record *rec) {
       LBF_HIP(hipEventRecord(ev_g2_[t & 1], tctx_->stream));
     };
     // the epoch's gathered rows and w are complete (the context stream was synchronised above)
+    static const int host_timing = env_int("LBF_HOST_TIMING", 0);
+    const auto th0 = std::chrono::steady_clock::now();
     if (tnet_) anchor_ahead(0);
     for (int t = 0; t < m_inner; ++t) {
       const Slice &sl = mb[t];
@@ -836,6 +839,14 @@ int SlbfgsSolver::run(lbf_record *rec) {
         LBF_HIP(hipMemcpyAsync(up_.get(), u_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
         have_u = true;
       }
+    }
+    if (host_timing) { // host time to enqueue the epoch's inner steps vs the epoch on the device
+      const auto th1 = std::chrono::steady_clock::now();
+      LBF_HIP(hipStreamSynchronize(s));
+      const auto th2 = std::chrono::steady_clock::now();
+      std::fprintf(stderr, "[lbf host] epoch %d: %d inner steps enqueued in %.3f ms, device done %.3f ms later\n",
+                   iters_, m_inner, std::chrono::duration<double, std::milli>(th1 - th0).count(),
+                   std::chrono::duration<double, std::milli>(th2 - th1).count());
     }
     // the next epoch's lists, drawn while the GPU runs this epoch's queued steps
     if (iters_ + 1 < prm_.max_epochs) {
@@ -921,7 +932,7 @@ void put_record(lbf_record *rec, int i, double loss, double gnorm, double ms, do
 // blocking cublasSnrm2 becomes the evaluation's g.g, read with the loss once per iteration.
 int run_gd(Mlp *net, const lbf_gd_params &prm, float *d_params, const float *X, const float *Y, long long n_local,
            long long n_global, lbf_record *rec, lbf_solve_info *info) {
-  LBF_REQUIRE(d_params && X && Y && n_local >= 0 && n_global > 0, "bad argument");
+  LBF_REQUIRE(d_params && n_local >= 0 && n_global > 0 && (n_local == 0 || (X && Y)), "bad argument");
   Ctx *c = net->ctx();
   c->set_device();
   hipStream_t s = c->stream;

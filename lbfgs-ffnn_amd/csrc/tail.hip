@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
     xp[c] = (a.x_prev ? a.x_prev : ra.w)[e[c]];
     gp[c] = (a.g_prev ? a.g_prev : ra.w)[e[c]];
     pv[c] = (ra.p ? ra.p : ra.w)[e[c]];
-    gw[c] = ra.G[e[c]];
+    gw[c] = (a.g_src ? a.g_src : ra.G)[e[c]];
   }
   KT(49);
   // ---- gradient columns: split-K slabs in split order (4 stripes) ----
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
       if (live[c]) {
         gv = S.splits > 0 ? float(((part[0][q] + part[1][q]) + part[2][q]) + part[3][q]) : gw[c];
         if (ra.lambda != 0.0) gv = gv + float(ra.lambda) * wv[c]; // finalize_kernel's update
-        if (S.splits > 0 || ra.lambda != 0.0) ra.G[e[c]] = gv;
+        if (S.splits > 0 || ra.lambda != 0.0 || a.g_src) ra.G[e[c]] = gv;
         if (a.has_pair) {
           sv = wv[c] - xp[c];
           yv = gv - gp[c];

@@ -495,20 +495,21 @@ int dots_partials_wg(long long n) {
   return int(w < 1 ? 1 : (w > 512 ? 512 : w));
 }
 
-__global__ __launch_bounds__(256) void finalize_kernel(long long n, float *g, const float *w, double lambda,
-                                                       const float *p, double *partials, const int *abort) {
+// g_in (nullable): read the gradient there and always write g (a data-parallel evaluation's all-reduced
+// words buffer -> the live gradient, only when the speculative chain was not aborted)
+__global__ __launch_bounds__(256) void finalize_kernel(long long n, float *g, const float *g_in, const float *w,
+                                                       double lambda, const float *p, double *partials,
+                                                       const int *abort) {
   if (abort && *abort) return;
   __shared__ double scratch[48];
   double acc[3] = {0.0, 0.0, 0.0};
   const long long stride = (long long)gridDim.x * blockDim.x;
   const float lf = float(lambda);
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
-    float gv = g[e];
+    float gv = (g_in ? g_in : g)[e];
     const float wv = w ? w[e] : 0.0f;
-    if (lambda != 0.0) {
-      gv = gv + lf * wv;
-      g[e] = gv;
-    }
+    if (lambda != 0.0) gv = gv + lf * wv;
+    if (lambda != 0.0 || g_in) g[e] = gv;
     acc[0] += double(gv) * double(gv);
     if (p) acc[1] += double(gv) * double(p[e]);
     acc[2] += double(wv) * double(wv);
@@ -522,8 +523,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(long long n, float *g, co
 }
 
 void finalize_grad_dots(hipStream_t s, long long n, float *g, const float *w, double lambda, const float *p,
-                        double *partials, const int *abort) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(dots_partials_wg(n)), dim3(256), 0, s, n, g, w, lambda, p, partials,
+                        double *partials, const int *abort, const float *g_in) {
+  hipLaunchKernelGGL(finalize_kernel, dim3(dots_partials_wg(n)), dim3(256), 0, s, n, g, g_in, w, lambda, p, partials,
                      abort);
   LBF_KERNEL_CHECK();
 }

