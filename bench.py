@@ -36,7 +36,8 @@ REF_GPU = {("784,128,10", 10): 139.1, ("784,128,10", 100): 87.2,
 FP32_MFMA_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix peak (dense)
 HBM_PEAK_GBS = 8000.0
 PROF_EVERY = 8                   # time every 8th launch of the dominant kernel inside the timed region ...
-PROF_MIN_LAUNCHES = 40           # ... unless that would time fewer launches than this (then every launch)
+PROF_MIN_LAUNCHES = 10           # ... or more often, so that at least this many launches are timed (an event
+                                 # pair costs ~10 us of GPU time: profiles/r03/launch_floor.txt)
 
 
 def parse():
@@ -199,8 +200,11 @@ def main_slbfgs(a, pkg, ctx, world, rank):
         obj = [dominant]
         torch.distributed.broadcast_object_list(obj, src=0)
         dominant = obj[0]
-    # timed region: only the dominant section carries events (every launch: the batch sizes differ)
+    # timed region: only the dominant section carries events, on every PROF_EVERY-th launch (an event pair
+    # costs ~10 us of GPU time, and this section runs ~2x per inner step); the rows of every timed launch
+    # are counted (lbf_prof_read_work), so the sampled flops are exact whatever the batch sizes
     ctx.prof_select(dominant)
+    ctx.prof_sample(PROF_EVERY)
     ctx.prof_enable(True)
     torch.cuda.synchronize()
     if world > 1:
@@ -219,8 +223,10 @@ def main_slbfgs(a, pkg, ctx, world, rank):
         torch.distributed.barrier()
     elapsed, evals_all, rows_all = float(cnt[0]), float(cnt[1]), float(cnt[2])
     prof = ctx.prof_read()
+    work = ctx.prof_read_work()
     ctx.prof_enable(False)
     ctx.prof_select(None)
+    ctx.prof_sample(1)
     if rank == 0:
         epochs = int(info.iterations)
         F = pkg.grad_flops_per_sample(dims)
@@ -228,12 +234,13 @@ def main_slbfgs(a, pkg, ctx, world, rank):
         kind, layer = name.split("[")[0], int(name.split("[")[1].rstrip("]"))
         roof = dict(bound="mfma", achieved=None, peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s", frac=None)
         if kind in ("gemm_fwd", "gemm_dw", "gemm_dx"):
-            # every evaluation runs this GEMM once over its batch rows: algorithmic flops over all of
-            # this rank's launches / their summed event time
-            flops = 2.0 * dims[layer] * dims[layer + 1] * float(info.n_rows)
+            # algorithmic flops of the timed launches (2 In Out per row, rows counted per launch) / their
+            # summed event time
+            flops = 2.0 * dims[layer] * dims[layer + 1] * float(work.get(dominant, 0.0))
             roof["achieved"] = round(flops / (ms / 1e3) / 1e12, 3)
             roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
         roof.update(kernel=name, avg_launch_us=round(ms * 1e3 / launches, 2), timed_launches=launches,
+                    sampled_every=PROF_EVERY, avg_rows_per_timed_launch=round(work.get(dominant, 0.0) / launches, 1),
                     traffic=None)
         out = {
             "metric": "S-LBFGS epochs/s + grad-evals/s, 784-512-256-10 MLP",
@@ -329,7 +336,7 @@ def main():
     # the dominant section runs about once per evaluation: sample every PROF_EVERY-th launch only when
     # that still times PROF_MIN_LAUNCHES of them
     launches = breakdown[dominant][1] / max(bd_steps, 1) * a.steps
-    every = PROF_EVERY if launches / PROF_EVERY >= PROF_MIN_LAUNCHES else 1
+    every = max(1, min(PROF_EVERY, int(launches // PROF_MIN_LAUNCHES)))
     ctx.prof_sample(every)
     ctx.prof_enable(True)
 
@@ -351,6 +358,7 @@ def main():
         elapsed = float(t.item())
     barrier()
     prof = ctx.prof_read()
+    work = ctx.prof_read_work()
     ctx.prof_enable(False)
     ctx.prof_select(None)
     ctx.prof_sample(1)
@@ -373,7 +381,7 @@ def main():
         n_loc = hi - lo
         In, Out = dims[layer], dims[layer + 1]
         if kind in ("gemm_fwd", "gemm_dw", "gemm_dx"):
-            flops = 2.0 * n_loc * In * Out                    # per launch, per rank
+            flops = 2.0 * In * Out * work.get(dominant, n_loc * cnt) / cnt  # per launch (rows counted), per rank
             roof = dict(bound="mfma", achieved=round(flops / avg_s / 1e12, 3), peak=FP32_MFMA_PEAK_TFLOPS,
                         unit="TFLOP/s")
         else:

@@ -252,6 +252,9 @@ int lbf_prof_select(lbf_ctx *ctx, int section_id);
  * region at 1/every of the event cost (an event record idles the GPU for ~5 us). */
 int lbf_prof_sample(lbf_ctx *ctx, int every);
 int lbf_prof_read(lbf_ctx *ctx, int cap, int *ids, double *ms, long long *counts, int *n_out);
+/* ABI 2: the work units of the timed launches per section, same order as lbf_prof_read (GEMM sections: the
+ * batch rows of every timed launch, so a sampled section's flops are 2 * In * Out * work). */
+int lbf_prof_read_work(lbf_ctx *ctx, int cap, int *ids, double *work, int *n_out);
 
 /* ---- device memory, so C/C++ consumers need no HIP headers (the reference's DeviceBuffer,
  * src/cuda/device_buffer.cuh:7-96). kind: 0 host->device, 1 device->host, 2 device->device;

@@ -542,6 +542,7 @@ int lbf_prof_enable(lbf_ctx *ctx, int on) {
     if (on) {
       ctx->c.prof.ms.clear();
       ctx->c.prof.cnt.clear();
+      ctx->c.prof.work.clear();
     }
   });
 }
@@ -573,6 +574,24 @@ int lbf_prof_read(lbf_ctx *ctx, int cap, int *ids, double *ms, long long *counts
         if (ids) ids[k] = int(i);
         if (ms) ms[k] = ctx->c.prof.ms[i];
         if (counts) counts[k] = ctx->c.prof.cnt[i];
+      }
+      ++k;
+    }
+    *n_out = k;
+  });
+}
+
+int lbf_prof_read_work(lbf_ctx *ctx, int cap, int *ids, double *work, int *n_out) {
+  return guard([&] {
+    LBF_REQUIRE(ctx && n_out, "null argument");
+    ctx->c.set_device();
+    ctx->c.prof.resolve();
+    int k = 0;
+    for (size_t i = 0; i < ctx->c.prof.cnt.size(); ++i) {
+      if (ctx->c.prof.cnt[i] == 0) continue;
+      if (k < cap) {
+        if (ids) ids[k] = int(i);
+        if (work) work[k] = i < ctx->c.prof.work.size() ? ctx->c.prof.work[i] : 0.0;
       }
       ++k;
     }

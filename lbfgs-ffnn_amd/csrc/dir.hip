@@ -33,7 +33,6 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
   const GramArgs &g = a.g;
   const HistView &h = g.h;
   if (h.abort && *h.abort) return;
-  __shared__ float xs[4 * VPW][TC]; // this group's values of the live history vectors
   __shared__ float ops[3][TC];      // s, y, g
   __shared__ int ist[IST_ORDER + DIR_MAXM];
   const int t = threadIdx.x, lane = t & 63;
@@ -94,60 +93,63 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
       ops[2][q] = gv;
     }
   }
+  lds_barrier();
+  // ---- dots: every (history vector, new vector) dot is owned by one wave: 4 exact fp64 products per lane,
+  // a DPP wave sum, lane 0 stores the partial row entry (no LDS staging of the history values: staged
+  // rows 1 KB apart put every quad of a wave on the same LDS banks) ----
+  const f32x4 s4 = *reinterpret_cast<const f32x4 *>(&ops[0][4 * lane]);
+  const f32x4 y4 = *reinterpret_cast<const f32x4 *>(&ops[1][4 * lane]);
+  const f32x4 g4 = *reinterpret_cast<const f32x4 *>(&ops[2][4 * lane]);
+  double *rows = a.rows + blockIdx.x;
+  const long long nb = a.nb;
 #pragma unroll
   for (int j = 0; j < VPW; ++j) {
-    const int v = wave + 4 * j;
-    if (v < nvec) {
-      f32x4 x;
+    const int v = wave + 4 * j; // wave-uniform
+    if (v >= nvec) break;
+    double ds = 0.0, dy = 0.0, dg = 0.0;
+    if (!((zero_mask >> j) & 1u)) { // the slot being overwritten contributes zeros (gram_kernel's rule)
 #pragma unroll
-      for (int c = 0; c < C; ++c) x[c] = ((zero_mask >> j) & 1u) || !live[c] ? 0.0f : vv[j][c];
-      *reinterpret_cast<f32x4 *>(&xs[v][4 * lane]) = x;
+      for (int c = 0; c < C; ++c) {
+        const double x = live[c] ? double(vv[j][c]) : 0.0;
+        ds += x * double(s4[c]);
+        dy += x * double(y4[c]);
+        dg += x * double(g4[c]);
+      }
+    }
+    ds = wave_sum_f64(ds);
+    dy = wave_sum_f64(dy);
+    dg = wave_sum_f64(dg);
+    if (lane == 0) {
+      const int li = v < count0 ? v : v - count0, cc = v < count0 ? 0 : 1;
+      rows[(long long)(6 * li + cc + 0) * nb] = ds;
+      rows[(long long)(6 * li + cc + 2) * nb] = dy;
+      rows[(long long)(6 * li + cc + 4) * nb] = dg;
     }
   }
-  lds_barrier();
-  // ---- dot columns: 4 lanes per column, TC/4 exact fp64 products each, fixed order ----
-  // history columns 6i + {0..5}: S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g ; self 6m + {s.s s.y y.y g.s g.y g.g}
-  const int nh = 6 * count0, ncu = nh + 6;
-  const int q = t & 3;
-  for (int base = 0; base < 4 * ncu; base += 256) {
-    const int u = (base + t) >> 2;
-    double d = 0.0;
-    int c = -1;
-    if (u < ncu) {
-      const float *A, *B;
-      if (u < nh) {
-        const int i = u / 6, r = u - 6 * i;
-        A = xs[(r & 1) ? count0 + i : i];
-        B = ops[r >> 1];
-        c = u;
-      } else {
-        const int z = u - nh; // (s,s) (s,y) (y,y) (g,s) (g,y) (g,g)
-        const int ia = (0x222100 >> (4 * z)) & 0xF, ib = (0x210110 >> (4 * z)) & 0xF;
-        A = ops[ia];
-        B = ops[ib];
-        c = 6 * h.m + z;
-      }
-      const f32x4 *A4 = reinterpret_cast<const f32x4 *>(A + (TC / 4) * q);
-      const f32x4 *B4 = reinterpret_cast<const f32x4 *>(B + (TC / 4) * q);
+  if (wave == 3) { // self block 6m + {s.s, s.y, y.y, g.s, g.y, g.g}
+    double d[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-      for (int k = 0; k < TC / 16; ++k) {
-        const f32x4 x = A4[k], y = B4[k];
-        d += double(x[0]) * double(y[0]);
-        d += double(x[1]) * double(y[1]);
-        d += double(x[2]) * double(y[2]);
-        d += double(x[3]) * double(y[3]);
-      }
+    for (int c = 0; c < C; ++c) {
+      const double sv = s4[c], yv = y4[c], gv = g4[c];
+      d[0] += sv * sv;
+      d[1] += sv * yv;
+      d[2] += yv * yv;
+      d[3] += gv * sv;
+      d[4] += gv * yv;
+      d[5] += gv * gv;
     }
-    d += dpp_f64<0xB1, 0xF>(d); // quad_perm [1,0,3,2]
-    d += dpp_f64<0x4E, 0xF>(d); // quad_perm [2,3,0,1]
-    if (c >= 0 && q == 0) a.rows[(long long)c * a.nb + blockIdx.x] = d;
+#pragma unroll
+    for (int z = 0; z < 6; ++z) d[z] = wave_sum_f64(d[z]);
+    if (lane == 0)
+#pragma unroll
+      for (int z = 0; z < 6; ++z) rows[(long long)(6 * h.m + z) * nb] = d[z];
   }
 }
 
 constexpr int DF_THREADS = 256;
 
-// Column sums, then the last block runs the history step. Release: each block's column store, fence,
-// arrival; acquire: the last arrival fences before reading the other blocks' sums (agent scope).
+// Column sums, then the last block runs the history step. Hand-off without fences (tail.hip's
+// tail_cols_fin): sc1 column stores waited for before the arrival add; the last arrival reads them sc1.
 __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs a) {
   const HistView &h = a.g.h;
   if (h.abort && *h.abort) return; // uniform for the launch: nobody arrives, the counter stays 0
@@ -174,20 +176,21 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs 
     s = wave_sum_f64(s);
     if ((t & 63) == 0) ws[t >> 6] = s;
     lds_barrier();
-    if (t == 0) a.dots[c] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+    if (t == 0) {
+      __hip_atomic_store(&a.dots[c], ((ws[0] + ws[1]) + ws[2]) + ws[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
-  if (t == 0) {
-    __threadfence();
-    s_last = atomicAdd(a.cols_done, 1u) == gridDim.x - 1;
-  }
+  if (t == 0)
+    s_last = __hip_atomic_fetch_add(a.cols_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
   if (t == 0) *a.cols_done = 0u; // ready for the next launch (stream-ordered)
   // ---- the history step, from LDS: dots, ring header, and (fused) SY, YY, rho ----
   const int m = h.m, S_ = h.slots;
   double *SYp = dyn + 3 * m * m, *YYp = SYp + S_ * S_, *rhop = YYp + S_ * S_;
-  for (int q = t; q < 6 * m + 6; q += DF_THREADS) sm.dots[q] = a.dots[q];
+  for (int q = t; q < 6 * m + 6; q += DF_THREADS) // sc1 loads: written this launch by other blocks
+    sm.dots[q] = __hip_atomic_load(&a.dots[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (t < IST_ORDER + m) ist_l[t] = h.ist[t];
   const bool fused = a.want_dir == 1 && !a.g.reset;
   if (fused) {

@@ -39,9 +39,11 @@ void Profiler::resolve() {
     if (size_t(r.id) >= ms.size()) {
       ms.resize(r.id + 1, 0.0);
       cnt.resize(r.id + 1, 0);
+      work.resize(r.id + 1, 0.0);
     }
     ms[r.id] += t;
     cnt[r.id] += 1;
+    work[r.id] += r.work;
   }
   recs.clear();
   used = 0;
@@ -52,13 +54,16 @@ void Profiler::merge_into(Profiler &dst) {
   if (dst.ms.size() < ms.size()) {
     dst.ms.resize(ms.size(), 0.0);
     dst.cnt.resize(ms.size(), 0);
+    dst.work.resize(ms.size(), 0.0);
   }
   for (size_t i = 0; i < ms.size(); ++i) {
     dst.ms[i] += ms[i];
     dst.cnt[i] += cnt[i];
+    dst.work[i] += work[i];
   }
   ms.assign(ms.size(), 0.0);
   cnt.assign(cnt.size(), 0);
+  work.assign(work.size(), 0.0);
 }
 
 void Ctx::set_device() const { LBF_HIP(hipSetDevice(device)); }
@@ -336,11 +341,11 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
       d.splits = L.fsplits;
       d.k_chunk = L.fk_chunk;
       d.slab_stride = B * L.out;
-      ProfScope ps(ctx_, PK_FWD, int(l));
+      ProfScope ps(ctx_, PK_FWD, int(l), double(B));
       gemm(s, d);
       fwd_reduce_act(s, fslab_.get(), L.fsplits, B * L.out, int(B), L.out, d.bias, L.act, A_[l].get(), ctx_->abort);
     } else {
-      ProfScope ps(ctx_, PK_FWD, int(l));
+      ProfScope ps(ctx_, PK_FWD, int(l), double(B));
       gemm(s, d);
     }
     in = A_[l].get();
@@ -383,7 +388,7 @@ void Mlp::forward_phase(const float *P, const float *X, const float *Y, const in
     d.head_sse = loss_part_.get();
     d.head_fold = fold;
     d.head_fold_c0 = fold_c0_;
-    ProfScope ps(ctx_, PK_FWD, nl - 2);
+    ProfScope ps(ctx_, PK_FWD, nl - 2, double(B));
     gemm(s, d);
     lstart = nl - 2;
   } else if (fused) {
@@ -530,11 +535,11 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     if (L.splits > 1) {
       d.C = slab_.get() + L.slab_off;
       d.slab_stride = seg;
-      ProfScope ps(ctx_, PK_DW, l);
+      ProfScope ps(ctx_, PK_DW, l, double(B));
       gemm(s, d);
     } else {
       d.C = Gl + L.off;
-      ProfScope ps(ctx_, PK_DW, l);
+      ProfScope ps(ctx_, PK_DW, l, double(B));
       gemm(s, d);
     }
     if (l > 0) {
@@ -558,7 +563,7 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       x.aux_act = P0.act;
       x.abort = ctx_->abort;
       x.tile = dx_tile(B, L.in);
-      ProfScope ps(ctx_, PK_DX, l);
+      ProfScope ps(ctx_, PK_DX, l, double(B));
       gemm(s, x);
     }
   }

@@ -25,10 +25,11 @@ struct Profiler {
   }
   std::vector<hipEvent_t> pool;
   size_t used = 0;
-  struct Rec { int id; size_t a, b; };
+  struct Rec { int id; size_t a, b; double work; };
   std::vector<Rec> recs;
   std::vector<double> ms;      // by section id
   std::vector<long long> cnt;  // by section id
+  std::vector<double> work;    // by section id: the caller's work units of the timed launches (GEMMs: rows)
   ~Profiler();
   size_t mark(hipStream_t s);
   void resolve();
@@ -84,11 +85,13 @@ struct ProfScope {
   int id;
   size_t a = 0;
   bool on;
-  ProfScope(Ctx *ctx, int kind, int layer = 0) : c(ctx), id(kind * 16 + layer), on(ctx->prof.want(id)) {
+  double work;
+  ProfScope(Ctx *ctx, int kind, int layer = 0, double w = 0.0)
+      : c(ctx), id(kind * 16 + layer), on(ctx->prof.want(id)), work(w) {
     if (on) a = c->prof.mark(c->stream);
   }
   ~ProfScope() {
-    if (on) c->prof.recs.push_back({id, a, c->prof.mark(c->stream)});
+    if (on) c->prof.recs.push_back({id, a, c->prof.mark(c->stream), work});
   }
 };
 

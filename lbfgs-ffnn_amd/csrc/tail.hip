@@ -45,7 +45,6 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   const RedAllArgs &ra = a.ra;
   if (ra.abort && *ra.abort) return;
   __shared__ double part[4][TC];
-  __shared__ float xs[2 * TAIL_MAXM][TC]; // this group's values of the live history vectors
   __shared__ float ops[5][TC];            // s, y, g, p, w
   __shared__ int ist[IST_ORDER + TAIL_MAXM];
   const HistView &h = a.h;
@@ -132,13 +131,6 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   KT(50);
 #pragma unroll
   for (int c = 0; c < C; ++c) part[stripe][lane + 64 * c] = acc[c];
-#pragma unroll
-  for (int j = 0; j < VPW; ++j) {
-    const int v = wave + 4 * j;
-    if (v < nvec)
-#pragma unroll
-      for (int c = 0; c < C; ++c) xs[v][lane + 64 * c] = ((zero_mask >> j) & 1u) || !live[c] ? 0.0f : vv[j][c];
-  }
   lds_barrier();
   KT(51);
   KTB(2);
@@ -168,43 +160,63 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   lds_barrier();
   KT(52);
   KTB(3);
-  // ---- dot columns: 4 lanes per column, 32 exact fp64 products each, fixed order ----
-  // history columns 6i + {0..5}: S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g ; then the 8 self columns
-  // s.s s.y y.y g.s g.y g.g g.p w.w at 6m + q.
-  const int nh = 6 * count0, ncu = nh + 8;
-  const int q = t & 3;
-  for (int base = 0; base < 4 * ncu; base += 256) {
-    const int u = (base + t) >> 2;
-    double d = 0.0;
-    int c = -1;
-    if (u < ncu) {
-      const float *A, *B;
-      if (u < nh) {
-        const int i = u / 6, r = u - 6 * i;
-        A = xs[(r & 1) ? count0 + i : i];
-        B = ops[r >> 1];
-        c = u;
-      } else {
-        const int z = u - nh; // (s,s) (s,y) (y,y) (g,s) (g,y) (g,g) (g,p) (w,w)
-        const int ia = (0x42222100 >> (4 * z)) & 0xF, ib = (0x43210110 >> (4 * z)) & 0xF;
-        A = ops[ia];
-        B = ops[ib];
-        c = 6 * h.m + z;
-      }
-      const f32x4 *A4 = reinterpret_cast<const f32x4 *>(A + (TC / 4) * q);
-      const f32x4 *B4 = reinterpret_cast<const f32x4 *>(B + (TC / 4) * q);
+  // ---- dots: every (history vector, new vector) dot is owned by one wave: C exact fp64 products per
+  // lane, a DPP wave sum, lane 0 stores the transposed partial row entry. History columns 6i + {0..5}:
+  // S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g; then the 8 self columns s.s s.y y.y g.s g.y g.g g.p w.w at
+  // 6m + z. (Staging the history values in LDS rows 512 B apart and reducing them by four lanes per column
+  // put every quad of a wave on the same banks.) ----
+  float s_[C], y_[C], g_[C];
 #pragma unroll
-      for (int k = 0; k < TC / 16; ++k) {
-        const f32x4 x = A4[k], y = B4[k];
-        d += double(x[0]) * double(y[0]);
-        d += double(x[1]) * double(y[1]);
-        d += double(x[2]) * double(y[2]);
-        d += double(x[3]) * double(y[3]);
+  for (int c = 0; c < C; ++c) {
+    s_[c] = ops[0][lane + 64 * c];
+    y_[c] = ops[1][lane + 64 * c];
+    g_[c] = ops[2][lane + 64 * c];
+  }
+  double *rows = a.rows + blockIdx.x;
+  const long long nb = a.nb;
+#pragma unroll
+  for (int j = 0; j < VPW; ++j) {
+    const int v = wave + 4 * j; // wave-uniform
+    if (v >= nvec) break;
+    double ds = 0.0, dy = 0.0, dg = 0.0;
+    if (!((zero_mask >> j) & 1u)) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const double x = live[c] ? double(vv[j][c]) : 0.0;
+        ds += x * double(s_[c]);
+        dy += x * double(y_[c]);
+        dg += x * double(g_[c]);
       }
     }
-    d += dpp_f64<0xB1, 0xF>(d); // quad_perm [1,0,3,2]
-    d += dpp_f64<0x4E, 0xF>(d); // quad_perm [2,3,0,1]: every lane of the quad holds the same sum
-    if (c >= 0 && q == 0) a.rows[(long long)c * a.nb + blockIdx.x] = d;
+    ds = t_wave_sum(ds);
+    dy = t_wave_sum(dy);
+    dg = t_wave_sum(dg);
+    if (lane == 0) {
+      const int li = v < count0 ? v : v - count0, cc = v < count0 ? 0 : 1;
+      rows[(long long)(6 * li + cc + 0) * nb] = ds;
+      rows[(long long)(6 * li + cc + 2) * nb] = dy;
+      rows[(long long)(6 * li + cc + 4) * nb] = dg;
+    }
+  }
+  if (wave == 3) {
+    double d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const double sv = s_[c], yv = y_[c], gv = g_[c], pvv = ops[3][lane + 64 * c], wvv = ops[4][lane + 64 * c];
+      d[0] += sv * sv;
+      d[1] += sv * yv;
+      d[2] += yv * yv;
+      d[3] += gv * sv;
+      d[4] += gv * yv;
+      d[5] += gv * gv;
+      d[6] += gv * pvv;
+      d[7] += wvv * wvv;
+    }
+#pragma unroll
+    for (int z = 0; z < 8; ++z) d[z] = t_wave_sum(d[z]);
+    if (lane == 0)
+#pragma unroll
+      for (int z = 0; z < 8; ++z) rows[(long long)(6 * h.m + z) * nb] = d[z];
   }
   KT(54);
   KTB(4);
@@ -214,8 +226,10 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
 }
 
 // dots[c] = sum over rows in row order (per-thread strided rows, then a fixed tree); rows are stored
-// transposed ([nc][nb]), so each block reads one contiguous column.
-__device__ __forceinline__ void tail_cols_body(const TailArgs &a) {
+// transposed ([nc][nb]), so each block reads one contiguous column. HANDOFF (tail_cols_fin): the sum is
+// stored write-through (agent-scope relaxed store = sc1) and waited for, so the arrival counter's add
+// publishes it without a release fence (MI355X_MICROARCH.md hand-off table, first row).
+template <bool HANDOFF> __device__ __forceinline__ void tail_cols_body(const TailArgs &a) {
   __shared__ double ws[4];
   const int c = blockIdx.x, t = threadIdx.x;
   const int count0 = a.h.ist[IST_COUNT];
@@ -236,12 +250,20 @@ __device__ __forceinline__ void tail_cols_body(const TailArgs &a) {
   s = t_wave_sum(s);
   if ((t & 63) == 0) ws[t >> 6] = s;
   lds_barrier();
-  if (t == 0) a.dots[c] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+  if (t == 0) {
+    const double d = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+    if constexpr (HANDOFF) {
+      __hip_atomic_store(&a.dots[c], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      a.dots[c] = d;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void tail_cols_kernel(const TailArgs a) {
   if (a.ra.abort && *a.ra.abort) return;
-  tail_cols_body(a);
+  tail_cols_body<false>(a);
 }
 
 constexpr int TF_THREADS = 256;
@@ -270,7 +292,8 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
   double sse = 0.0;
   if (!a.hilo)
     for (int r = t; r < ra.nsse; r += TF_THREADS) sse += ra.sse_part[r];
-  for (int q = t; q < a.nc; q += TF_THREADS) sm.dots[q] = a.dots[q];
+  for (int q = t; q < a.nc; q += TF_THREADS) // sc1 loads: written this launch by other blocks (hand-off)
+    sm.dots[q] = __hip_atomic_load(&a.dots[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int i = t; i < S_ * S_; i += TF_THREADS) {
     SYp[i] = h.SY[i];
     YYp[i] = h.YY[i];
@@ -379,19 +402,17 @@ __global__ __launch_bounds__(TF_THREADS) void tail_fin_kernel(const TailArgs a) 
 }
 
 // tail_cols, then (cols_done) the last block to finish runs the one-block fin: one launch fewer on
-// the iteration's critical path. Release: each block's dots store, fence, arrival; acquire: the last
-// arrival fences before reading the other blocks' dots (agent scope: the blocks span XCDs' L2s).
+// the iteration's critical path. Hand-off without fences (the guide prices __threadfence at ~3.5 us):
+// each block's column sum is an sc1 (write-through) store waited for with vmcnt(0) before the same lane's
+// agent-scope add; the block whose add returns the last count reads the sums with sc1 loads.
 __global__ __launch_bounds__(TF_THREADS) void tail_cols_fin_kernel(const TailArgs a) {
   if (a.ra.abort && *a.ra.abort) return; // uniform for the launch: nobody arrives, the counter stays 0
-  tail_cols_body(a);
+  tail_cols_body<true>(a);
   __shared__ int s_last;
-  if (threadIdx.x == 0) {
-    __threadfence();
-    s_last = atomicAdd(a.cols_done, 1u) == gridDim.x - 1;
-  }
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(a.cols_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
   if (threadIdx.x == 0) *a.cols_done = 0u; // ready for the next launch (stream-ordered)
   tail_fin_body(a);
 }

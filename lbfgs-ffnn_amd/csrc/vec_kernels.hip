@@ -889,18 +889,25 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
   const int nwg = gram_nwg(a.h.n);
   const long long chunk = gram_chunk(a.h.n, nwg);
   const size_t shmem = size_t(3 * chunk) * sizeof(float);
+  // 16-B loads in flight per lane while streaming a history vector (LBF_GRAM_U: 4 or 8)
+  static const int U = env_int("LBF_GRAM_U", 4) >= 8 ? 8 : 4;
   static bool attr_set = false;
   if (!attr_set && shmem > 64 * 1024) {
-    LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gram_kernel<4, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
-    LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(gram_kernel<4, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+    for (const void *f : {reinterpret_cast<const void *>(gram_kernel<4, false>),
+                          reinterpret_cast<const void *>(gram_kernel<4, true>),
+                          reinterpret_cast<const void *>(gram_kernel<8, false>),
+                          reinterpret_cast<const void *>(gram_kernel<8, true>)})
+      LBF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
     attr_set = true;
   }
-  if (hist_nt(a.h))
-    hipLaunchKernelGGL((gram_kernel<4, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
-  else
-    hipLaunchKernelGGL((gram_kernel<4, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
+  const bool nt = hist_nt(a.h);
+  if (U == 8) {
+    if (nt) hipLaunchKernelGGL((gram_kernel<8, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
+    else hipLaunchKernelGGL((gram_kernel<8, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
+  } else {
+    if (nt) hipLaunchKernelGGL((gram_kernel<4, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
+    else hipLaunchKernelGGL((gram_kernel<4, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
+  }
   LBF_KERNEL_CHECK();
 }
 

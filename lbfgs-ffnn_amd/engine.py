@@ -101,6 +101,21 @@ class Context:
         """Time only every `every`-th launch of the selected sections."""
         check(lib().lbf_prof_sample(self.h, int(every)), "lbf_prof_sample")
 
+    def prof_read_work(self):
+        """{section name: work units of the timed launches} (GEMM sections: batch rows)."""
+        n = C.c_int(0)
+        check(lib().lbf_prof_read_work(self.h, 0, None, None, C.byref(n)), "lbf_prof_read_work")
+        cap = n.value
+        ids = (C.c_int * max(cap, 1))()
+        work = (C.c_double * max(cap, 1))()
+        check(lib().lbf_prof_read_work(self.h, cap, ids, work, C.byref(n)), "lbf_prof_read_work")
+        out = {}
+        for i in range(min(cap, n.value)):
+            kind, layer = divmod(ids[i], 16)
+            name = self.PROF_KINDS[kind] if kind < len(self.PROF_KINDS) else f"k{kind}"
+            out[f"{name}[{layer}]"] = work[i]
+        return out
+
     def prof_read(self):
         """{section name: (total ms, launches)}; section = kind[layer]."""
         n = C.c_int(0)

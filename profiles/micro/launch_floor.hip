@@ -58,12 +58,9 @@ __global__ void publish_dev_k(Rec *r, int seq) {
   }
 }
 
-struct BigArgs { double v[192]; }; // 1.5 KB of kernel arguments, like RedAllArgs / TailArgs
-__global__ void big_arg_k(const BigArgs a, double *out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0 && a.v[0] < -1.0) out[0] = a.v[191];
-}
 
 int main() {
+  setvbuf(stdout, nullptr, _IONBF, 0); // a crash keeps the lines printed so far
   double *buf, *out;
   const long long N = 1 << 22;
   CK(hipMalloc(&buf, N * 8));
@@ -120,9 +117,7 @@ int main() {
       CK(hipStreamSynchronize(s));
       printf("%-58s %8.2f us/call (host)\n", name, std::chrono::duration<double, std::micro>(t1 - t0).count() / R2);
     };
-    BigArgs big{};
     host_rate("host: hipLaunchKernelGGL empty<<<1,64>>>", [&] { hipLaunchKernelGGL(empty_k, 1, 64, 0, s); });
-    host_rate("host: hipLaunchKernelGGL big_arg_k (1.5 KB args)", [&] { hipLaunchKernelGGL(big_arg_k, 1, 64, 0, s, big, out); });
     host_rate("host: hipEventRecord", [&] { hipEventRecord(m, s); });
     host_rate("host: hipStreamWaitEvent", [&] { hipStreamWaitEvent(s, m, 0); });
   }
@@ -147,6 +142,42 @@ int main() {
     });
     CK(hipHostFree(hrec));
     CK(hipFree(drec));
+  }
+  // cross-stream hand-off per step: s2 waits for s's work, then s waits for s2's (the S-LBFGS twin's
+  // pattern): with events, and with stream memory operations (write / wait on a device word)
+  {
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    hipEvent_t e1, e2;
+    CK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+    unsigned *flag;
+    CK(hipMalloc(&flag, 64));
+    CK(hipMemset(flag, 0, 64));
+    unsigned seq = 0;
+    time("ping-pong s -> s2 -> s, events (per round trip)", [&] {
+      hipLaunchKernelGGL(empty_k, 1, 64, 0, s);
+      hipEventRecord(e1, s);
+      hipStreamWaitEvent(s2, e1, 0);
+      hipLaunchKernelGGL(empty_k, 1, 64, 0, s2);
+      hipEventRecord(e2, s2);
+      hipStreamWaitEvent(s, e2, 0);
+    });
+    time("ping-pong s -> s2 -> s, stream write/wait value", [&] {
+      ++seq;
+      hipLaunchKernelGGL(empty_k, 1, 64, 0, s);
+      hipStreamWriteValue32(s, flag, 2 * seq, 0);
+      hipStreamWaitValue32(s2, flag, 2 * seq, hipStreamWaitValueGte, 0xffffffffu);
+      hipLaunchKernelGGL(empty_k, 1, 64, 0, s2);
+      hipStreamWriteValue32(s2, flag + 16, 2 * seq, 0);
+      hipStreamWaitValue32(s, flag + 16, 2 * seq, hipStreamWaitValueGte, 0xffffffffu);
+    });
+    time("two empty launches, one stream (reference)", [&] {
+      hipLaunchKernelGGL(empty_k, 1, 64, 0, s);
+      hipLaunchKernelGGL(empty_k, 1, 64, 0, s);
+    });
+    CK(hipStreamSynchronize(s2));
+    CK(hipStreamDestroy(s2));
   }
   // dependent chains of 10 launches at several grid sizes: eager, and the same chain as one hipGraph
   for (int nb : {1, 16, 64, 256, 1024}) {

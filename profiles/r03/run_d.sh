@@ -6,7 +6,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r03d
 mkdir -p $O
 cd $R
-timeout -k 10 90 ./profiles/micro/launch_floor > $O/launch_floor.txt 2>&1 || { echo "launch_floor failed"; exit 1; }
+timeout -k 10 90 ./profiles/micro/launch_floor > $O/launch_floor.txt 2>&1 || echo "launch_floor failed"
 timeout -k 10 200 python -u profiles/r03/dbg_slbfgs_ranks.py > $O/dbg_slbfgs.log 2>&1 || { echo "dbg failed"; tail -5 $O/dbg_slbfgs.log; }
 timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -k "ranks or dp or slbfgs or cfg4 or armijo or spec" > $O/tests.log 2>&1
 echo "tests rc=$?"; grep -E "FAILED|passed|failed" $O/tests.log | tail -8

@@ -222,14 +222,15 @@ def test_ranks_empty_share_lbfgs(ctx, pkg):
 @pytest.mark.parametrize("world,kw", [
     (2, dict(M=5, L=4, b=32, b_H=16)),
     (3, dict(M=5, L=4, b=32, b_H=16)),
-    (2, dict(M=5, L=4, b=1, b_H=1)),            # b < world: a rank's minibatch slice is empty
+    (2, dict(M=5, L=4, b=1, b_H=1, step=0.002)),  # b < world: a rank's slice is empty (0.02 diverges at b = 1)
     (2, dict(M=5, L=4, b=32, b_H=1, hvp_exact=1)),  # exact HVP with b_H < world
 ])
 def test_ranks_slbfgs_equals_single(ctx, pkg, world, kw):
     dims, acts, N = [784, 16, 10], ["relu", "linear"], 512 if kw["b"] > 1 else 64
     Xh, Yh = pkg.synth_mnist(N)
     X, Y = dev(Xh), dev(Yh)
-    args = dict(step=0.02, max_epochs=2, tol=0.0, lam=1e-4, **kw)
+    args = dict(step=0.02, max_epochs=2, tol=0.0, lam=1e-4)
+    args.update(kw)
     net1 = pkg.Mlp(ctx, dims, acts)
     P0 = net1.init_params(123, "cpu")
     P1 = P0.clone()
