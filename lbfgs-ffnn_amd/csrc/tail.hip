@@ -45,6 +45,7 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   const RedAllArgs &ra = a.ra;
   if (ra.abort && *ra.abort) return;
   __shared__ double part[4][TC];
+  __shared__ float xs[2 * TAIL_MAXM][TC]; // this group's values of the live history vectors
   __shared__ float ops[5][TC];            // s, y, g, p, w
   __shared__ int ist[IST_ORDER + TAIL_MAXM];
   const HistView &h = a.h;
@@ -131,6 +132,13 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   KT(50);
 #pragma unroll
   for (int c = 0; c < C; ++c) part[stripe][lane + 64 * c] = acc[c];
+#pragma unroll
+  for (int j = 0; j < VPW; ++j) {
+    const int v = wave + 4 * j;
+    if (v < nvec)
+#pragma unroll
+      for (int c = 0; c < C; ++c) xs[v][lane + 64 * c] = ((zero_mask >> j) & 1u) || !live[c] ? 0.0f : vv[j][c];
+  }
   lds_barrier();
   KT(51);
   KTB(2);
@@ -160,63 +168,43 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   lds_barrier();
   KT(52);
   KTB(3);
-  // ---- dots: every (history vector, new vector) dot is owned by one wave: C exact fp64 products per
-  // lane, a DPP wave sum, lane 0 stores the transposed partial row entry. History columns 6i + {0..5}:
-  // S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g; then the 8 self columns s.s s.y y.y g.s g.y g.g g.p w.w at
-  // 6m + z. (Staging the history values in LDS rows 512 B apart and reducing them by four lanes per column
-  // put every quad of a wave on the same banks.) ----
-  float s_[C], y_[C], g_[C];
+  // ---- dot columns: 4 lanes per column, 32 exact fp64 products each, fixed order ----
+  // history columns 6i + {0..5}: S_i.s, Y_i.s, S_i.y, Y_i.y, S_i.g, Y_i.g ; then the 8 self columns
+  // s.s s.y y.y g.s g.y g.g g.p w.w at 6m + q.
+  const int nh = 6 * count0, ncu = nh + 8;
+  const int q = t & 3;
+  for (int base = 0; base < 4 * ncu; base += 256) {
+    const int u = (base + t) >> 2;
+    double d = 0.0;
+    int c = -1;
+    if (u < ncu) {
+      const float *A, *B;
+      if (u < nh) {
+        const int i = u / 6, r = u - 6 * i;
+        A = xs[(r & 1) ? count0 + i : i];
+        B = ops[r >> 1];
+        c = u;
+      } else {
+        const int z = u - nh; // (s,s) (s,y) (y,y) (g,s) (g,y) (g,g) (g,p) (w,w)
+        const int ia = (0x42222100 >> (4 * z)) & 0xF, ib = (0x43210110 >> (4 * z)) & 0xF;
+        A = ops[ia];
+        B = ops[ib];
+        c = 6 * h.m + z;
+      }
+      const f32x4 *A4 = reinterpret_cast<const f32x4 *>(A + (TC / 4) * q);
+      const f32x4 *B4 = reinterpret_cast<const f32x4 *>(B + (TC / 4) * q);
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    s_[c] = ops[0][lane + 64 * c];
-    y_[c] = ops[1][lane + 64 * c];
-    g_[c] = ops[2][lane + 64 * c];
-  }
-  double *rows = a.rows + blockIdx.x;
-  const long long nb = a.nb;
-#pragma unroll
-  for (int j = 0; j < VPW; ++j) {
-    const int v = wave + 4 * j; // wave-uniform
-    if (v >= nvec) break;
-    double ds = 0.0, dy = 0.0, dg = 0.0;
-    if (!((zero_mask >> j) & 1u)) {
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const double x = live[c] ? double(vv[j][c]) : 0.0;
-        ds += x * double(s_[c]);
-        dy += x * double(y_[c]);
-        dg += x * double(g_[c]);
+      for (int k = 0; k < TC / 16; ++k) {
+        const f32x4 x = A4[k], y = B4[k];
+        d += double(x[0]) * double(y[0]);
+        d += double(x[1]) * double(y[1]);
+        d += double(x[2]) * double(y[2]);
+        d += double(x[3]) * double(y[3]);
       }
     }
-    ds = t_wave_sum(ds);
-    dy = t_wave_sum(dy);
-    dg = t_wave_sum(dg);
-    if (lane == 0) {
-      const int li = v < count0 ? v : v - count0, cc = v < count0 ? 0 : 1;
-      rows[(long long)(6 * li + cc + 0) * nb] = ds;
-      rows[(long long)(6 * li + cc + 2) * nb] = dy;
-      rows[(long long)(6 * li + cc + 4) * nb] = dg;
-    }
-  }
-  if (wave == 3) {
-    double d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const double sv = s_[c], yv = y_[c], gv = g_[c], pvv = ops[3][lane + 64 * c], wvv = ops[4][lane + 64 * c];
-      d[0] += sv * sv;
-      d[1] += sv * yv;
-      d[2] += yv * yv;
-      d[3] += gv * sv;
-      d[4] += gv * yv;
-      d[5] += gv * gv;
-      d[6] += gv * pvv;
-      d[7] += wvv * wvv;
-    }
-#pragma unroll
-    for (int z = 0; z < 8; ++z) d[z] = t_wave_sum(d[z]);
-    if (lane == 0)
-#pragma unroll
-      for (int z = 0; z < 8; ++z) rows[(long long)(6 * h.m + z) * nb] = d[z];
+    d += dpp_f64<0xB1, 0xF>(d); // quad_perm [1,0,3,2]
+    d += dpp_f64<0x4E, 0xF>(d); // quad_perm [2,3,0,1]: every lane of the quad holds the same sum
+    if (c >= 0 && q == 0) a.rows[(long long)c * a.nb + blockIdx.x] = d;
   }
   KT(54);
   KTB(4);

@@ -104,23 +104,6 @@ int main() {
     hipLaunchKernelGGL(write_k, (unsigned)(N / 256), 256, 0, s, buf, N);
     hipLaunchKernelGGL(onesum_k, 1, 1024, 0, s, buf, 8192LL, out);
   });
-  // host-side cost of enqueueing (no dependency wait: the GPU runs empty kernels faster than the host
-  // submits them, so host time / call is the submission cost)
-  {
-    auto host_rate = [&](const char *name, auto body) {
-      for (int i = 0; i < 200; ++i) body();
-      CK(hipStreamSynchronize(s));
-      const int R2 = 4000;
-      auto t0 = std::chrono::steady_clock::now();
-      for (int i = 0; i < R2; ++i) body();
-      auto t1 = std::chrono::steady_clock::now();
-      CK(hipStreamSynchronize(s));
-      printf("%-58s %8.2f us/call (host)\n", name, std::chrono::duration<double, std::micro>(t1 - t0).count() / R2);
-    };
-    host_rate("host: hipLaunchKernelGGL empty<<<1,64>>>", [&] { hipLaunchKernelGGL(empty_k, 1, 64, 0, s); });
-    host_rate("host: hipEventRecord", [&] { hipEventRecord(m, s); });
-    host_rate("host: hipStreamWaitEvent", [&] { hipStreamWaitEvent(s, m, 0); });
-  }
   // what a kernel that publishes to host-mapped memory costs its successor (tail_cols_fin -> combine)
   {
     Rec *hrec, *drec;
@@ -210,6 +193,21 @@ int main() {
     printf("%-58s %8.2f us\n", nm, ms * 1e3f / (R * 10));
     CK(hipGraphExecDestroy(ge));
     CK(hipGraphDestroy(g));
+  }
+  // host-side cost of enqueueing (no dependency wait: the GPU runs empty kernels faster than the host
+  // submits them, so host time / call is the submission cost)
+  {
+    auto host_rate = [&](const char *name, auto body) {
+      for (int i = 0; i < 200; ++i) body();
+      CK(hipStreamSynchronize(s));
+      const int R2 = 4000;
+      auto t0 = std::chrono::steady_clock::now();
+      for (int i = 0; i < R2; ++i) body();
+      auto t1 = std::chrono::steady_clock::now();
+      CK(hipStreamSynchronize(s));
+      printf("%-58s %8.2f us/call (host)\n", name, std::chrono::duration<double, std::micro>(t1 - t0).count() / R2);
+    };
+    host_rate("host: hipLaunchKernelGGL empty<<<1,64>>>", [&] { hipLaunchKernelGGL(empty_k, 1, 64, 0, s); });
   }
   return 0;
 }
