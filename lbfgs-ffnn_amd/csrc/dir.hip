@@ -56,12 +56,16 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
   unsigned zero_mask = 0; // bit j: vector j of this wave is not live (or is the slot being overwritten)
 #pragma unroll
   for (int j = 0; j < VPW; ++j) {
-    const int v = wave + 4 * j;
-    const int vi = v < nvec ? v : 0;
-    const int slot = __builtin_amdgcn_readfirstlane(ist[IST_ORDER + (vi < count0 ? vi : vi - count0)]);
-    const float *base = (vi < count0 ? h.S : h.Y) + (long long)slot * h.ld;
-    vv[j] = *reinterpret_cast<const f32x4 *>(base + e4);
-    if (v >= nvec || (g.has_pair && slot == w)) zero_mask |= 1u << j;
+    const int v = wave + 4 * j; // wave-uniform: the branch is scalar, no per-lane wait
+    vv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (v < nvec) {
+      const int slot = __builtin_amdgcn_readfirstlane(ist[IST_ORDER + (v < count0 ? v : v - count0)]);
+      const float *base = (v < count0 ? h.S : h.Y) + (long long)slot * h.ld;
+      vv[j] = *reinterpret_cast<const f32x4 *>(base + e4);
+      if (g.has_pair && slot == w) zero_mask |= 1u << j;
+    } else {
+      zero_mask |= 1u << j;
+    }
   }
   if (wave == 0) { // the new vectors of the group (null operands read ga / sa and are masked)
     const float *dflt = g.has_g ? g.ga : g.sa;
