@@ -112,6 +112,14 @@ int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const 
  * Replaces, as an option, the finite-difference HVP of s_lbfgs.hpp:88-101. */
 int lbf_mlp_hvp(lbf_mlp *net, const float *d_params, const float *d_v, const float *d_X, const float *d_Y,
                 const int *d_idx, long long batch, double inv_scale, double l2, float *d_hv);
+/* Per-minibatch gradients at one point (extension; the reference evaluates them one step at a time:
+ * SLBFGS::stochastic_solve's batch_g(w) of every inner step, s_lbfgs.hpp:218-230, at the epoch's fixed anchor
+ * w): rows [t cnt, (t+1) cnt) of d_X / d_Y are minibatch t, t < nmb; its gradient of
+ * 0.5 inv_scale ||net - Y||^2 + 0.5 l2 ||w||^2 is written to d_grads + t ld (ld >= param count). One
+ * evaluation over nmb cnt rows whose dW GEMMs split K at the minibatch boundaries. cnt % 32 == 0.
+ * Single rank only (a communicator's ranks would each hold partial sums). */
+int lbf_mlp_batch_grads(lbf_mlp *net, const float *d_params, const float *d_X, const float *d_Y, int nmb,
+                        long long cnt, double inv_scale, double l2, float *d_grads, long long ld);
 /* Loss only (CudaNetwork::forward_only, network.cuh:79-88, + the MSE of network.cuh:105; the CPU f closure of
  * unified_optimization.hpp:101-108): forward pass and 0.5 * inv_scale * ||out - Y||^2 (summed over ranks with a
  * communicator), bitwise the loss lbf_mlp_loss_grad reports for the same point. */

@@ -93,6 +93,8 @@ def lib():
         "lbf_init_params_host": (C.c_int, [C.c_int, _ip, _ip, C.c_uint, C.c_int, _vp]),
         "lbf_mlp_forward": (C.c_int, [_vp, _vp, _vp, C.c_longlong, _vp]),
         "lbf_mlp_loss_grad": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_longlong, C.c_double, C.c_double, _dp]),
+        "lbf_mlp_batch_grads": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int, C.c_longlong, C.c_double, C.c_double, _vp,
+                                          C.c_longlong]),
         "lbf_two_loop": (C.c_int, [_vp, C.c_longlong, C.c_int, _vp, _vp, _dp, _vp, _vp, C.c_int]),
         "lbf_dot": (C.c_int, [_vp, C.c_longlong, _vp, _vp, _dp]),
         "lbf_nrm2": (C.c_int, [_vp, C.c_longlong, _vp, _dp]),
@@ -146,7 +148,7 @@ def lib():
 
 EXPORTS = ("lbf_last_error lbf_version lbf_abi_version lbf_ctx_create lbf_ctx_destroy lbf_ctx_sync lbf_ctx_stream "
            "lbf_comm_unique_id lbf_comm_init lbf_comm_init_local lbf_comm_rank lbf_allreduce_sum lbf_mlp_create lbf_mlp_destroy "
-           "lbf_mlp_param_count lbf_mlp_init_params lbf_init_params_host lbf_mlp_forward lbf_mlp_loss_grad lbf_two_loop lbf_dot "
+           "lbf_mlp_param_count lbf_mlp_init_params lbf_init_params_host lbf_mlp_forward lbf_mlp_loss_grad lbf_mlp_batch_grads lbf_two_loop lbf_dot "
            "lbf_nrm2 lbf_axpy lbf_scal lbf_lbfgs_default_params lbf_slbfgs_default_params lbf_lbfgs_solve "
            "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_prof_enable lbf_prof_select lbf_prof_sample lbf_prof_read lbf_prof_read_work lbf_synth_mnist "
            "lbf_sample_indices lbf_synth_regression lbf_gd_default_params lbf_sgd_default_params lbf_gd_solve "

@@ -240,6 +240,18 @@ int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const 
   });
 }
 
+int lbf_mlp_batch_grads(lbf_mlp *net, const float *d_params, const float *d_X, const float *d_Y, int nmb,
+                        long long cnt, double inv_scale, double l2, float *d_grads, long long ld) {
+  return guard([&] {
+    LBF_REQUIRE(net && d_params && d_X && d_Y && d_grads && nmb > 0 && cnt > 0, "bad argument");
+    lbf_ctx *c = net->ctx;
+    LBF_REQUIRE(!c->c.dp(), "lbf_mlp_batch_grads: single rank only");
+    c->c.set_device();
+    net->net->batch_grads(d_params, d_X, d_Y, nmb, cnt, inv_scale, l2, d_grads, ld, false);
+    LBF_HIP(hipStreamSynchronize(c->c.stream));
+  });
+}
+
 int lbf_mlp_loss(lbf_mlp *net, const float *d_params, const float *d_X, const float *d_Y, const int *d_idx,
                  long long batch, double inv_scale, double *h_loss) {
   return guard([&] {

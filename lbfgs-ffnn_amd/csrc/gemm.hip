@@ -57,6 +57,9 @@ struct GemmK {
   float *head_delta, *head_slab;
   double *head_sse;
   int head_fold, head_fold_c0;
+  unsigned *fin_cnt;
+  float *fin_out;
+  int nsplits;
 };
 
 // Side job (see GemmDesc): one 256-column group (four per lane) x 4 split stripes per block, fp64 in
@@ -245,6 +248,63 @@ __device__ __forceinline__ void store_mc(float *lds, const f32x4 (&r)[R / 32], i
 
 // Epilogues shared by both main loops: the fused output layer (EPI_HEAD) or the bias/activation/
 // derivative/slab store of the accumulators.
+typedef __attribute__((address_space(1))) float gfloat_t;
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+
+// In-launch split-K reduction (GemmDesc::fin_cnt), the hand-off of MI355X_MICROARCH.md's visibility table,
+// first row (cdna_hip_programming.md's split-K recipe, sc1 variant): every split stored its slab tile with
+// sc1 (write-through) stores; each storing wave drains them (vmcnt(0)), the workgroup barrier, then ONE
+// lane's relaxed agent-scope add on the tile's counter. The workgroup whose add returns nsplits - 1 reads
+// every slab of the tile with sc1 buffer loads (no acquire fence needed for them), in split order.
+template <int BM, int BN, int KW>
+__device__ __forceinline__ void gemm_fin_reduce(const GemmK &g, float *lds, int m0, int n0) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int *flag = reinterpret_cast<int *>(lds); // the staging array is free: every k-step is done
+  if (threadIdx.x == 0) {
+    gu32_t *cnt = (gu32_t *)(g.fin_cnt + (int(blockIdx.y) * int(gridDim.x) + int(blockIdx.x)));
+    const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == unsigned(g.nsplits - 1) ? 1 : 0;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // next launch (stream-ordered)
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); // compiler-only: the slab loads stay below
+  constexpr int NT = 256 * KW, Q = BN / 4, RP = NT / Q; // 16-B column groups per row, rows per pass
+  static_assert(NT % Q == 0 && BM % RP == 0, "fin: tile shape");
+  const int ns = g.nsplits;
+  const unsigned plane = unsigned(g.slab_stride) * 4u; // bytes per split (host-checked < 2^31 in all)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(g.C), 0, int(unsigned(ns) * plane), 0x00020000);
+#pragma unroll
+  for (int r0 = 0; r0 < BM; r0 += RP) {
+    const int m = m0 + r0 + int(threadIdx.x) / Q, n = n0 + 4 * (int(threadIdx.x) % Q);
+    const bool ok = m < g.M && n < g.N;
+    const unsigned off = ok ? unsigned((long long)m * g.ldc + n) * 4u : 0u;
+    f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+    int k = 0;
+    for (; k + 8 <= ns; k += 8) { // eight 16-B loads in flight, summed in split order
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, int(off + unsigned(k + u) * plane),
+                                                                                0, 16)); // aux 16 = sc1
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; k < ns; ++k)
+      acc += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, int(off + unsigned(k) * plane), 0, 16));
+    if (ok) {
+      const f32x4 b = g.bias ? *reinterpret_cast<const f32x4 *>(g.bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = act_rt(g.act, acc[j] + b[j]); // fwd_reduce_act's expression
+      *reinterpret_cast<f32x4 *>(g.fin_out + (long long)m * g.N + n) = o;
+    }
+  }
+}
+
 template <int WM, int WN, int TM, int TN, int EPI, int KW, class HPre>
 __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][TN], float *lds, HPre &hpre, int zsplit,
                                               int m0, int n0, int wm, int wn, int li, int lh, int kgrp) {
@@ -335,7 +395,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
     KTB(7);
     return;
   }
-  if (KW > 1 && kgrp != 0) return; // group 0 holds the sums
+  const bool fin = EPI == EPI_STORE && g.fin_cnt != nullptr; // uniform: every wave joins the reduction
+  if (KW > 1 && kgrp != 0) {
+    if constexpr (EPI == EPI_STORE)
+      if (fin) gemm_fin_reduce<BM, BN, KW>(g, lds, m0, n0);
+    return; // group 0 holds the sums
+  }
   // Epilogue: lanes 0-31 own consecutive columns -> each register row is a 128-B coalesced store.
   float *C = g.C + (EPI == EPI_STORE ? (long long)zsplit * g.slab_stride : 0LL);
   // EPI_DX's act' operand (the previous layer's activations) is loaded for the whole (tm, tn) block before
@@ -367,11 +432,19 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
           float v = acc[tm][tn][r];
           if constexpr (EPI == EPI_FWD) v = act_c<A>(v + bn);
           if constexpr (EPI == EPI_DX) v *= dact_c<A>(ax[r]);
-          if (nok && m < g.M) C[(long long)m * g.ldc + n] = v;
+          if (nok && m < g.M) {
+            if (EPI == EPI_STORE && fin) // write-through for the in-launch reduction
+              __hip_atomic_store((gfloat_t *)(C + (long long)m * g.ldc + n), v, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            else
+              C[(long long)m * g.ldc + n] = v;
+          }
         }
       }
     }
   });
+  if constexpr (EPI == EPI_STORE)
+    if (fin) gemm_fin_reduce<BM, BN, KW>(g, lds, m0, n0);
 }
 
 // KW k-groups of 4 waves each (KW = 2: 8 waves, two per SIMD, for tiles too small to fill the chip
@@ -921,6 +994,9 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.head_sse = d.head_sse;
   k.head_fold = d.head_fold;
   k.head_fold_c0 = d.head_fold_c0;
+  k.fin_cnt = d.fin_cnt;
+  k.fin_out = d.fin_out;
+  k.nsplits = d.splits > 1 ? d.splits : 1;
   dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
   static const bool glds_on = env_int("LBF_GEMM_GLDS", 1) != 0;
   if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
@@ -993,8 +1069,22 @@ int gemm_row_tiles(int M, int tile) {
   return (M + BM - 1) / BM;
 }
 
+long long gemm_tiles(const GemmDesc &d) {
+  int BM, BN;
+  gemm_tile_for(d.N, d.tile, &BM, &BN);
+  return cdiv((long long)d.M, (long long)BM) * cdiv((long long)d.N, (long long)BN);
+}
+
 void gemm(hipStream_t s, const GemmDesc &d) {
   if (d.M <= 0 || d.N <= 0) return;
+  if (d.fin_cnt) {
+    const long long bytes = (long long)(d.splits > 1 ? d.splits : 1) * d.slab_stride * 4;
+    if (d.epi != EPI_STORE || d.splits < 2 || d.N % 4 || d.ldc != d.N || !d.fin_out || !aligned16(d.C) ||
+        !aligned16(d.fin_out) || (d.bias && !aligned16(d.bias)) || d.slab_stride % 4 || bytes >= (1LL << 31) ||
+        d.side_slab)
+      throw std::runtime_error("gemm: in-launch split-K reduction needs EPI_STORE, >= 2 splits, N % 4 == 0, "
+                               "dense aligned slabs under 2 GiB, no side job");
+  }
   if (d.epi == EPI_HEAD) {
     int BM, BN;
     gemm_tile_for(d.N, d.tile, &BM, &BN);

@@ -69,7 +69,15 @@ struct GemmDesc {
   // accumulated in the epilogue and written in front of the head's rows: the slab per workgroup is
   // then [(head_fold + 1) x N | (N+1) x head_out], and the dW GEMM covers rows < head_fold_c0 only.
   int head_fold = -1, head_fold_c0 = 0;
+  // In-launch split-K reduction (EPI_STORE with splits > 1, N % 4 == 0): every split stores its slab
+  // tile write-through (sc1) and adds to fin_cnt[tile]; the split that arrives last sums the tile's
+  // slabs in split order (bitwise fwd_reduce_act), adds the bias, applies `act` and writes fin_out
+  // ([M][N]). fin_cnt: one zeroed word per output tile (the last arrival re-zeroes its own).
+  unsigned *fin_cnt = nullptr;
+  float *fin_out = nullptr;
 };
+// Output tiles of a GEMM launch (the fin_cnt words it needs)
+long long gemm_tiles(const GemmDesc &d);
 // Row tiles of the forward GEMM for M rows and N columns (== EPI_HEAD partial slabs).
 int gemm_row_tiles(int M, int tile);
 
@@ -199,6 +207,8 @@ void epoch_loss_acc(hipStream_t s, const double *scal, long long rows, float *es
 void average_slots(hipStream_t s, long long n, const float *W, long long ld, const int *h_slots, int cnt, float *u);
 // out = a + c*b
 void lincomb(hipStream_t s, long long n, const float *a, double c, const float *b, float *out);
+// G[r * ld + e] += lambda w[e], r < rows, e < n (finalize_kernel's fp32 update on a block of gradients)
+void add_l2_rows(hipStream_t s, long long n, int rows, long long ld, float *G, const float *w, double lambda);
 void gather_rows(hipStream_t s, const float *src, long long ld, const int *idx, long long count, int cols,
                  float *dst);
 void diff_scale(hipStream_t s, long long n, const float *a, const float *b, float scale, float *out);

@@ -99,6 +99,7 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
   if (const char *e = std::getenv("LBF_DW_TILE64")) dw64_ = e[0] != '0';
   if (const char *e = std::getenv("LBF_NO_FOLD")) fold_on_ = e[0] != '1';
   tail_split_ = env_int("LBF_TAIL_SPLIT", 0) != 0; // 1: tail_fin as its own launch (A/B and tests)
+  fwd_fin_ = env_int("LBF_FWD_FIN", 0) != 0; // measured slower at S-LBFGS minibatches (profiles/r03)
 }
 
 // Split-K factor for `tiles` output tiles over a K of `K` rows: the GEMM tiles run two workgroups per
@@ -341,9 +342,22 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
       d.splits = L.fsplits;
       d.k_chunk = L.fk_chunk;
       d.slab_stride = B * L.out;
+      // the slabs summed inside the launch by each tile's last split (no fwd_reduce_act launch)
+      const bool fin = fwd_fin_ && L.out % 4 == 0 && (B * L.out) % 4 == 0 &&
+                       (long long)L.fsplits * B * L.out * 4 < (1LL << 31);
+      if (fin) {
+        const size_t tiles = size_t(gemm_tiles(d));
+        if (fin_cnt_.size() < tiles) {
+          fin_cnt_.resize(tiles);
+          LBF_HIP(hipMemsetAsync(fin_cnt_.get(), 0, tiles * sizeof(unsigned), s));
+        }
+        d.fin_cnt = fin_cnt_.get();
+        d.fin_out = A_[l].get();
+      }
       ProfScope ps(ctx_, PK_FWD, int(l), double(B));
       gemm(s, d);
-      fwd_reduce_act(s, fslab_.get(), L.fsplits, B * L.out, int(B), L.out, d.bias, L.act, A_[l].get(), ctx_->abort);
+      if (!fin)
+        fwd_reduce_act(s, fslab_.get(), L.fsplits, B * L.out, int(B), L.out, d.bias, L.act, A_[l].get(), ctx_->abort);
     } else {
       ProfScope ps(ctx_, PK_FWD, int(l), double(B));
       gemm(s, d);
@@ -701,6 +715,80 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     ctx_->allreduce(Gl, nparams_ + 2); // one RCCL all-reduce of [grad | sse_hi | sse_lo]
   }
   finish_reduced(P, G, inv_scale, lambda, pdir, scal, hilo_in, Gl != G ? Gl : nullptr);
+}
+
+void Mlp::batch_grads(const float *P, const float *X, const float *Y, int nmb, long long cnt, double inv_scale,
+                      double lambda, float *G, long long ldg, bool local) {
+  LBF_REQUIRE(nmb > 0 && cnt > 0 && cnt % 32 == 0, "batch_grads: minibatches of a multiple of 32 rows");
+  LBF_REQUIRE(ldg >= (long long)nparams_, "batch_grads: gradient stride below the parameter count");
+  hipStream_t s = ctx_->stream;
+  const int nl = int(layers_.size());
+  const Layer &Lo = layers_[nl - 1];
+  const long long R = (long long)nmb * cnt;
+  ensure(R);
+  // forward over every row (no fused head: its [dW ; db] partials are per 64-row tile, not per minibatch)
+  forward(P, X, nullptr, R, nl);
+  {
+    ProfScope ps(ctx_, PK_LOSS);
+    loss_diff(s, A_[nl - 1].get(), Lo.out, Y, Lo.out, nullptr, R, Lo.out, Lo.act, inv_scale, D_[nl - 1].get(),
+              Lo.out, loss_part_.get());
+  }
+  for (int l = nl - 1; l >= 0; --l) {
+    const Layer &L = layers_[l];
+    GemmDesc d; // [dW ; db] of minibatch t = split t of [A_in | 1]^T dZ
+    d.M = L.in + 1;
+    d.N = L.out;
+    d.K = int(R);
+    d.A = (l == 0) ? X : A_[l - 1].get();
+    d.lda = L.in;
+    d.a_kc = false;
+    d.a_mvalid = L.in;
+    d.a_ones = L.in;
+    d.B = D_[l].get();
+    d.ldb = L.out;
+    d.b_kc = false;
+    d.epi = EPI_STORE;
+    d.ldc = L.out;
+    d.splits = nmb;
+    d.k_chunk = int(cnt);
+    d.C = G + L.off;
+    d.slab_stride = ldg;
+    d.abort = ctx_->abort;
+    d.tile = TILE_64x64;
+    {
+      ProfScope ps(ctx_, PK_DW, l, double(R));
+      gemm(s, d);
+    }
+    if (l > 0) {
+      const Layer &P0 = layers_[l - 1];
+      GemmDesc x; // dX = dZ W^T .* act'(A_prev), as backward_phase
+      x.M = int(R);
+      x.N = L.in;
+      x.K = L.out;
+      x.A = D_[l].get();
+      x.lda = L.out;
+      x.a_kc = true;
+      x.B = P + L.off;
+      x.ldb = L.out;
+      x.b_kc = true;
+      x.C = D_[l - 1].get();
+      x.ldc = L.in;
+      x.epi = EPI_DX;
+      x.aux = A_[l - 1].get();
+      x.ldaux = L.in;
+      x.aux_act = P0.act;
+      x.abort = ctx_->abort;
+      x.tile = dx_tile(R, L.in);
+      ProfScope ps(ctx_, PK_DX, l, double(R));
+      gemm(s, x);
+    }
+  }
+  if (!local) {
+    ProfScope ps(ctx_, PK_FINAL, 0);
+    add_l2_rows(s, (long long)nparams_, nmb, ldg, G, P, lambda);
+  }
+  evals_ += nmb;
+  rows_ += R;
 }
 
 // The gradient and status of an all-reduced [G | hi | lo] block: G += lambda w, the dots of the status

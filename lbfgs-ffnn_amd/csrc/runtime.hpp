@@ -129,6 +129,13 @@ public:
   // g_src (nullable): the reduced words are there and the finished gradient is written to G
   void finish_reduced(const float *P, float *G, double inv_scale, double lambda, const float *pdir, double *scal,
                       const float *hilo_in = nullptr, const float *g_src = nullptr);
+  // Per-minibatch gradients at one point P (S-LBFGS's anchor gradients: w is fixed for an epoch): rows
+  // [t cnt, (t+1) cnt) of the gathered X / Y are minibatch t (t < nmb); its gradient, scaled by inv_scale,
+  // goes to G + t ldg (+ lambda P unless local: a data-parallel rank's partial sums). One evaluation over
+  // the nmb cnt rows (full-batch GEMM tiles), whose dW GEMMs split K exactly at the minibatch boundaries
+  // and write split t in place as minibatch t's [dW ; db]: no slab reduction. cnt % 32 == 0.
+  void batch_grads(const float *P, const float *X, const float *Y, int nmb, long long cnt, double inv_scale,
+                   double lambda, float *G, long long ldg, bool local);
   long long loss_only_evals() const { return loss_only_; }
   long long grad_after_loss_evals() const { return gal_; } // backward phases run after a loss_only
   // Exact Hessian-vector product Hv = H(P) V of the same batch loss (+ lambda V), Pearlmutter's
@@ -163,6 +170,10 @@ private:
   long long cap_ = -1, planned_ = -1;
   std::vector<DevBuf<float>> A_, D_;
   DevBuf<float> slab_, head_slab_, fslab_;
+  // arrival counters of the forward GEMMs' in-launch split-K reduction (GemmDesc::fin_cnt), one per
+  // output tile; each launch leaves them zero
+  DevBuf<unsigned> fin_cnt_;
+  bool fwd_fin_ = false; // LBF_FWD_FIN=1: in-launch reduction (the reducer's serial slab read costs more than the launch it saves)
   bool use_head_ = true;      // fused output layer when the shape allows (LBF_NO_HEAD=1 disables)
   bool use_gemm_head_ = true; // ... inside the forward GEMM's epilogue (LBF_NO_GEMM_HEAD=1 disables)
   int fwd_small_ = 1;         // 32x128 forward tiles for few row tiles (LBF_FWD_TILE32=0 disables)

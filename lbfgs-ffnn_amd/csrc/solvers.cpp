@@ -386,14 +386,16 @@ int LbfgsSolver::iterate_armijo(int iters, lbf_record *rec) {
 }
 
 // Spins on the host-mapped record of speculative iteration `seq` (no event: an event record costs
-// ~5 us of idle GPU per iteration). Every ~1 ms of spinning, the stream is queried so a failed launch
-// or an already-drained queue surfaces instead of spinning forever.
+// ~5 us of idle GPU per iteration). Only after 5 ms of spinning is the stream queried, so a failed
+// launch or an already-drained queue surfaces instead of spinning forever: hipStreamQuery enqueues a
+// marker packet behind the last launch, and a query per iteration put a ~6 us idle gap (the marker's
+// release) in front of the first kernel of the iterations enqueued after it (profiles/r03/README.md).
 void LbfgsSolver::wait_record(int seq, SpecRecord *out) {
   volatile SpecRecord *r = spec_rec_ + seq % kSpecRing;
   auto t0 = std::chrono::steady_clock::now();
   for (long long spin = 0;; ++spin) {
     if (__atomic_load_n(&spec_rec_[seq % kSpecRing].seq, __ATOMIC_ACQUIRE) == seq) break;
-    if ((spin & 1023) == 1023) {
+    if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) {
       const hipError_t q = hipStreamQuery(ctx_->stream);
       if (q == hipSuccess) { // queue drained: the record must be there now
         if (__atomic_load_n(&spec_rec_[seq % kSpecRing].seq, __ATOMIC_ACQUIRE) == seq) break;
@@ -437,11 +439,17 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
     Ctx *c;
     ~Clear() { c->abort = nullptr; }
   } clear{ctx_};
+  // LBF_HOST_TIMING=1: where the host thread spends an iteration (enqueue vs waiting for the device)
+  static const int host_timing = env_int("LBF_HOST_TIMING", 0);
+  double t_enq = 0.0, t_wait = 0.0;
+  long long n_wait = 0, n_ready = 0;
+  using clk = std::chrono::steady_clock;
   while (done < iters) {
     if (q.empty() && entry_converged()) {
       converged_ = true;
       break;
     }
+    const auto te0 = clk::now();
     while (issued < iters && int(q.size()) < depth_) {
       Flight f;
       f.roles = roles();
@@ -477,7 +485,16 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
     const Flight f = q.front();
     q.pop_front();
     SpecRecord r;
+    const auto tw0 = clk::now();
+    if (host_timing) {
+      t_enq += std::chrono::duration<double>(tw0 - te0).count();
+      n_ready += __atomic_load_n(&spec_rec_[f.seq % kSpecRing].seq, __ATOMIC_ACQUIRE) == f.seq ? 1 : 0;
+    }
     wait_record(f.seq, &r);
+    if (host_timing) {
+      t_wait += std::chrono::duration<double>(clk::now() - tw0).count();
+      ++n_wait;
+    }
     if (r.seq != f.seq) throw Error(2, "speculative line search: record out of sequence");
     if (f.roles.pair) mark_prev_accepted(rec, r.accept_prev);
     if (r.status == SPEC_REJECT) {
@@ -512,6 +529,9 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
       host_fold = true;
     }
   }
+  if (host_timing && n_wait)
+    std::fprintf(stderr, "[lbf host] spec: %lld records, enqueue %.2f us/iter, wait %.2f us/iter, %lld already there\n",
+                 n_wait, 1e6 * t_enq / double(n_wait), 1e6 * t_wait / double(n_wait), n_ready);
   return done;
 }
 
@@ -568,6 +588,7 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
   hs_.ensure(SC_N);
   evals0_ = net->evals();
   rows0_ = net->rows();
+  anchor_pre_ = env_int("LBF_SLBFGS_ANCHOR", 0) != 0; // the twin measured ~2-3 % faster (profiles/r03)
   if (env_int("LBF_SLBFGS_TWIN", 1)) {
     tctx_.reset(new Ctx());
     tctx_->device = ctx_->device;
@@ -672,33 +693,40 @@ int SlbfgsSolver::run(lbf_record *rec) {
     long long off = 0, cnt = 0, total = 0; // offset / count in this rank's flat list, whole batch size
   };
   struct EpochDraw {
-    std::vector<int> flat, batch;
+    std::vector<int> flat, hflat, batch;
     std::vector<Slice> mb, hb;
     int pick = -1;
     bool u_seen = false; // have_u after the epoch
   };
   MinibatchSampler sampler{size_t(N_)};
+  // The minibatch slices come first in `flat` (minibatch t's rows right after minibatch t-1's, as
+  // Mlp::batch_grads reads them), the Hessian-batch slices after them; the draws stay in RNG order.
   auto draw_epoch = [&](bool u_seen, EpochDraw &d) {
     d.flat.clear();
+    d.hflat.clear();
     d.mb.assign(size_t(m_inner), Slice{});
     d.hb.assign(size_t(m_inner), Slice{-1, 0, 0});
-    auto take = [&](size_t bsz) {
+    auto take = [&](size_t bsz, std::vector<int> &dst) {
       d.batch.clear();
       const long long tot = (long long)sampler.draw(bsz, rng, d.batch);
       const long long a0 = tot * rk / nr, a1 = tot * (rk + 1) / nr;
-      Slice sl{(long long)d.flat.size(), a1 - a0, tot};
-      d.flat.insert(d.flat.end(), d.batch.begin() + a0, d.batch.begin() + a1);
+      Slice sl{(long long)dst.size(), a1 - a0, tot};
+      dst.insert(dst.end(), d.batch.begin() + a0, d.batch.begin() + a1);
       return sl;
     };
     int whist_size = 1;
     for (int t = 0; t < m_inner; ++t) {
-      d.mb[t] = take(size_t(prm_.b));
+      d.mb[t] = take(size_t(prm_.b), d.flat);
       whist_size = std::min(whist_size + 1, L + 1);
       if (t > 0 && t % L == 0) {
-        if (u_seen) d.hb[t] = take(size_t(prm_.b_H));
+        if (u_seen) d.hb[t] = take(size_t(prm_.b_H), d.hflat);
         u_seen = true;
       }
     }
+    const long long nmb_rows = (long long)d.flat.size();
+    for (Slice &h : d.hb)
+      if (h.off >= 0) h.off += nmb_rows;
+    d.flat.insert(d.flat.end(), d.hflat.begin(), d.hflat.end());
     d.pick = -1;
     if (whist_size >= 2) {
       std::uniform_int_distribution<size_t> pk(0, size_t(whist_size) - 2); // s_lbfgs.hpp:266
@@ -765,6 +793,22 @@ int SlbfgsSolver::run(lbf_record *rec) {
     auto g2 = [&](int t) { return gpair_[t & 1].get() + ng_; };
     auto rows_x = [&](const Slice &sl) { return xg_.get() + sl.off * In; };
     auto rows_y = [&](const Slice &sl) { return yg_.get() + sl.off * Out; };
+    // Anchor gradients of the whole epoch up front (every minibatch slice of this rank the same size, a
+    // multiple of 32 rows): one evaluation over the epoch's minibatch rows at w (see gmb_).
+    const long long cnt0 = mb[0].cnt;
+    bool pre = anchor_pre_ && cnt0 > 0 && cnt0 % 32 == 0;
+    for (int t = 1; t < m_inner && pre; ++t) pre = mb[t].cnt == cnt0 && mb[t].off == t * cnt0;
+    if (pre) {
+      const size_t need = size_t(m_inner) * size_t(ng_);
+      if (gmb_.size() < need) {
+        gmb_.resize(need);
+        // the two loss words and the pad of each row are never written: zero (the DP copy sums them)
+        LBF_HIP(hipMemsetAsync(gmb_.get(), 0, need * sizeof(float), s));
+      }
+      net_->batch_grads(w_.get(), xg_.get(), yg_.get(), m_inner, cnt0, 1.0 / double(mb[0].total), prm_.lambda,
+                        gmb_.get(), ng_, dp);
+    }
+    auto gpre = [&](int t) { return gmb_.get() + (long long)t * ng_; };
     auto anchor_ahead = [&](int t) { // twin stream: the anchor half of step t's block
       const Slice &sl = mb[t];
       LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_free_[t & 1], 0)); // step t - 2's direction read it
@@ -778,11 +822,22 @@ int SlbfgsSolver::run(lbf_record *rec) {
     // the epoch's gathered rows and w are complete (the context stream was synchronised above)
     static const int host_timing = env_int("LBF_HOST_TIMING", 0);
     const auto th0 = std::chrono::steady_clock::now();
-    if (tnet_) anchor_ahead(0);
+    if (tnet_ && !pre) anchor_ahead(0);
     for (int t = 0; t < m_inner; ++t) {
       const Slice &sl = mb[t];
       const double inv_b = 1.0 / double(sl.total);
-      if (tnet_) {
+      const float *gb = g2(t);
+      if (pre) {
+        if (dp) {
+          net_->loss_grad_local(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b);
+          LBF_HIP(hipMemcpyAsync(g2(t), gpre(t), size_t(ng_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+          reduce_pair(wt_.get(), w_.get(), g1(t), inv_b);
+        } else {
+          net_->loss_grad(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda, nullptr,
+                          nullptr);
+          gb = gpre(t);
+        }
+      } else if (tnet_) {
         if (t + 1 < m_inner) anchor_ahead(t + 1);
         if (dp)
           net_->loss_grad_local(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b);
@@ -798,11 +853,11 @@ int SlbfgsSolver::run(lbf_record *rec) {
       ga.policy = POL_SLBFGS;
       ga.has_g = 1;
       ga.ga = g1(t);
-      ga.gb = g2(t);
+      ga.gb = gb;
       ga.gc = mu_.get();
       ga.g_out = v_.get();
       hist_.update(ga, 1, 1, +1.0);
-      if (tnet_) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
+      if (tnet_ && !pre) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
       const int slot = wh_push_slot();
       // wt = wt - step * r ; w_history.push_back(wt)
       hist_.combine(v_.get(), nullptr, wt_.get(), wt_.get(), wh_.get() + slot * ld, false, -prm_.step);

@@ -190,6 +190,12 @@ private:
   // [g(w_t) | g(w)] of an inner step, double-buffered (the twin fills the anchor half one step ahead),
   // and [g(u + eps s) | g(u - eps s)] of a Hessian step: one all-reduce per block under data parallelism
   DevBuf<float> gpair_[2], fdpair_;
+  // Anchor gradients of a whole epoch (LBF_SLBFGS_ANCHOR=1; default off): w is fixed for the epoch and so
+  // are its minibatches, so g(w) of every minibatch is computed up front in one evaluation over the
+  // epoch's rows (Mlp::batch_grads), minibatch t at gmb_ + t ng_. The inner steps then evaluate only
+  // g(w_t): no twin, no per-step cross-stream events.
+  DevBuf<float> gmb_;
+  bool anchor_pre_ = false; // LBF_SLBFGS_ANCHOR=1
   long long ng_ = 0; // floats per gradient in a block (n + 2 loss words, rounded to 4)
   DevBuf<int> idx_;
   PinnedBuf<double> hs_;

@@ -522,6 +522,25 @@ __global__ __launch_bounds__(256) void finalize_kernel(long long n, float *g, co
   }
 }
 
+// G[r * ld + e] += lambda w[e] for r < rows, e < n: finalize_kernel's update (same fp32 expression) on
+// each of a block of per-minibatch gradients (Mlp::batch_grads).
+__global__ __launch_bounds__(256) void add_l2_rows_kernel(long long n, int rows, long long ld, float *G,
+                                                          const float *w, double lambda) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float lf = float(lambda), wv = w[e];
+  float *g = G + e;
+  // written as the fused multiply-add the contracted `gv + lf * wv` of finalize_kernel / reduce_all
+  // compiles to (here the product is loop-invariant and would otherwise be hoisted and rounded once)
+  for (int r = 0; r < rows; ++r) g[r * ld] = __builtin_fmaf(lf, wv, g[r * ld]);
+}
+
+void add_l2_rows(hipStream_t s, long long n, int rows, long long ld, float *G, const float *w, double lambda) {
+  if (n <= 0 || rows <= 0 || lambda == 0.0) return;
+  hipLaunchKernelGGL(add_l2_rows_kernel, dim3(unsigned(cdiv(n, 256))), dim3(256), 0, s, n, rows, ld, G, w, lambda);
+  LBF_KERNEL_CHECK();
+}
+
 void finalize_grad_dots(hipStream_t s, long long n, float *g, const float *w, double lambda, const float *p,
                         double *partials, const int *abort, const float *g_in) {
   hipLaunchKernelGGL(finalize_kernel, dim3(dots_partials_wg(n)), dim3(256), 0, s, n, g, g_in, w, lambda, p, partials,

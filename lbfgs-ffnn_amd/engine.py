@@ -193,6 +193,19 @@ class Mlp:
               "lbf_mlp_loss_grad")
         return loss.value, grad
 
+    def batch_grads(self, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, nmb: int,
+                    inv_scale: Optional[float] = None, l2: float = 0.0) -> torch.Tensor:
+        """Gradients of nmb consecutive minibatches of X / Y (X.shape[0] // nmb rows each, a multiple of 32) at
+        one point, in one evaluation (lbf_mlp_batch_grads): returns an (nmb, nparams) tensor."""
+        cnt = int(X.shape[0]) // nmb
+        if inv_scale is None:
+            inv_scale = 1.0 / cnt
+        self._check_data(X, Y)
+        out = torch.empty((nmb, self.nparams), dtype=torch.float32, device=params.device)
+        check(lib().lbf_mlp_batch_grads(self.h, ptr(params, numel=self.nparams), ptr(X), ptr(Y), nmb, cnt, inv_scale,
+                                        l2, ptr(out), self.nparams), "lbf_mlp_batch_grads")
+        return out
+
     def loss(self, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, idx: Optional[torch.Tensor] = None,
              inv_scale: Optional[float] = None) -> float:
         """Forward + MSE only (lbf_mlp_loss): the f of a line-search trial."""

@@ -124,3 +124,72 @@ def test_dp_slbfgs_cfg4_bitwise(ctx, dp_ctx, pkg):
     assert np.array_equal(h1["accepted"], hd["accepted"])
     assert i1.n_evals == idd.n_evals and i1.n_rows == idd.n_rows
     assert abs(h1["loss"][0] - hd["loss"][0]) <= 1e-12 * abs(h1["loss"][0])
+
+
+def test_batch_grads_equal_per_minibatch_loss_grad(ctx, pkg):
+    """lbf_mlp_batch_grads (the S-LBFGS epoch's anchor gradients in one evaluation) against lbf_mlp_loss_grad on
+    each minibatch: the same sums in another order (one K split per minibatch, the unfused output layer),
+    so equal to fp32 rounding: max |diff| <= 1e-5 max |g| per minibatch."""
+    dims, acts = [784, 512, 256, 10], ["relu", "relu", "linear"]
+    nmb, cnt = 6, 256
+    Xh, Yh = pkg.synth_mnist(nmb * cnt)
+    X, Y = dev(Xh), dev(Yh)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(7, "cpu")
+    G = net.batch_grads(P, X, Y, nmb, inv_scale=1.0 / cnt, l2=1e-4)
+    for t in range(nmb):
+        _, g = net.loss_grad(P, X[t * cnt:(t + 1) * cnt], Y[t * cnt:(t + 1) * cnt], inv_scale=1.0 / cnt, l2=1e-4)
+        ref = host(g)
+        err = np.abs(host(G[t]) - ref).max()
+        assert err <= 1e-5 * np.abs(ref).max(), (t, err, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("route,exact,tol", [("single", 0, 3e-3), ("dp", 0, 3e-3), ("single", 1, 1e-4)])
+def test_slbfgs_anchor_precompute_matches_per_step(ctx, dp_ctx, pkg, route, exact, tol, monkeypatch):
+    """The epoch's anchor gradients g(w; B_t) computed up front (Mlp::batch_grads) against the per-step
+    evaluation at the same w (twin stream, LBF_SLBFGS_ANCHOR=0): equal to fp32 rounding (test above), so two
+    epochs of cfg 4's shape take the same decisions and agree closely. With the finite-difference HVP
+    (s_lbfgs.hpp:88-101) a rounding-level change of the iterate is amplified ~1/(2 eps) = 5000x in y, hence the
+    looser tolerance there than with the exact HVP."""
+    dims, acts = [784, 512, 256, 10], ["relu", "relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(12800)
+    X, Y = dev(Xh), dev(Yh)
+    kw = dict(M=10, L=10, b=256, b_H=128, step=0.005, max_epochs=2, tol=0.0, lam=1e-4, hvp_exact=exact)
+    c = ctx if route == "single" else dp_ctx
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("LBF_SLBFGS_ANCHOR", flag)
+        net = pkg.Mlp(c, dims, acts)
+        P = net.init_params(123, "cpu")
+        hist, info = pkg.slbfgs_solve(net, P, X, Y, **kw)
+        out.append((hist, P, info))
+    (h0, P0, i0), (h1, P1, i1) = out
+    assert i0.n_evals == i1.n_evals and i0.n_rows == i1.n_rows
+    assert np.array_equal(h0["accepted"], h1["accepted"])
+    np.testing.assert_allclose(h1["loss"], h0["loss"], rtol=tol)
+    rel = (P1 - P0).norm().item() / P0.norm().item()
+    assert rel < tol, rel
+
+
+@pytest.mark.parametrize("B", [256, 128, 96, 2944])
+def test_fwd_split_k_in_launch_reduction_is_bitwise(ctx, pkg, B, monkeypatch):
+    """The forward GEMM's split-K slabs summed inside the launch by each tile's last-arriving split
+    (GemmDesc::fin_cnt, sc1 hand-off) against the separate fwd_reduce_act launch (LBF_FWD_FIN=0): the same
+    fp32 sums in the same split order, so loss and gradient are bit for bit equal (S-LBFGS minibatch and
+    Hessian-batch shapes, and a ragged row count), over repeated calls (the arrival counters re-arm)."""
+    dims, acts = [784, 512, 256, 10], ["relu", "tanh", "linear"]
+    Xh, Yh = pkg.synth_mnist(B)
+    X, Y = dev(Xh), dev(Yh)
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("LBF_FWD_FIN", flag)
+        net = pkg.Mlp(ctx, dims, acts)
+        P = net.init_params(11, "cpu")
+        outs = []
+        for rep in range(3):
+            loss, g = net.loss_grad(P, X, Y, l2=1e-4)
+            outs.append((loss, g.clone()))
+        res.append(outs)
+    for (l0, g0), (l1, g1) in zip(res[0], res[1]):
+        assert l0 == l1
+        assert torch.equal(g0, g1)
