@@ -129,3 +129,44 @@ def test_hvp_empty_batch(ctx, pkg):
     hv = net.hvp(P, v, X, Y, idx=idx, inv_scale=1.0, l2=1e-4)
     ref = (1e-4 * v.double()).float()
     assert torch.allclose(hv, ref, rtol=1e-6, atol=0)
+
+
+def test_fd_hvp_across_a_relu_kink_matches_oracle(ctx, pkg, O):
+    """VERDICT r02 item 6, the step-0.01 NaN of config 4 (profiles/r03/diag_nan_step0.01.txt, diag_pair0.txt):
+    the reference's finite-difference HVP (s_lbfgs.hpp:88-101) differences the gradient at u +- eps s; when
+    a ReLU pre-activation changes sign in between, the gradient jumps and y picks up a term of order
+    |jump| / (2 eps) the Hessian does not have. At cfg 4's first pair one sign flip in 32768 made |y| 20x the
+    exact HVP's — in the device AND the fp64 / fp32 oracle alike at the same (u, s, rows); which run meets
+    such a pair first is a knife edge of the trajectory. Here a kink is placed on purpose (one hidden unit's
+    pre-activation is 0 at u on one row, and s moves it): the device FD equals the oracle's fp64 FD and both
+    are far from the exact R-operator HVP, which is what a device bug could not produce."""
+    dims, acts = [32, 16, 4], ["relu", "linear"]
+    rng = np.random.default_rng(5)
+    N, eps = 8, 1e-4
+    X = rng.standard_normal((N, dims[0]))
+    Y = rng.standard_normal((N, dims[-1]))
+    net = pkg.Mlp(ctx, dims, acts)
+    u = net.init_params(3, "cpu").double().cpu().numpy()
+    n0 = dims[0] * dims[1]
+    W0 = u[:n0].reshape(dims[0], dims[1])
+    j = 5
+    u[n0 + j] = -(X[0] @ W0[:, j])          # unit j of layer 0 sits exactly on its kink at row 0
+    s = 0.01 * rng.standard_normal(u.size)
+    s[n0 + j] = 1.0                         # ... and s crosses it: z = +-eps on that row
+    # the fp32 copies both sides use (the oracle restates the device's fp32 inputs in fp64)
+    u32, s32 = u.astype(np.float32), s.astype(np.float32)
+    X32, Y32 = X.astype(np.float32), Y.astype(np.float32)
+    onet = O.Net(dims, acts)
+    rows = np.arange(N)
+    y_or = onet.fd_hvp(u32.astype(np.float64), s32.astype(np.float64), X32.astype(np.float64),
+                       Y32.astype(np.float64), idx=rows, lam=0.0, eps=eps)
+    ud, sd = torch.from_numpy(u32).cuda(), torch.from_numpy(s32).cuda()
+    Xd, Yd = torch.from_numpy(X32).cuda(), torch.from_numpy(Y32).cuda()
+    y_fd = net.fd_hvp(ud, sd, Xd, Yd, inv_scale=1.0 / N, l2=0.0, eps=eps).double().cpu().numpy()
+    y_ex = net.hvp(ud, sd, Xd, Yd, inv_scale=1.0 / N, l2=0.0).double().cpu().numpy()
+    # the kink term: the FD result is far from the Hessian's product ...
+    assert np.linalg.norm(y_fd - y_ex) > 0.5 * np.linalg.norm(y_ex)
+    # ... and the device's FD is the reference algorithm's FD (fp32 differencing of fp32 gradients; the
+    # fp64 oracle differences exact gradients: agreement to the fp32 gradient rounding / (2 eps))
+    assert np.linalg.norm(y_fd - y_or) <= 2e-2 * np.linalg.norm(y_or), \
+        (np.linalg.norm(y_fd - y_or) / np.linalg.norm(y_or))
