@@ -26,10 +26,12 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// C columns per lane (64*C per block); VPW history vectors per wave (v = wave + 4j).
+// C columns per lane (64*C per block) as Q = C/4 quads, lane l owning columns 256q + 4l .. +3 of quad q;
+// VPW history vectors per wave (v = wave + 4j).
 template <int C, int VPW>
 __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
-  constexpr int TC = 64 * C;
+  constexpr int TC = 64 * C, Q = C / 4;
+  static_assert(C % 4 == 0, "dir_sweep: whole quads per lane");
   const GramArgs &g = a.g;
   const HistView &h = g.h;
   if (h.abort && *h.abort) return;
@@ -43,25 +45,30 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(hist_write_slot(ist, h.m, g.policy, g.reset));
   if (blockIdx.x == 0 && t == 0) h.ist[IST_WSLOT] = w;
   const int nvec = 2 * count0;
-  // Lane l owns columns 4l .. 4l+3 of the group (C == 4: 16-B loads; every vector the sweep touches is
-  // 16-B aligned and padded to a multiple of 4 floats, History::update checks). Every load is
-  // unconditional from a clamped address and masked after (tail.hip's discipline).
-  static_assert(C == 4, "dir_sweep: four columns per lane");
-  const long long col0 = (long long)blockIdx.x * TC + 4 * lane;
-  const long long e4 = col0 < h.n ? col0 : ((h.n - 1) & ~3LL); // clamped quad start (inside the padding)
-  bool live[C];
+  // 16-B loads (every vector the sweep touches is 16-B aligned and padded to a multiple of 4 floats,
+  // History::update checks). Every load is unconditional from a clamped address and masked after
+  // (tail.hip's discipline).
+  long long col0[Q], e4[Q];
+  bool live[Q][4];
 #pragma unroll
-  for (int c = 0; c < C; ++c) live[c] = col0 + c < h.n;
-  f32x4 vv[VPW];
+  for (int q = 0; q < Q; ++q) {
+    col0[q] = (long long)blockIdx.x * TC + 256 * q + 4 * lane;
+    e4[q] = col0[q] < h.n ? col0[q] : ((h.n - 1) & ~3LL); // clamped quad start (inside the padding)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) live[q][c] = col0[q] + c < h.n;
+  }
+  f32x4 vv[VPW][Q];
   unsigned zero_mask = 0; // bit j: vector j of this wave is not live (or is the slot being overwritten)
 #pragma unroll
   for (int j = 0; j < VPW; ++j) {
     const int v = wave + 4 * j; // wave-uniform: the branch is scalar, no per-lane wait
-    vv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < Q; ++q) vv[j][q] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (v < nvec) {
       const int slot = __builtin_amdgcn_readfirstlane(ist[IST_ORDER + (v < count0 ? v : v - count0)]);
       const float *base = (v < count0 ? h.S : h.Y) + (long long)slot * h.ld;
-      vv[j] = *reinterpret_cast<const f32x4 *>(base + e4);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) vv[j][q] = *reinterpret_cast<const f32x4 *>(base + e4[q]);
       if (g.has_pair && slot == w) zero_mask |= 1u << j;
     } else {
       zero_mask |= 1u << j;
@@ -69,41 +76,48 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
   }
   if (wave == 0) { // the new vectors of the group (null operands read ga / sa and are masked)
     const float *dflt = g.has_g ? g.ga : g.sa;
-    auto ld4 = [&](const float *p) { return *reinterpret_cast<const f32x4 *>((p ? p : dflt) + e4); };
-    const f32x4 sa = ld4(g.sa), sb = ld4(g.sb), ya = ld4(g.ya), yb = ld4(g.yb);
-    const f32x4 ga = ld4(g.ga), gb = ld4(g.gb), gc = ld4(g.gc);
     const float ysc = float(g.yscale);
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int q = 4 * lane + c;
-      const long long e = col0 + c;
-      float sv = 0.f, yv = 0.f, gv = 0.f;
-      if (live[c]) {
-        if (g.has_pair) { // gram_kernel's arithmetic
-          sv = sa[c] - sb[c];
-          yv = (ya[c] - yb[c]) * ysc;
-          h.S[(long long)w * h.ld + e] = sv;
-          h.Y[(long long)w * h.ld + e] = yv;
+    for (int q = 0; q < Q; ++q) {
+      auto ld4 = [&](const float *p) { return *reinterpret_cast<const f32x4 *>((p ? p : dflt) + e4[q]); };
+      const f32x4 sa = ld4(g.sa), sb = ld4(g.sb), ya = ld4(g.ya), yb = ld4(g.yb);
+      const f32x4 ga = ld4(g.ga), gb = ld4(g.gb), gc = ld4(g.gc);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int qq = 256 * q + 4 * lane + c;
+        const long long e = col0[q] + c;
+        float sv = 0.f, yv = 0.f, gv = 0.f;
+        if (live[q][c]) {
+          if (g.has_pair) { // gram_kernel's arithmetic
+            sv = sa[c] - sb[c];
+            yv = (ya[c] - yb[c]) * ysc;
+            h.S[(long long)w * h.ld + e] = sv;
+            h.Y[(long long)w * h.ld + e] = yv;
+          }
+          if (g.has_g) {
+            gv = ga[c];
+            if (g.gb) gv = gv - gb[c];
+            if (g.gc) gv = gv + gc[c];
+            if (g.g_out) g.g_out[e] = gv;
+          }
         }
-        if (g.has_g) {
-          gv = ga[c];
-          if (g.gb) gv = gv - gb[c];
-          if (g.gc) gv = gv + gc[c];
-          if (g.g_out) g.g_out[e] = gv;
-        }
+        ops[0][qq] = sv;
+        ops[1][qq] = yv;
+        ops[2][qq] = gv;
       }
-      ops[0][q] = sv;
-      ops[1][q] = yv;
-      ops[2][q] = gv;
     }
   }
   lds_barrier();
-  // ---- dots: every (history vector, new vector) dot is owned by one wave: 4 exact fp64 products per lane,
+  // ---- dots: every (history vector, new vector) dot is owned by one wave: 4Q exact fp64 products per lane,
   // a DPP wave sum, lane 0 stores the partial row entry (no LDS staging of the history values: staged
   // rows 1 KB apart put every quad of a wave on the same LDS banks) ----
-  const f32x4 s4 = *reinterpret_cast<const f32x4 *>(&ops[0][4 * lane]);
-  const f32x4 y4 = *reinterpret_cast<const f32x4 *>(&ops[1][4 * lane]);
-  const f32x4 g4 = *reinterpret_cast<const f32x4 *>(&ops[2][4 * lane]);
+  f32x4 s4[Q], y4[Q], g4[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    s4[q] = *reinterpret_cast<const f32x4 *>(&ops[0][256 * q + 4 * lane]);
+    y4[q] = *reinterpret_cast<const f32x4 *>(&ops[1][256 * q + 4 * lane]);
+    g4[q] = *reinterpret_cast<const f32x4 *>(&ops[2][256 * q + 4 * lane]);
+  }
   double *rows = a.rows + blockIdx.x;
   const long long nb = a.nb;
 #pragma unroll
@@ -113,12 +127,14 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
     double ds = 0.0, dy = 0.0, dg = 0.0;
     if (!((zero_mask >> j) & 1u)) { // the slot being overwritten contributes zeros (gram_kernel's rule)
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const double x = live[c] ? double(vv[j][c]) : 0.0;
-        ds += x * double(s4[c]);
-        dy += x * double(y4[c]);
-        dg += x * double(g4[c]);
-      }
+      for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const double x = live[q][c] ? double(vv[j][q][c]) : 0.0;
+          ds += x * double(s4[q][c]);
+          dy += x * double(y4[q][c]);
+          dg += x * double(g4[q][c]);
+        }
     }
     ds = wave_sum_f64(ds);
     dy = wave_sum_f64(dy);
@@ -133,15 +149,17 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
   if (wave == 3) { // self block 6m + {s.s, s.y, y.y, g.s, g.y, g.g}
     double d[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const double sv = s4[c], yv = y4[c], gv = g4[c];
-      d[0] += sv * sv;
-      d[1] += sv * yv;
-      d[2] += yv * yv;
-      d[3] += gv * sv;
-      d[4] += gv * yv;
-      d[5] += gv * gv;
-    }
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double sv = s4[q][c], yv = y4[q][c], gv = g4[q][c];
+        d[0] += sv * sv;
+        d[1] += sv * yv;
+        d[2] += yv * yv;
+        d[3] += gv * sv;
+        d[4] += gv * yv;
+        d[5] += gv * gv;
+      }
 #pragma unroll
     for (int z = 0; z < 6; ++z) d[z] = wave_sum_f64(d[z]);
     if (lane == 0)
@@ -232,6 +250,7 @@ void launch_sweep(hipStream_t s, const DirArgs &a, int vpw) {
   switch (vpw) {
   case 2: hipLaunchKernelGGL((dir_sweep_kernel<C, 2>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
   case 4: hipLaunchKernelGGL((dir_sweep_kernel<C, 4>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 6: hipLaunchKernelGGL((dir_sweep_kernel<C, 6>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
   case 8: hipLaunchKernelGGL((dir_sweep_kernel<C, 8>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
   default: throw Error(2, "dir_sweep: history size not supported");
   }
@@ -241,15 +260,21 @@ void launch_sweep(hipStream_t s, const DirArgs &a, int vpw) {
 
 static int dir_vpw(int m) {
   const int per_wave = (2 * m + 3) / 4;
-  return per_wave <= 2 ? 2 : per_wave <= 4 ? 4 : per_wave <= 8 ? 8 : 16;
+  return per_wave <= 2 ? 2 : per_wave <= 4 ? 4 : per_wave <= 6 ? 6 : per_wave <= 8 ? 8 : 16;
 }
-// 256 columns per block (16-B loads, four columns per lane); the LDS copy of a group holds 4 * VPW vectors,
-// so m <= 16 (VPW 8: 32 KB)
+// Columns per block: 256 (one quad per lane) or, by default, 512 (two): at n = 535,818 (cfg 4) 256-column
+// blocks are 2093, above the 1792 this kernel's 88 SGPRs admit at once (7 per CU), so the sweep ran in
+// two rounds; 1047 blocks of 512 columns run in one, with twice the loads in flight per lane.
+// (LBF_DIR_COLS=256 selects the narrow form.) m <= 16.
+static int dir_c() {
+  static const int c = env_int("LBF_DIR_COLS", 512) == 256 ? 4 : 8;
+  return c;
+}
 bool dir_supported(int m, long long n) { return m >= 0 && m <= DIR_MAXM && n > 0 && n <= DIR_MAXN; }
 int dir_cols_per_block(int m, long long n) {
   (void)m;
   (void)n;
-  return 256;
+  return 64 * dir_c();
 }
 int dir_ncols(int m) { return 6 * m + 6; }
 
@@ -257,7 +282,8 @@ void dir_sweep(hipStream_t s, const DirArgs &a) {
   LBF_REQUIRE(dir_supported(a.g.h.m, a.g.h.n), "dir_sweep: history size / vector length");
   LBF_REQUIRE(a.want_dir == 0 || a.want_dir == 1, "dir_sweep: want_dir 0 / 1");
   LBF_REQUIRE(a.nb == int(cdiv(a.g.h.n, dir_cols_per_block(a.g.h.m, a.g.h.n))), "dir_sweep: block count");
-  launch_sweep<4>(s, a, dir_vpw(a.g.h.m));
+  if (dir_c() == 8) launch_sweep<8>(s, a, dir_vpw(a.g.h.m));
+  else launch_sweep<4>(s, a, dir_vpw(a.g.h.m));
   LBF_KERNEL_CHECK();
 }
 
