@@ -316,10 +316,19 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
     // the head runs on them. n0 == 0 (N <= BN).
     constexpr int QM = headc::qstrips(BN);
     headc::Smem hs = headc::carve(lds, g.N);
-    hs.xr = hs.ys + BM * 16;
+    // the head tile runs on TB-row halves: a 32-row GEMM tile's ys / xr rows [BM, TB) are zero (rows past
+    // the tile contribute nothing: their delta is zero, and zero times the LDS left by an earlier kernel
+    // could be NaN)
+    constexpr int YRA = BM > headc::TB ? BM : headc::TB;
+    hs.xr = hs.ys + YRA * 16;
     const bool fold = g.head_fold >= 0; // uniform
     hpre.store(hs);
     if (g.head_fold > 0) hpre.store_fold(hs);
+    if constexpr (YRA > BM) {
+      for (int e = threadIdx.x; e < (YRA - BM) * 16; e += 256 * KW) hs.ys[BM * 16 + e] = 0.0f;
+      if (g.head_fold > 0)
+        for (int e = threadIdx.x; e < (YRA - BM) * headc::XLD; e += 256 * KW) hs.xr[BM * headc::XLD + e] = 0.0f;
+    }
     KT(26);
     KTB(2);
     headc::f32x4 cw[QM];
@@ -457,7 +466,7 @@ __global__ __launch_bounds__(256 * KW, 2) void gemm_kernel(const GemmK g) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32, LDK = BK + 4;
   constexpr int ASZ = AKC ? BM * LDK : BK * (BM + 4);
   constexpr int BSZ = BKC ? BN * LDK : BK * (BN + 4);
-  constexpr int HEAD_F = headc::smem_floats_epi(BN, BM);
+  constexpr int HEAD_F = headc::smem_floats_epi(BN, BM > headc::TB ? BM : headc::TB);
   constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > 2 * (ASZ + BSZ)) ? HEAD_F : 2 * (ASZ + BSZ);
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
   if (g.abort && *g.abort) return;
@@ -711,7 +720,7 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
   static_assert((BM + BN) % 32 == 0, "pieces per wave");
   static_assert(AKC || BM >= 64, "mn-contiguous swizzle needs >= 64 columns");
   static_assert(BKC || BN >= 64, "mn-contiguous swizzle needs >= 64 columns");
-  constexpr int HEAD_F = headc::smem_floats_epi(BN, BM);
+  constexpr int HEAD_F = headc::smem_floats_epi(BN, BM > headc::TB ? BM : headc::TB);
   constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > NS * STG) ? HEAD_F : NS * STG;
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
   if (g.abort && *g.abort) return;
@@ -939,6 +948,127 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
   gemm_epilogue<WM, WN, TM, TN, EPI, KW>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, kgrp);
 }
 
+// Direct-operand GEMM for the 32 x 128 tile with a k-contiguous A (rows of X / activations) and an
+// mn-contiguous B (W as [K][N]), no gather: the MFMA operands are loaded from global memory (L2) straight
+// into registers, with no LDS staging in the main loop. The LDS-DMA kernel's 32 x 128 tile moves ~22 GB/s
+// of operands per CU (every DMA piece stalls its issuing wave ~100+ cycles), half its MFMA rate; vector
+// loads issue in a few cycles and land asynchronously. Two k-groups of four waves (KW = 2) split the 16
+// k-steps of every 32-deep k-tile exactly as gemm_glds_kernel<1, 4, 1, 1, true, false, *, false, *, 2>
+// does (lane half h consumes k = 16h + 8q + s at step s of group q, groups summed through LDS in group
+// order): the same MFMA sequence on the same values, so the results are bitwise the LDS-DMA kernel's.
+// Operands of D k-tiles are in flight per wave (registers rotate over an unrolled loop).
+template <int EPI, int D, int SETS>
+__global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(1, 2))) void gemm_direct_kernel(const GemmK g) {
+  static_assert(SETS >= D, "register sets");
+  constexpr int WM = 1, WN = 4, TM = 1, TN = 1, KW = 2, BM = 32, BN = 128, BK = 32;
+  constexpr int HEAD_F = headc::smem_floats_epi(BN, BM > headc::TB ? BM : headc::TB);
+  constexpr int RED_F = TM * TN * 16 * 256;
+  constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > RED_F) ? HEAD_F : RED_F;
+  __shared__ __attribute__((aligned(16))) float lds[LDS_F];
+  if (g.abort && *g.abort) return;
+  const int zsplit = int(blockIdx.z);
+  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
+  const int kgrp = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 8));
+  const int wm = 0, wn = wave;
+  const int li = lane & 31, lh = lane >> 5;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int kb = zsplit * g.k_chunk;
+  const int ke = min(g.K, kb + g.k_chunk);
+  const int nk = kb < ke ? (ke - kb + BK - 1) / BK : 0;
+  // this lane's operand streams: A row m0 + li (clamped), B column n0 + 32 wn + li (clamped)
+  const int row = min(m0 + li, g.M - 1);
+  const int col = min(n0 + wn * 32 + li, g.N - 1);
+  const float *Ar = g.A + (long long)row * g.lda;
+  const float *Bc = g.B + col;
+  // rows past M and columns past N read clamped addresses but must contribute exact zeros, as the LDS-DMA
+  // kernel's zero chunk does: the EPI_HEAD epilogue (delta, the fold's partial rows) consumes the
+  // accumulators of the whole tile, not only the stored entries
+  const bool row_ok = m0 + li < g.M, col_ok = n0 + wn * 32 + li < g.N;
+  const int kl = 16 * lh + 8 * kgrp; // first k of this lane's 8 within a k-tile
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.0f;
+  headc::EpiPrefetch<BN, BM, 256 * KW> hpre;
+  if constexpr (EPI == EPI_HEAD) {
+    hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
+    if (g.head_fold > 0) hpre.load_fold(g.A, g.lda, g.a_idx, g.head_fold_c0, g.head_fold, m0, g.M);
+  }
+  struct Ops {
+    f32x4 a0, a1;
+    float b[8];
+  };
+  // k-tile t's operands: unconditional loads from clamped addresses (k >= ke reads an earlier k of the
+  // same row / column), the out-of-range values zeroed when used
+  auto load = [&](int t, Ops &o) {
+    const int k0 = kb + t * BK + kl;
+    const int ka = k0 + 4 <= ke ? k0 : kb, kc = k0 + 8 <= ke ? k0 + 4 : kb;
+    o.a0 = *reinterpret_cast<const f32x4 *>(Ar + ka);
+    o.a1 = *reinterpret_cast<const f32x4 *>(Ar + kc);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = k0 + s;
+      o.b[s] = Bc[(long long)(k < ke ? k : kb) * g.ldb];
+    }
+  };
+  auto mask = [&](Ops &o) { // after the loads have landed (the selects consume them)
+    if (!row_ok) {
+      o.a0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+      o.a1 = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    if (!col_ok)
+#pragma unroll
+      for (int s = 0; s < 8; ++s) o.b[s] = 0.0f;
+  };
+  auto mma = [&](int t, Ops &o) {
+    mask(o);
+    const int k0 = kb + t * BK + kl;
+    const bool full = k0 + 8 <= ke; // wave-uniform only per lane half; masks are per element
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      float a = s < 4 ? o.a0[s] : o.a1[s - 4];
+      float b = o.b[s];
+      if (!full && k0 + s >= ke) {
+        a = 0.0f;
+        b = 0.0f;
+      }
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[0][0], 0, 0, 0);
+    }
+  };
+  // The loop runs a multiple of D k-tiles and every load is unconditional (k-tiles past the end read
+  // clamped addresses and contribute zero products, which leave the sums bitwise unchanged): straight-line
+  // code, so the compiler's wait counts keep D - 1 k-tiles in flight instead of draining at a branch.
+  // SETS > D register sets: a set is refilled SETS - D + 1 k-tiles after its MFMAs were issued, not
+  // right behind them (the refill's loads must not land in registers a queued MFMA has yet to read).
+  Ops ops[SETS];
+  if (nk > 0) {
+    const int nkp = (nk + SETS - 1) / SETS * SETS;
+#pragma unroll
+    for (int t = 0; t < D - 1; ++t) load(t, ops[t]);
+    for (int i = 0; i < nkp; i += SETS) {
+#pragma unroll
+      for (int u = 0; u < SETS; ++u) { // unrolled by SETS: the register sets are static
+        load(i + u + D - 1, ops[(u + D - 1) % SETS]);
+        __builtin_amdgcn_sched_barrier(0); // the loads stay ahead of this k-tile's MFMAs (no sinking)
+        mma(i + u, ops[u]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  // k-group sums through LDS, in group order (group 0 keeps the result): gemm_glds_kernel's
+  float *red = lds;
+  if (kgrp == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[r * 256 + (threadIdx.x & 255)] = acc[0][0][r];
+  }
+  __syncthreads();
+  if (kgrp == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][0][r] += red[r * 256 + threadIdx.x];
+  }
+  __syncthreads();
+  gemm_epilogue<WM, WN, TM, TN, EPI, KW>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, kgrp);
+}
+
 namespace {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -999,6 +1129,15 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.nsplits = d.splits > 1 ? d.splits : 1;
   dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
   static const bool glds_on = env_int("LBF_GEMM_GLDS", 1) != 0;
+  if constexpr (WM == 1 && WN == 4 && TM == 1 && TN == 1 && AKC && !BKC && KW == 2 && EPI != EPI_DX) {
+    // the 32 x 128 forward tile with operands straight from L2 into registers (gemm_direct_kernel)
+    if (d.direct && fast && !d.a_idx && k.side_planes == 0 && d.K >= 8) {
+      static const int var = env_int("LBF_GEMM_DIRECT_SETS", 4);
+      if (var == 3) hipLaunchKernelGGL((gemm_direct_kernel<EPI, 3, 3>), grid, dim3(512), 0, s, k);
+      else hipLaunchKernelGGL((gemm_direct_kernel<EPI, 3, 4>), grid, dim3(512), 0, s, k);
+      return;
+    }
+  }
   if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
     if (fast && glds_on && (AKC || !d.a_idx)) {
       const dim3 gb(256 * KW);

@@ -99,6 +99,7 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
   if (const char *e = std::getenv("LBF_DW_TILE64")) dw64_ = e[0] != '0';
   if (const char *e = std::getenv("LBF_NO_FOLD")) fold_on_ = e[0] != '1';
   tail_split_ = env_int("LBF_TAIL_SPLIT", 0) != 0; // 1: tail_fin as its own launch (A/B and tests)
+  gemm_direct_ = env_int("LBF_GEMM_DIRECT", 0) != 0; // measured slower (profiles/r03/bench_7500_direct.json)
   fwd_fin_ = env_int("LBF_FWD_FIN", 0) != 0; // measured slower at S-LBFGS minibatches (profiles/r03)
 }
 
@@ -325,6 +326,7 @@ GemmDesc Mlp::fwd_desc(size_t l, const float *P, const float *in, const int *idx
   d.act = L.act;
   d.abort = ctx_->abort;
   d.tile = L.ftile;
+  d.direct = gemm_direct_;
   return d;
 }
 
@@ -354,6 +356,9 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
         d.fin_cnt = fin_cnt_.get();
         d.fin_out = A_[l].get();
       }
+      static const int poison = env_int("LBF_DBG_POISON_FSLAB", 0); // debug: unwritten slab entries read as NaN
+      if (poison)
+        LBF_HIP(hipMemsetAsync(fslab_.get(), 0xff, size_t(L.fsplits) * size_t(B) * L.out * sizeof(float), s));
       ProfScope ps(ctx_, PK_FWD, int(l), double(B));
       gemm(s, d);
       if (!fin)

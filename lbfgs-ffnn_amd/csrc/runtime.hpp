@@ -173,6 +173,7 @@ private:
   // arrival counters of the forward GEMMs' in-launch split-K reduction (GemmDesc::fin_cnt), one per
   // output tile; each launch leaves them zero
   DevBuf<unsigned> fin_cnt_;
+  bool gemm_direct_ = false; // LBF_GEMM_DIRECT=1: gemm_direct_kernel for the 32 x 128 forward tiles (opt-in)
   bool fwd_fin_ = false; // LBF_FWD_FIN=1: in-launch reduction (the reducer's serial slab read costs more than the launch it saves)
   bool use_head_ = true;      // fused output layer when the shape allows (LBF_NO_HEAD=1 disables)
   bool use_gemm_head_ = true; // ... inside the forward GEMM's epilogue (LBF_NO_GEMM_HEAD=1 disables)

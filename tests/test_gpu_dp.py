@@ -193,3 +193,35 @@ def test_fwd_split_k_in_launch_reduction_is_bitwise(ctx, pkg, B, monkeypatch):
     for (l0, g0), (l1, g1) in zip(res[0], res[1]):
         assert l0 == l1
         assert torch.equal(g0, g1)
+
+
+@pytest.mark.parametrize("dims,acts,B", [([784, 128, 10], ["relu", "linear"], 7500),   # 32x128 EPI_HEAD + fold
+                                         ([784, 128, 10], ["relu", "linear"], 1000),
+                                         ([784, 512, 256, 10], ["relu", "tanh", "linear"], 256),  # split-K
+                                         ([784, 512, 256, 10], ["relu", "relu", "linear"], 96),
+                                         ([784, 128, 64, 10], ["sigmoid", "relu", "linear"], 333),
+                                         # N = 16 < the tile width, EPI_HEAD with the 16-column fold, M < 32: the
+                                         # epilogue consumes the whole tile's accumulators (rows >= M, columns
+                                         # >= N must be exact zeros; they were copies of the clamped edge once,
+                                         # and the fold's rows came out NaN)
+                                         ([784, 16, 10], ["relu", "linear"], 16),
+                                         ([784, 16, 10], ["relu", "linear"], 2048)])
+def test_direct_operand_gemm_is_bitwise(ctx, pkg, dims, acts, B, monkeypatch):
+    """The 32 x 128 forward tile with its operands loaded from L2 straight into registers (gemm_direct_kernel)
+    against the LDS-DMA kernel (LBF_GEMM_DIRECT=0): the same MFMA sequence on the same values, so loss and
+    gradient are bit for bit equal (EPI_HEAD with the fold, plain forward, split-K slabs; ragged rows)."""
+    Xh, Yh = pkg.synth_mnist(B)
+    X, Y = dev(Xh), dev(Yh)
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("LBF_GEMM_DIRECT", flag)
+        net = pkg.Mlp(ctx, dims, acts)
+        P = net.init_params(21, "cpu")
+        loss, g = net.loss_grad(P, X, Y, l2=1e-4)
+        out = net.forward(P, X)
+        res.append((loss, g.clone(), out.clone()))
+    (l0, g0, o0), (l1, g1, o1) = res
+    assert torch.equal(o0, o1)
+    assert l0 == l1
+    assert bool(torch.isfinite(g1).all())
+    assert torch.equal(g0, g1)
