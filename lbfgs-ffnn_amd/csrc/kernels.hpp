@@ -77,7 +77,7 @@ struct GemmDesc {
   float *fin_out = nullptr;
   // 32 x 128 tiles with a k-contiguous A and mn-contiguous B: the direct-operand kernel (operands from L2
   // straight into registers) instead of the LDS-DMA one; bitwise the same results
-  bool direct = true;
+  bool direct = false;
 };
 // Output tiles of a GEMM launch (the fin_cnt words it needs)
 long long gemm_tiles(const GemmDesc &d);
