@@ -179,7 +179,7 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs 
   __shared__ HistSmem sm;
   __shared__ double ws[4];
   __shared__ int s_last;
-  __shared__ int ist_l[IST_ORDER + DIR_MAXM + 4];
+  __shared__ int ist_l[IST_ORDER + GRAM_FIN_MAXM + 4];
   const int c = blockIdx.x, t = threadIdx.x;
   const int count0 = a.g.reset ? 0 : h.ist[IST_COUNT];
   if (!(c < 6 * h.m && c >= 6 * count0)) { // only the columns in use (live pairs and the self block)
@@ -287,11 +287,28 @@ void dir_sweep(hipStream_t s, const DirArgs &a) {
   LBF_KERNEL_CHECK();
 }
 
-void dir_fin(hipStream_t s, const DirArgs &a) {
+static void cols_fin_launch(hipStream_t s, const DirArgs &a) {
+  static bool attr_set = false;
+  if (!attr_set) { // m up to GRAM_FIN_MAXM: ~100 KB of dynamic LDS
+    LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(dir_cols_fin_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 16 * 1024));
+    attr_set = true;
+  }
   const int m = a.g.h.m;
   const size_t shmem = (size_t(3) * m * m + 2 * size_t(a.g.h.slots) * a.g.h.slots + a.g.h.slots) * sizeof(double);
   hipLaunchKernelGGL(dir_cols_fin_kernel, dim3(unsigned(dir_ncols(m))), dim3(DF_THREADS), shmem, s, a);
   LBF_KERNEL_CHECK();
+}
+
+void dir_fin(hipStream_t s, const DirArgs &a) { cols_fin_launch(s, a); }
+
+bool gram_fin_supported(int m) { return m >= 0 && m <= GRAM_FIN_MAXM; }
+
+void gram_fin(hipStream_t s, const DirArgs &a) {
+  LBF_REQUIRE(gram_fin_supported(a.g.h.m), "gram_fin: history size");
+  LBF_REQUIRE(a.want_dir == 0 || a.want_dir == 1, "gram_fin: want_dir 0 / 1");
+  LBF_REQUIRE(a.nb == gram_nwg(a.g.h.n), "gram_fin: one partial row per Gram workgroup");
+  cols_fin_launch(s, a);
 }
 
 } // namespace lbf

@@ -310,8 +310,9 @@ struct GramArgs {
 // Number of fp64 partial columns per workgroup and the workgroup count for a given n.
 int gram_ncols(int m);
 int gram_nwg(long long n);
-// Chooses the write slot (device), then streams the history once computing all new dots.
-void gram_update(hipStream_t s, const GramArgs &a, double *partials);
+// Chooses the write slot (device), then streams the history once computing all new dots. Partials
+// [gram_nwg(n)][gram_ncols(m)], or transposed ([gram_ncols(m)][gram_nwg(n)], gram_fin's input).
+void gram_update(hipStream_t s, const GramArgs &a, double *partials, int transposed = 0);
 
 struct CoefArgs {
   HistView h;
@@ -381,6 +382,12 @@ int dir_cols_per_block(int m, long long n);
 int dir_ncols(int m);
 void dir_sweep(hipStream_t s, const DirArgs &a);
 void dir_fin(hipStream_t s, const DirArgs &a);
+// The same column sums + last-block history step for gram_update's transposed partials (the unfused
+// L-BFGS path: n > 2M or m > TAIL_MAXM), replacing fold_rows + hist_step: a.rows = the partials,
+// a.nb = gram_nwg(n). m <= GRAM_FIN_MAXM (LDS of the fused step).
+constexpr int GRAM_FIN_MAXM = 52;
+bool gram_fin_supported(int m);
+void gram_fin(hipStream_t s, const DirArgs &a);
 
 struct CombineArgs {
   HistView h;

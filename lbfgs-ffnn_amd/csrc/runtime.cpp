@@ -1019,6 +1019,12 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
     dcount_.resize(1);
     LBF_HIP(hipMemsetAsync(dcount_.get(), 0, sizeof(unsigned), ctx_->stream));
   }
+  gfin_on_ = gram_fin_supported(m) && env_int("LBF_GRAM_FIN", 1) != 0;
+  if (gfin_on_) {
+    gdots_.resize(size_t(gram_ncols(m)));
+    gcount_.resize(1);
+    LBF_HIP(hipMemsetAsync(gcount_.get(), 0, sizeof(unsigned), ctx_->stream));
+  }
 }
 
 void History::reset() { hist_reset(ctx_->stream, v_); }
@@ -1049,6 +1055,26 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
     }
     ProfScope ps(ctx_, PK_COEF);
     dir_fin(s, d);
+    return;
+  }
+  if (gfin_on_ && (want_dir == 0 || want_dir == 1)) {
+    // Gram sweep with transposed partials, then one block per column whose last arrival runs the step:
+    // two launches instead of gram -> fold_rows -> hist_step
+    DirArgs d;
+    d.g = g;
+    d.want_dir = want_dir;
+    d.iter = iter;
+    d.dsign = dsign;
+    d.rows = part_.get();
+    d.dots = gdots_.get();
+    d.nb = gram_nwg(v_.n);
+    d.cols_done = gcount_.get();
+    {
+      ProfScope ps(ctx_, PK_GRAM);
+      gram_update(s, g, part_.get(), 1);
+    }
+    ProfScope ps(ctx_, PK_COEF);
+    gram_fin(s, d);
     return;
   }
   {

@@ -223,6 +223,10 @@ private:
   DevBuf<double> drows_, ddots_;
   DevBuf<unsigned> dcount_;
   bool dir_on_ = false;
+  // unfused path: Gram sweep (transposed partials in part_) + column sums whose last block runs the step
+  DevBuf<double> gdots_;
+  DevBuf<unsigned> gcount_;
+  bool gfin_on_ = false;
 };
 
 struct LbfgsRecordRow {

@@ -791,8 +791,32 @@ int gram_nwg(long long n) {
 static long long gram_chunk(long long n, int nwg) { return cdiv(cdiv(n, nwg), 4) * 4; }
 
 
+// The new vectors of one element: gram_kernel's arithmetic (s = sa - sb, y = (ya - yb) * yscale into the
+// ring's write slot, g = ga - gb + gc into g_out), staged in LDS, self dots accumulated.
+struct GramNew {
+  float sv, yv, gv;
+};
+__device__ __forceinline__ GramNew gram_new(const GramArgs &a, float sa, float sb, float ya, float yb, float ga, float gb,
+                                            float gc, float ysc) {
+  GramNew r{0.f, 0.f, 0.f};
+  if (a.has_pair) {
+    r.sv = sa - sb;
+    r.yv = (ya - yb) * ysc;
+  }
+  if (a.has_g) {
+    r.gv = ga;
+    if (a.gb) r.gv = r.gv - gb;
+    if (a.gc) r.gv = r.gv + gc;
+  }
+  return r;
+}
+
+// tr: partials stored transposed, [ncols][gridDim.x] (each column contiguous for gram_fin's column sums);
+// else [gridDim.x][ncols] (hist_step / fold_rows). vec: every operand and the ring 16-B aligned (host
+// check), so the new vectors are formed from 16-B loads, all issued before the first use.
 template <int U, bool NT>
-__global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, long long chunk, double *partials) {
+__global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, long long chunk, double *partials, int tr,
+                                                            int vec) {
   if (a.h.abort && *a.h.abort) return;
   KT(16);
   extern __shared__ __attribute__((aligned(16))) float sh[];
@@ -811,38 +835,74 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
   float *Sw = h.S + (long long)w * h.ld + e0;
   float *Yw = h.Y + (long long)w * h.ld + e0;
   const float ysc = float(a.yscale);
-  for (int i = threadIdx.x; i < len; i += blockDim.x) {
-    const long long e = e0 + i;
-    float sv = 0.f, yv = 0.f, gv = 0.f;
-    if (a.has_pair) {
-      sv = a.sa[e] - a.sb[e];
-      yv = (a.ya[e] - a.yb[e]) * ysc;
-      Sw[i] = sv;
-      Yw[i] = yv;
-    }
-    if (a.has_g) {
-      gv = a.ga[e];
-      if (a.gb) gv = gv - a.gb[e];
-      if (a.gc) gv = gv + a.gc[e];
-      if (a.g_out) a.g_out[e] = gv;
-    }
-    ls[i] = sv;
-    ly[i] = yv;
-    lg[i] = gv;
-    const double s = sv, y = yv, g = gv;
+  auto put = [&](int i, const GramNew &r) {
+    ls[i] = r.sv;
+    ly[i] = r.yv;
+    lg[i] = r.gv;
+    const double s = r.sv, y = r.yv, g = r.gv;
     self[0] += s * s;
     self[1] += s * y;
     self[2] += y * y;
     self[3] += g * s;
     self[4] += g * y;
     self[5] += g * g;
+  };
+  int i_scalar = 0;
+  if (vec) { // two quads per thread per round, all seven operand loads of both issued up front
+    const int nq = len >> 2;
+    const float *dflt = a.ga ? a.ga : a.sa; // null operands read this and are masked
+    for (int q0 = threadIdx.x; q0 < nq; q0 += 2 * GRAM_THREADS) {
+      f32x4 op[2][7];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int q = min(q0 + u * GRAM_THREADS, nq - 1);
+        const long long e = e0 + 4LL * q;
+        const float *src[7] = {a.sa, a.sb, a.ya, a.yb, a.ga, a.gb, a.gc};
+#pragma unroll
+        for (int j = 0; j < 7; ++j) op[u][j] = *reinterpret_cast<const f32x4 *>((src[j] ? src[j] : dflt) + e);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int q = q0 + u * GRAM_THREADS;
+        if (q >= nq) break;
+        f32x4 s4, y4, g4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const GramNew r = gram_new(a, op[u][0][c], op[u][1][c], op[u][2][c], op[u][3][c], op[u][4][c], op[u][5][c],
+                                     op[u][6][c], ysc);
+          s4[c] = r.sv;
+          y4[c] = r.yv;
+          g4[c] = r.gv;
+          put(4 * q + c, r);
+        }
+        if (a.has_pair) {
+          *reinterpret_cast<f32x4 *>(Sw + 4 * q) = s4;
+          *reinterpret_cast<f32x4 *>(Yw + 4 * q) = y4;
+        }
+        if (a.has_g && a.g_out) *reinterpret_cast<f32x4 *>(a.g_out + e0 + 4 * q) = g4;
+      }
+    }
+    i_scalar = 4 * nq;
+  }
+  for (int i = i_scalar + int(threadIdx.x); i < len; i += blockDim.x) {
+    const long long e = e0 + i;
+    const GramNew r = gram_new(a, a.has_pair ? a.sa[e] : 0.f, a.has_pair ? a.sb[e] : 0.f, a.has_pair ? a.ya[e] : 0.f,
+                               a.has_pair ? a.yb[e] : 0.f, a.has_g ? a.ga[e] : 0.f, a.gb ? a.gb[e] : 0.f,
+                               a.gc ? a.gc[e] : 0.f, ysc);
+    if (a.has_pair) {
+      Sw[i] = r.sv;
+      Yw[i] = r.yv;
+    }
+    if (a.has_g && a.g_out) a.g_out[e] = r.gv;
+    put(i, r);
   }
   KT(17);
   block_sum<6>(self, scratch); // includes __syncthreads: LDS vectors complete after this
   KT(18);
-  double *out = partials + (long long)blockIdx.x * ncols;
+  const long long rs = tr ? (long long)gridDim.x : 1LL; // column stride of the partial table
+  double *out = partials + (tr ? (long long)blockIdx.x : (long long)blockIdx.x * ncols);
   if (threadIdx.x == 0)
-    for (int j = 0; j < 6; ++j) out[6 * h.m + j] = self[j];
+    for (int j = 0; j < 6; ++j) out[(6 * h.m + j) * rs] = self[j];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int v = wave; v < 2 * count; v += nw) {
@@ -850,9 +910,9 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
     const int slot = h.ist[IST_ORDER + li];
     if (a.has_pair && slot == w) { // overwritten in this sweep (CUDA full ring): dots from the self block
       if (lane == 0) {
-        out[6 * li + (v < count ? 0 : 1)] = 0.0;
-        out[6 * li + (v < count ? 2 : 3)] = 0.0;
-        out[6 * li + (v < count ? 4 : 5)] = 0.0;
+        out[(6 * li + (v < count ? 0 : 1)) * rs] = 0.0;
+        out[(6 * li + (v < count ? 2 : 3)) * rs] = 0.0;
+        out[(6 * li + (v < count ? 4 : 5)) * rs] = 0.0;
       }
       continue;
     }
@@ -896,15 +956,15 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
     dg = wave_sum(dg);
     if (lane == 0) {
       const int c = v < count ? 0 : 1;
-      out[6 * li + c + 0] = ds;
-      out[6 * li + c + 2] = dy;
-      out[6 * li + c + 4] = dg;
+      out[(6 * li + c + 0) * rs] = ds;
+      out[(6 * li + c + 2) * rs] = dy;
+      out[(6 * li + c + 4) * rs] = dg;
     }
   }
   KT(19);
 }
 
-void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
+void gram_update(hipStream_t s, const GramArgs &a, double *partials, int transposed) {
   const int nwg = gram_nwg(a.h.n);
   const long long chunk = gram_chunk(a.h.n, nwg);
   const size_t shmem = size_t(3 * chunk) * sizeof(float);
@@ -920,12 +980,22 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials) {
     attr_set = true;
   }
   const bool nt = hist_nt(a.h);
+  auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }; // null passes
+  static const int vec_on = env_int("LBF_GRAM_VEC", 1);
+  const int vec = vec_on && (a.ga || a.sa) && chunk % 4 == 0 && a.h.ld % 4 == 0 && al16(a.h.S) && al16(a.h.Y) &&
+                  al16(a.sa) && al16(a.sb) && al16(a.ya) && al16(a.yb) && al16(a.ga) && al16(a.gb) && al16(a.gc) &&
+                  al16(a.g_out);
+  const int tr = transposed ? 1 : 0;
   if (U == 8) {
-    if (nt) hipLaunchKernelGGL((gram_kernel<8, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
-    else hipLaunchKernelGGL((gram_kernel<8, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
+    if (nt)
+      hipLaunchKernelGGL((gram_kernel<8, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
+    else
+      hipLaunchKernelGGL((gram_kernel<8, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
   } else {
-    if (nt) hipLaunchKernelGGL((gram_kernel<4, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
-    else hipLaunchKernelGGL((gram_kernel<4, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials);
+    if (nt)
+      hipLaunchKernelGGL((gram_kernel<4, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
+    else
+      hipLaunchKernelGGL((gram_kernel<4, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
   }
   LBF_KERNEL_CHECK();
 }

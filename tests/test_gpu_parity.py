@@ -211,6 +211,36 @@ def test_lbfgs_wolfe_trajectory(ctx, pkg, O, m):
     assert np.all(np.diff(hist["loss"]) <= 1e-7)
 
 
+@pytest.mark.parametrize("line_search", ["wolfe", "armijo"])
+def test_gram_fin_route_matches_oracle(ctx, pkg, O, monkeypatch, line_search):
+    """m = 40 > TAIL_MAXM: every direction takes the unfused history path (lbfgs.hpp:106-139 /
+    lbfgs.cuh:206-261), whose Gram partials are now summed per column by a launch whose last block runs
+    the history step (gram_fin). Against the oracle, and against the fold_rows + hist_step route it
+    replaces (LBF_GRAM_FIN=0): same line-search decisions, losses within fp64-summation-order rounding."""
+    dims, acts = [784, 32, 10], ["relu", "linear"]
+    Xh, Yh = pkg.synth_mnist(256)
+    runs = {}
+    for fin in ("1", "0"):
+        monkeypatch.setenv("LBF_GRAM_FIN", fin)
+        net = pkg.Mlp(ctx, dims, acts)
+        P = net.init_params(123, "cpu" if line_search == "wolfe" else "cuda")
+        P0 = host(P)
+        runs[fin] = pkg.lbfgs_solve(net, P, dev(Xh), dev(Yh), line_search=line_search, m=40, max_iters=25,
+                                    tol=0.0)[0]
+    net_o = O.Net(dims, acts)
+    if line_search == "wolfe":
+        _, rec, _ = net_o.lbfgs_wolfe(P0, Xh.astype(np.float64), Yh.astype(np.float64), m=40, max_iters=25)
+    else:
+        _, rec = net_o.lbfgs_armijo(P0, Xh.astype(np.float64), Yh.astype(np.float64), m=40, max_iters=25,
+                                    fp32=True)
+    a, b = runs["1"], runs["0"]
+    assert np.array_equal(a["ls_trials"][:15], b["ls_trials"][:15])
+    assert np.abs(a["loss"][:15] - b["loss"][:15]).max() <= 1e-5 * np.abs(b["loss"][:15]).max()
+    r = np.abs(a["loss"][:10] - rec[:10, 0]) / np.abs(rec[:10, 0])
+    assert r.max() <= 1e-3, r
+    assert np.array_equal(a["ls_trials"][:8], rec[:8, 4].astype(int))
+
+
 def test_lbfgs_armijo_trajectory(ctx, pkg, O):
     """CUDA semantics (lbfgs.cuh:39-194) vs the oracle's fp32 instantiation of the same algorithm."""
     dims, acts = [784, 32, 10], ["relu", "linear"]
