@@ -247,6 +247,16 @@ int lbf_sgd_solve(lbf_mlp *net, const lbf_sgd_params *prm, float *d_params, cons
 
 int lbf_slbfgs_solve(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params, const float *d_X,
                      const float *d_Y, long long N, lbf_record *rec, lbf_solve_info *info);
+/* Stateful S-LBFGS (benchmarking, and callers that check progress between epochs): begin copies nothing
+ * yet; iterate runs up to `epochs` more epochs (returns early on convergence) with d_params updated after
+ * each call; end releases the solver. One begin + iterate(max_epochs) is lbf_slbfgs_solve. With
+ * LBF_SLBFGS_GRAPH=1 (single rank), an epoch whose launch sequence repeats runs from a hipGraph captured
+ * from its second occurrence on (bitwise the eager epochs; measured slower on ROCm 7.2, off by default). */
+typedef struct lbf_slbfgs lbf_slbfgs;
+int lbf_slbfgs_begin(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params, const float *d_X,
+                     const float *d_Y, long long N, lbf_slbfgs **out);
+int lbf_slbfgs_iterate(lbf_slbfgs *s, int epochs, lbf_record *rec, lbf_solve_info *info);
+int lbf_slbfgs_end(lbf_slbfgs *s);
 
 /* ---- profiling: HIP-event timing of every kernel class on the context stream (benchmark use).
  * Section id = kind*16 + layer; kinds: 0 fwd GEMM, 1 dW GEMM, 2 dX GEMM, 3 loss, 4 split-K reduce,

@@ -546,6 +546,38 @@ int lbf_slbfgs_solve(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params
   });
 }
 
+struct lbf_slbfgs {
+  std::unique_ptr<SlbfgsSolver> s;
+};
+
+int lbf_slbfgs_begin(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params, const float *d_X,
+                     const float *d_Y, long long N, lbf_slbfgs **out) {
+  return guard([&] {
+    LBF_REQUIRE(net && prm && out, "null argument");
+    net->ctx->c.set_device();
+    auto *h = new lbf_slbfgs();
+    try {
+      h->s.reset(new SlbfgsSolver(net->net.get(), *prm, d_params, d_X, d_Y, N));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int lbf_slbfgs_iterate(lbf_slbfgs *s, int epochs, lbf_record *rec, lbf_solve_info *info) {
+  return guard([&] {
+    LBF_REQUIRE(s && epochs >= 0, "bad argument");
+    s->s->iterate(epochs, rec);
+    s->s->info(info);
+  });
+}
+
+int lbf_slbfgs_end(lbf_slbfgs *s) {
+  return guard([&] { delete s; });
+}
+
 int lbf_prof_enable(lbf_ctx *ctx, int on) {
   return guard([&] {
     LBF_REQUIRE(ctx, "ctx");

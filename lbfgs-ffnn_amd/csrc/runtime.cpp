@@ -22,12 +22,40 @@ Profiler::~Profiler() {
 
 size_t Profiler::mark(hipStream_t s) {
   if (used == pool.size()) {
+    LBF_REQUIRE(!capture, "profiler: event pool exhausted inside a graph capture");
     hipEvent_t e;
     LBF_HIP(hipEventCreate(&e));
     pool.push_back(e);
   }
-  LBF_HIP(hipEventRecord(pool[used], s));
+  if (capture) {
+    // an event-record node of the graph being captured, appended behind the stream's current capture
+    // dependencies and made the new one (hipEventRecordWithFlags(..., hipEventRecordExternal) is refused
+    // inside a capture by this ROCm)
+    hipStreamCaptureStatus st;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t *deps = nullptr;
+    size_t ndeps = 0;
+    LBF_HIP(hipStreamGetCaptureInfo_v2(s, &st, nullptr, &g, &deps, &ndeps));
+    LBF_REQUIRE(st == hipStreamCaptureStatusActive && g, "profiler: stream not capturing");
+    hipGraphNode_t node;
+    LBF_HIP(hipGraphAddEventRecordNode(&node, g, deps, ndeps, pool[used]));
+    LBF_HIP(hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies));
+  } else {
+    LBF_HIP(hipEventRecord(pool[used], s));
+  }
+  ++marks;
   return used++;
+}
+
+void Profiler::add(const Rec &r, float t) {
+  if (size_t(r.id) >= ms.size()) {
+    ms.resize(r.id + 1, 0.0);
+    cnt.resize(r.id + 1, 0);
+    work.resize(r.id + 1, 0.0);
+  }
+  ms[r.id] += t;
+  cnt[r.id] += 1;
+  work[r.id] += r.work;
 }
 
 void Profiler::resolve() {
@@ -36,17 +64,47 @@ void Profiler::resolve() {
   for (auto &r : recs) {
     float t = 0.f;
     LBF_HIP(hipEventElapsedTime(&t, pool[r.a], pool[r.b]));
-    if (size_t(r.id) >= ms.size()) {
-      ms.resize(r.id + 1, 0.0);
-      cnt.resize(r.id + 1, 0);
-      work.resize(r.id + 1, 0.0);
-    }
-    ms[r.id] += t;
-    cnt[r.id] += 1;
-    work[r.id] += r.work;
+    add(r, t);
   }
   recs.clear();
   used = 0;
+}
+
+void Profiler::capture_begin(long long reserve) {
+  resolve();
+  while ((long long)pool.size() < reserve) {
+    hipEvent_t e;
+    LBF_HIP(hipEventCreate(&e));
+    pool.push_back(e);
+  }
+  capture = true;
+}
+
+GraphProf Profiler::capture_end() {
+  capture = false;
+  GraphProf g;
+  g.ev.assign(pool.begin(), pool.begin() + long(used));
+  g.recs = recs;
+  pool.erase(pool.begin(), pool.begin() + long(used));
+  recs.clear();
+  used = 0;
+  return g;
+}
+
+void Profiler::add_graph(const GraphProf &g) {
+  if (g.recs.empty()) return;
+  LBF_HIP(hipEventSynchronize(g.ev.back()));
+  for (const auto &r : g.recs) {
+    float t = 0.f;
+    LBF_HIP(hipEventElapsedTime(&t, g.ev[r.a], g.ev[r.b]));
+    add(r, t);
+  }
+}
+
+void GraphProf::release() {
+  for (auto e : ev) (void)hipEventDestroy(e);
+  ev.clear();
+  recs.clear();
 }
 
 void Profiler::merge_into(Profiler &dst) {

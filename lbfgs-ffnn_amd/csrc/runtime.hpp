@@ -14,18 +14,28 @@ namespace lbf {
 // Per-kernel-class timing with HIP events on the launch stream (enabled by the benchmark only).
 enum ProfKind : int { PK_FWD = 0, PK_DW = 1, PK_DX = 2, PK_LOSS = 3, PK_SLAB = 4, PK_FINAL = 5, PK_GRAM = 6,
                       PK_COEF = 7, PK_COMBINE = 8, PK_AXPY = 9, PK_ALLREDUCE = 10 };
+struct ProfRec { int id; size_t a, b; double work; };
+// Timed sections captured into a hipGraph: event-record nodes on events the graph owns, read after each
+// replay (Profiler::add_graph).
+struct GraphProf {
+  std::vector<hipEvent_t> ev;
+  std::vector<ProfRec> recs;
+  void release();
+};
 struct Profiler {
   bool on = false;
   int only = -1; // section filter (-1: all)
   int every = 1;  // sample every k-th launch of a wanted section
   long long seen = 0;
+  long long marks = 0;    // events recorded so far (sizes a capture's event pool)
+  bool capture = false;   // marks are external event-record nodes of the graph being captured
   bool want(int id) {
     if (!on || (only >= 0 && only != id)) return false;
     return every <= 1 || (seen++ % every) == 0;
   }
   std::vector<hipEvent_t> pool;
   size_t used = 0;
-  struct Rec { int id; size_t a, b; double work; };
+  using Rec = ProfRec;
   std::vector<Rec> recs;
   std::vector<double> ms;      // by section id
   std::vector<long long> cnt;  // by section id
@@ -34,6 +44,12 @@ struct Profiler {
   size_t mark(hipStream_t s);
   void resolve();
   void merge_into(Profiler &dst); // resolve this one and add its totals to dst's
+  void add(const Rec &r, float t);
+  // Capture: resolve, then (capture_begin) create `reserve` events up front (no event creation inside the
+  // capture) and record the marks as graph nodes; capture_end hands the events and records to the graph.
+  void capture_begin(long long reserve);
+  GraphProf capture_end();
+  void add_graph(const GraphProf &g); // after a replay has completed
 };
 
 struct Ctx {
@@ -147,6 +163,10 @@ public:
   void discard_evals(long long k, long long B) { // speculative evaluations (B rows each) that were aborted
     evals_ -= k;
     rows_ -= k * B;
+  }
+  void add_counts(long long evals, long long rows) { // evaluations a replayed graph ran
+    evals_ += evals;
+    rows_ += rows;
   }
 
 private:

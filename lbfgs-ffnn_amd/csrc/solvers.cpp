@@ -589,6 +589,14 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
   evals0_ = net->evals();
   rows0_ = net->rows();
   anchor_pre_ = env_int("LBF_SLBFGS_ANCHOR", 0) != 0; // the twin measured ~2-3 % faster (profiles/r03)
+  rng_.seed(prm.seed);
+  sampler_.reset(new MinibatchSampler(size_t(N)));
+  // epoch graphs (LBF_SLBFGS_GRAPH=1; off by default): not with a communicator (the collectives stay eager)
+  // nor with the synchronous pair trace. Measured slower than the eager epochs on ROCm 7.2
+  // (profiles/r03b/README.md): hipGraphLaunch spends about as much host time per node as an eager launch
+  // (≈ 20 ms per cfg-4 epoch), and the replay runs every node on one queue, so the twin's anchor
+  // gradients no longer overlap the context stream's chain (kernel trace: 5503 launches on one stream).
+  graph_on_ = env_int("LBF_SLBFGS_GRAPH", 0) != 0 && !ctx_->dp() && !prm.pair_trace;
   if (env_int("LBF_SLBFGS_TWIN", 1)) {
     tctx_.reset(new Ctx());
     tctx_->device = ctx_->device;
@@ -664,15 +672,321 @@ void SlbfgsSolver::eval_pair(const float *wa, const float *wb, float *gab, long 
 // order; because no sample depends on device values, each epoch's index lists are drawn up front
 // and uploaded once, and the epoch then runs without a host synchronisation.
 int SlbfgsSolver::run(lbf_record *rec) {
-  ctx_->set_device();
-  hipStream_t s = ctx_->stream;
+  iterate(prm_.max_epochs, rec);
+  return iters_;
+}
+
+// An epoch's index lists in the reference's RNG order (s_lbfgs.hpp:212-266). Every rank draws the same
+// lists and keeps only its slice [b*rk/nr, b*(rk+1)/nr) of each batch. The minibatch slices come first
+// in `flat` (minibatch t's rows right after minibatch t-1's, as Mlp::batch_grads reads them), the
+// Hessian-batch slices after them; the draws stay in RNG order.
+void SlbfgsSolver::draw_epoch(bool u_seen, EpochDraw &d) {
   const int nr = ctx_->nranks, rk = ctx_->rank;
+  const int m_inner = int(std::max(1LL, N_ / prm_.b));
+  const int L = prm_.L;
+  d.flat.clear();
+  d.hflat.clear();
+  d.mb.assign(size_t(m_inner), Slice{});
+  d.hb.assign(size_t(m_inner), Slice{-1, 0, 0});
+  auto take = [&](size_t bsz, std::vector<int> &dst) {
+    d.batch.clear();
+    const long long tot = (long long)sampler_->draw(bsz, rng_, d.batch);
+    const long long a0 = tot * rk / nr, a1 = tot * (rk + 1) / nr;
+    Slice sl{(long long)dst.size(), a1 - a0, tot};
+    dst.insert(dst.end(), d.batch.begin() + a0, d.batch.begin() + a1);
+    return sl;
+  };
+  int whist_size = 1;
+  for (int t = 0; t < m_inner; ++t) {
+    d.mb[t] = take(size_t(prm_.b), d.flat);
+    whist_size = std::min(whist_size + 1, L + 1);
+    if (t > 0 && t % L == 0) {
+      if (u_seen) d.hb[t] = take(size_t(prm_.b_H), d.hflat);
+      u_seen = true;
+    }
+  }
+  const long long nmb_rows = (long long)d.flat.size();
+  for (Slice &h : d.hb)
+    if (h.off >= 0) h.off += nmb_rows;
+  d.flat.insert(d.flat.end(), d.hflat.begin(), d.hflat.end());
+  d.pick = -1;
+  if (whist_size >= 2) {
+    std::uniform_int_distribution<size_t> pk(0, size_t(whist_size) - 2); // s_lbfgs.hpp:266
+    d.pick = int(pk(rng_));
+  }
+  d.u_seen = u_seen;
+}
+
+int SlbfgsSolver::wh_push_slot() {
+  const int L = prm_.L;
+  int slot;
+  if (wh_count_ < L + 1) {
+    slot = (wh_head_ + wh_count_) % (L + 1);
+    ++wh_count_;
+  } else {
+    slot = wh_head_;
+    wh_head_ = (wh_head_ + 1) % (L + 1);
+  }
+  return slot;
+}
+
+// The inner steps of one epoch (s_lbfgs.hpp:218-262), from the anchor copy to the last step; the epoch's
+// rows are gathered (xg_, yg_) and the context stream is idle when this is called.
+void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
+  hipStream_t s = ctx_->stream;
   const long long In = net_->layers().front().in, Out = net_->layers().back().out;
   const long long ld = round4(n_);
   const int m_inner = int(std::max(1LL, N_ / prm_.b));
   const int L = prm_.L;
-  std::mt19937 rng(prm_.seed);
-  LBF_HIP(hipMemcpyAsync(w_.get(), user_params_, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+  const bool dp = ctx_->dp();
+  const auto &mb = d.mb, &hb = d.hb;
+  LBF_HIP(hipMemcpyAsync(wt_.get(), w_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+  wh_head_ = 0;
+  wh_count_ = 0;
+  {
+    const int slot = wh_push_slot();
+    LBF_HIP(hipMemcpyAsync(wh_.get() + slot * ld, wt_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice,
+                           s));
+  }
+  // With the twin stream, the minibatch gradients at the anchor w (fixed for the epoch, and independent
+  // of the iterates) run one step ahead on it, double-buffered in the second half of gpair_[t & 1]: step
+  // t's evaluation at w_t and its direction on the context stream then overlap the twin's gradient of
+  // minibatch t + 1 at w, instead of joining the two evaluations of each step. Same evaluations on the
+  // same inputs: bitwise the same. Data parallel: both halves are this rank's partial sums until the
+  // step's one all-reduce of the whole block.
+  auto g1 = [&](int t) { return gpair_[t & 1].get(); };
+  auto g2 = [&](int t) { return gpair_[t & 1].get() + ng_; };
+  auto rows_x = [&](const Slice &sl) { return xg_.get() + sl.off * In; };
+  auto rows_y = [&](const Slice &sl) { return yg_.get() + sl.off * Out; };
+  const bool pre = pre_;
+  if (pre) {
+    const long long cnt0 = mb[0].cnt;
+    net_->batch_grads(w_.get(), xg_.get(), yg_.get(), m_inner, cnt0, 1.0 / double(mb[0].total), prm_.lambda,
+                      gmb_.get(), ng_, dp);
+  }
+  auto gpre = [&](int t) { return gmb_.get() + (long long)t * ng_; };
+  auto anchor_ahead = [&](int t) { // twin stream: the anchor half of step t's block
+    const Slice &sl = mb[t];
+    LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_free_[t & 1], 0)); // step t - 2's direction read it
+    if (dp)
+      tnet_->loss_grad_local(w_.get(), g2(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, 1.0 / double(sl.total));
+    else
+      tnet_->loss_grad(w_.get(), g2(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, 1.0 / double(sl.total),
+                       prm_.lambda, nullptr, nullptr);
+    LBF_HIP(hipEventRecord(ev_g2_[t & 1], tctx_->stream));
+  };
+  // LBF_HOST_TIMING=2: host time of each part of the inner step's enqueue (where the epoch's host-bound
+  // ~130 us per step go)
+  static const int host_timing = env_int("LBF_HOST_TIMING", 0);
+  using hclk = std::chrono::steady_clock;
+  double ht[6] = {0, 0, 0, 0, 0, 0}; // twin, main eval, events, direction, combine, Hessian step
+  auto tick = [&]() { return host_timing >= 2 ? hclk::now() : hclk::time_point(); };
+  auto tock = [&](int i, hclk::time_point a) {
+    if (host_timing >= 2) ht[i] += std::chrono::duration<double, std::micro>(hclk::now() - a).count();
+  };
+  if (tnet_ && !pre) {
+    // the twin may reuse block t & 1 once the direction of step t - 2 has read it: nothing of this epoch
+    // has yet (recorded here so that a captured epoch's first waits are on events of the capture)
+    LBF_HIP(hipEventRecord(ev_free_[0], s));
+    LBF_HIP(hipEventRecord(ev_free_[1], s));
+    anchor_ahead(0);
+  }
+  for (int t = 0; t < m_inner; ++t) {
+    const Slice &sl = mb[t];
+    const double inv_b = 1.0 / double(sl.total);
+    const float *gb = g2(t);
+    if (pre) {
+      if (dp) {
+        net_->loss_grad_local(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b);
+        LBF_HIP(hipMemcpyAsync(g2(t), gpre(t), size_t(ng_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+        reduce_pair(wt_.get(), w_.get(), g1(t), inv_b);
+      } else {
+        net_->loss_grad(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda, nullptr,
+                        nullptr);
+        gb = gpre(t);
+      }
+    } else if (tnet_) {
+      auto h0 = tick();
+      if (t + 1 < m_inner) anchor_ahead(t + 1);
+      tock(0, h0);
+      h0 = tick();
+      if (dp)
+        net_->loss_grad_local(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b);
+      else
+        net_->loss_grad(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda, nullptr,
+                        nullptr);
+      tock(1, h0);
+      h0 = tick();
+      LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_g2_[t & 1], 0));
+      tock(2, h0);
+      if (dp) reduce_pair(wt_.get(), w_.get(), g1(t), inv_b);
+    } else {
+      eval_pair(wt_.get(), w_.get(), g1(t), sl.off, sl.cnt, inv_b);
+    }
+    GramArgs ga;
+    ga.policy = POL_SLBFGS;
+    ga.has_g = 1;
+    ga.ga = g1(t);
+    ga.gb = gb;
+    ga.gc = mu_.get();
+    ga.g_out = v_.get();
+    auto h0 = tick();
+    hist_.update(ga, 1, 1, +1.0);
+    tock(3, h0);
+    h0 = tick();
+    if (tnet_ && !pre) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
+    tock(2, h0);
+    h0 = tick();
+    const int slot = wh_push_slot();
+    // wt = wt - step * r ; w_history.push_back(wt)
+    hist_.combine(v_.get(), nullptr, wt_.get(), wt_.get(), wh_.get() + slot * ld, false, -prm_.step);
+    tock(4, h0);
+    h0 = tick();
+    if (t > 0 && t % L == 0) {
+      int slots[64];
+      for (int i = 0; i < wh_count_; ++i) slots[i] = wh_slot(i);
+      average_slots(s, n_, wh_.get(), ld, slots, wh_count_, u_.get());
+      if (have_u_) {
+        const Slice &hs = hb[t];
+        const double eps = prm_.fd_eps;
+        lincomb(s, n_, u_.get(), -1.0, up_.get(), s_.get()); // s = u - u_prev
+        GramArgs pa;
+        pa.policy = POL_SLBFGS;
+        pa.has_pair = 1;
+        pa.sa = u_.get();
+        pa.sb = up_.get();
+        float *gp = fdpair_.get(), *gm = fdpair_.get() + ng_;
+        if (prm_.hvp_exact) { // y = H(u) s on the b_H batch, R-operator (hvp.hip)
+          net_->hvp(u_.get(), s_.get(), X_, Y_, idx_.get() + hs.off, hs.cnt, 1.0 / double(hs.total), prm_.lambda,
+                    gp);
+          LBF_HIP(hipMemsetAsync(gm, 0, size_t(n_) * sizeof(float), s));
+          pa.yscale = 1.0;
+        } else { // s_lbfgs.hpp:88-101: central difference of two batch gradients
+          lincomb(s, n_, u_.get(), eps, s_.get(), wp_.get()); // fd_hvp_grads, the two evaluations paired
+          lincomb(s, n_, u_.get(), -eps, s_.get(), wm_.get());
+          eval_pair(wp_.get(), wm_.get(), fdpair_.get(), hs.off, hs.cnt, 1.0 / double(hs.total));
+          pa.yscale = 1.0 / (2.0 * eps);
+        }
+        pa.ya = gp;
+        pa.yb = gm;
+        hist_.update(pa, 0, 1, +1.0);
+        if (prm_.pair_trace && npairs_ < prm_.pair_trace_cap) trace_pair(iters_, t);
+      }
+      LBF_HIP(hipMemcpyAsync(up_.get(), u_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+      have_u_ = true;
+    }
+    tock(5, h0);
+  }
+  if (host_timing >= 2)
+    std::fprintf(stderr, "[lbf host] per inner step (us): twin %.1f, main eval %.1f, events %.1f, direction %.1f, "
+                 "combine %.1f, Hessian step %.1f\n", ht[0] / m_inner, ht[1] / m_inner, ht[2] / m_inner,
+                 ht[3] / m_inner, ht[4] / m_inner, ht[5] / m_inner);
+}
+
+SlbfgsSolver::EpochGraph::~EpochGraph() {
+  if (exec) (void)hipGraphExecDestroy(exec);
+  if (graph) (void)hipGraphDestroy(graph);
+  prof.release();
+  tprof.release();
+}
+
+std::vector<long long> SlbfgsSolver::graph_key(const EpochDraw &d) const {
+  std::vector<long long> k;
+  auto ptr = [](const void *p) { return (long long)reinterpret_cast<uintptr_t>(p); };
+  k.insert(k.end(), {have_u_ ? 1LL : 0LL, pre_ ? 1LL : 0LL, (long long)d.mb.size(), ptr(xg_.get()), ptr(yg_.get()),
+                     ptr(idx_.get()), ptr(gmb_.get())});
+  for (const Slice &sl : d.mb) k.insert(k.end(), {sl.off, sl.cnt, sl.total});
+  for (const Slice &sl : d.hb) k.insert(k.end(), {sl.off, sl.cnt, sl.total});
+  for (const Ctx *c : {ctx_, tctx_.get()}) {
+    if (!c) continue;
+    const Profiler &p = c->prof;
+    k.insert(k.end(), {p.on ? 1LL : 0LL, (long long)p.only, (long long)p.every});
+  }
+  return k;
+}
+
+// Runs this epoch's inner steps from a graph when its launch sequence was captured before (or is seen
+// for the second time now: captured, then launched). Returns false when the steps must run eagerly
+// (first sight: the eager run allocates whatever workspace the sequence needs, which a capture must not).
+bool SlbfgsSolver::epoch_graph(const EpochDraw &d) {
+  hipStream_t s = ctx_->stream;
+  const std::vector<long long> key = graph_key(d);
+  EpochGraph *G = nullptr;
+  for (auto &g : graphs_)
+    if (g->key == key) G = g.get();
+  if (!G) {
+    long long marks = -1;
+    for (auto &sk : seen_keys_)
+      if (sk.first == key) marks = sk.second;
+    if (marks < 0) { // first sight: eager, remembering how many profiler events the sequence records
+      const long long m0 = ctx_->prof.marks + (tctx_ ? tctx_->prof.marks : 0);
+      epoch_steps(d);
+      seen_keys_.emplace_back(key, ctx_->prof.marks + (tctx_ ? tctx_->prof.marks : 0) - m0);
+      if (seen_keys_.size() > 8) seen_keys_.erase(seen_keys_.begin());
+      return true;
+    }
+    std::unique_ptr<EpochGraph> g(new EpochGraph());
+    g->key = key;
+    const long long e0 = net_->evals(), r0 = net_->rows();
+    const long long te0 = tnet_ ? tnet_->evals() : 0, tr0 = tnet_ ? tnet_->rows() : 0;
+    ctx_->prof.capture_begin((long long)ctx_->prof.pool.size() + marks + 64);
+    if (tctx_) tctx_->prof.capture_begin((long long)tctx_->prof.pool.size() + marks + 64);
+    LBF_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+    try {
+      epoch_steps(d);
+    } catch (...) {
+      hipGraph_t tmp = nullptr;
+      (void)hipStreamEndCapture(s, &tmp);
+      if (tmp) (void)hipGraphDestroy(tmp);
+      ctx_->prof.capture_end().release();
+      if (tctx_) tctx_->prof.capture_end().release();
+      throw;
+    }
+    LBF_HIP(hipStreamEndCapture(s, &g->graph));
+    g->prof = ctx_->prof.capture_end();
+    if (tctx_) g->tprof = tctx_->prof.capture_end();
+    LBF_HIP(hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0));
+    g->evals = net_->evals() - e0;
+    g->rows = net_->rows() - r0;
+    g->tevals = tnet_ ? tnet_->evals() - te0 : 0;
+    g->trows = tnet_ ? tnet_->rows() - tr0 : 0;
+    g->wh_head = wh_head_;
+    g->wh_count = wh_count_;
+    g->have_u = have_u_;
+    if (graphs_.size() >= 4) graphs_.erase(graphs_.begin());
+    graphs_.push_back(std::move(g));
+    G = graphs_.back().get();
+  } else { // replay: the host state and counters the captured epoch leaves behind
+    wh_head_ = G->wh_head;
+    wh_count_ = G->wh_count;
+    have_u_ = G->have_u;
+    net_->add_counts(G->evals, G->rows);
+    if (tnet_) tnet_->add_counts(G->tevals, G->trows);
+  }
+  LBF_HIP(hipGraphLaunch(G->exec, s));
+  pending_graph_ = G;
+  return true;
+}
+
+int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
+  ctx_->set_device();
+  hipStream_t s = ctx_->stream;
+  const long long In = net_->layers().front().in, Out = net_->layers().back().out;
+  const long long ld = round4(n_);
+  const int nr = ctx_->nranks, rk = ctx_->rank;
+  const int m_inner = int(std::max(1LL, N_ / prm_.b));
+  if (tctx_) { // the benchmark's section timing covers the twin's launches too (settings may change per call)
+    tctx_->prof.on = ctx_->prof.on;
+    tctx_->prof.only = ctx_->prof.only;
+    if (tctx_->prof.every != ctx_->prof.every) tctx_->prof.seen = 0;
+    tctx_->prof.every = ctx_->prof.every;
+  }
+  if (!started_) {
+    LBF_HIP(hipMemcpyAsync(w_.get(), user_params_, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+    t0_ = std::chrono::steady_clock::now();
+    rec_i_ = rec ? rec->size : 0;
+    started_ = true;
+  }
   // full-batch shard of this rank
   const long long lo = N_ * rk / nr, hi = N_ * (rk + 1) / nr;
   const float *Xs = X_ + lo * In, *Ys = Y_ + lo * Out;
@@ -684,75 +998,24 @@ int SlbfgsSolver::run(lbf_record *rec) {
     LBF_HIP(hipMemcpyAsync(hs_.get(), hist_.scal(), SC_N * sizeof(double), hipMemcpyDeviceToHost, s));
     LBF_HIP(hipStreamSynchronize(s));
   };
-  bool have_u = false, mu_valid = false;
-  // An epoch's index lists: every minibatch, the Hessian batches (only once a u exists), then the anchor
-  // pick, in the reference's RNG order (s_lbfgs.hpp:212-266). No draw depends on device values, so the next
-  // epoch's lists are drawn on the host while the GPU runs the current epoch. Every rank draws the same
-  // lists and keeps only its slice [b*rk/nr, b*(rk+1)/nr) of each batch: `flat` holds those slices.
-  struct Slice {
-    long long off = 0, cnt = 0, total = 0; // offset / count in this rank's flat list, whole batch size
-  };
-  struct EpochDraw {
-    std::vector<int> flat, hflat, batch;
-    std::vector<Slice> mb, hb;
-    int pick = -1;
-    bool u_seen = false; // have_u after the epoch
-  };
-  MinibatchSampler sampler{size_t(N_)};
-  // The minibatch slices come first in `flat` (minibatch t's rows right after minibatch t-1's, as
-  // Mlp::batch_grads reads them), the Hessian-batch slices after them; the draws stay in RNG order.
-  auto draw_epoch = [&](bool u_seen, EpochDraw &d) {
-    d.flat.clear();
-    d.hflat.clear();
-    d.mb.assign(size_t(m_inner), Slice{});
-    d.hb.assign(size_t(m_inner), Slice{-1, 0, 0});
-    auto take = [&](size_t bsz, std::vector<int> &dst) {
-      d.batch.clear();
-      const long long tot = (long long)sampler.draw(bsz, rng, d.batch);
-      const long long a0 = tot * rk / nr, a1 = tot * (rk + 1) / nr;
-      Slice sl{(long long)dst.size(), a1 - a0, tot};
-      dst.insert(dst.end(), d.batch.begin() + a0, d.batch.begin() + a1);
-      return sl;
-    };
-    int whist_size = 1;
-    for (int t = 0; t < m_inner; ++t) {
-      d.mb[t] = take(size_t(prm_.b), d.flat);
-      whist_size = std::min(whist_size + 1, L + 1);
-      if (t > 0 && t % L == 0) {
-        if (u_seen) d.hb[t] = take(size_t(prm_.b_H), d.hflat);
-        u_seen = true;
-      }
-    }
-    const long long nmb_rows = (long long)d.flat.size();
-    for (Slice &h : d.hb)
-      if (h.off >= 0) h.off += nmb_rows;
-    d.flat.insert(d.flat.end(), d.hflat.begin(), d.hflat.end());
-    d.pick = -1;
-    if (whist_size >= 2) {
-      std::uniform_int_distribution<size_t> pk(0, size_t(whist_size) - 2); // s_lbfgs.hpp:266
-      d.pick = int(pk(rng));
-    }
-    d.u_seen = u_seen;
-  };
-  EpochDraw cur, next;
-  bool next_ready = false;
-  const auto t0 = std::chrono::steady_clock::now();
-  int rec_i = rec ? rec->size : 0;
-  iters_ = 0;
-  const bool dp = ctx_->dp();
-  while (iters_ < prm_.max_epochs) {
-    if (!mu_valid) {
+  const int target = iters_ + std::max(0, epochs);
+  const int done0 = iters_;
+  while (iters_ < target && !converged_) {
+    if (!mu_valid_) {
       eval_full(w_.get(), mu_.get());
       read();
     }
-    if (std::sqrt(hs_[SC_TGG]) < prm_.tol) break; // s_lbfgs.hpp:208
+    if (std::sqrt(hs_[SC_TGG]) < prm_.tol) { // s_lbfgs.hpp:208
+      converged_ = true;
+      break;
+    }
     // --- this epoch's samples in reference order (drawn during the previous epoch when it ran) -------
-    if (next_ready) std::swap(cur, next);
-    else draw_epoch(have_u, cur);
-    next_ready = false;
-    const std::vector<int> &flat = cur.flat;
-    const auto &mb = cur.mb, &hb = cur.hb;
-    const int pick = cur.pick;
+    if (next_ready_) std::swap(cur_, next_);
+    else draw_epoch(have_u_, cur_);
+    next_ready_ = false;
+    const std::vector<int> &flat = cur_.flat;
+    const auto &mb = cur_.mb;
+    const int pick = cur_.pick;
     idx_.ensure(std::max<size_t>(1, flat.size()));
     if (!flat.empty())
       LBF_HIP(hipMemcpyAsync(idx_.get(), flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
@@ -762,151 +1025,37 @@ int SlbfgsSolver::run(lbf_record *rec) {
     yg_.ensure(std::max<size_t>(1, flat.size()) * size_t(Out));
     gather_rows(s, X_, In, idx_.get(), (long long)flat.size(), int(In), xg_.get());
     gather_rows(s, Y_, Out, idx_.get(), (long long)flat.size(), int(Out), yg_.get());
-    LBF_HIP(hipStreamSynchronize(s)); // flat is a pageable temporary
-    // --- epoch -----------------------------------------------------------------------------------
-    LBF_HIP(hipMemcpyAsync(wt_.get(), w_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
-    int wh_head = 0, wh_count = 0; // ring of L+1 iterates (w_history)
-    auto wh_slot = [&](int logical) { return (wh_head + logical) % (L + 1); };
-    auto wh_push_slot = [&]() {
-      int slot;
-      if (wh_count < L + 1) {
-        slot = (wh_head + wh_count) % (L + 1);
-        ++wh_count;
-      } else {
-        slot = wh_head;
-        wh_head = (wh_head + 1) % (L + 1);
-      }
-      return slot;
-    };
-    {
-      const int slot = wh_push_slot();
-      LBF_HIP(hipMemcpyAsync(wh_.get() + slot * ld, wt_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice,
-                             s));
-    }
-    // With the twin stream, the minibatch gradients at the anchor w (fixed for the epoch, and independent
-    // of the iterates) run one step ahead on it, double-buffered in the second half of gpair_[t & 1]: step
-    // t's evaluation at w_t and its direction on the context stream then overlap the twin's gradient of
-    // minibatch t + 1 at w, instead of joining the two evaluations of each step. Same evaluations on the
-    // same inputs: bitwise the same. Data parallel: both halves are this rank's partial sums until the
-    // step's one all-reduce of the whole block.
-    auto g1 = [&](int t) { return gpair_[t & 1].get(); };
-    auto g2 = [&](int t) { return gpair_[t & 1].get() + ng_; };
-    auto rows_x = [&](const Slice &sl) { return xg_.get() + sl.off * In; };
-    auto rows_y = [&](const Slice &sl) { return yg_.get() + sl.off * Out; };
     // Anchor gradients of the whole epoch up front (every minibatch slice of this rank the same size, a
     // multiple of 32 rows): one evaluation over the epoch's minibatch rows at w (see gmb_).
     const long long cnt0 = mb[0].cnt;
-    bool pre = anchor_pre_ && cnt0 > 0 && cnt0 % 32 == 0;
-    for (int t = 1; t < m_inner && pre; ++t) pre = mb[t].cnt == cnt0 && mb[t].off == t * cnt0;
-    if (pre) {
+    pre_ = anchor_pre_ && cnt0 > 0 && cnt0 % 32 == 0;
+    for (int t = 1; t < m_inner && pre_; ++t) pre_ = mb[t].cnt == cnt0 && mb[t].off == t * cnt0;
+    if (pre_) {
       const size_t need = size_t(m_inner) * size_t(ng_);
       if (gmb_.size() < need) {
         gmb_.resize(need);
         // the two loss words and the pad of each row are never written: zero (the DP copy sums them)
         LBF_HIP(hipMemsetAsync(gmb_.get(), 0, need * sizeof(float), s));
       }
-      net_->batch_grads(w_.get(), xg_.get(), yg_.get(), m_inner, cnt0, 1.0 / double(mb[0].total), prm_.lambda,
-                        gmb_.get(), ng_, dp);
     }
-    auto gpre = [&](int t) { return gmb_.get() + (long long)t * ng_; };
-    auto anchor_ahead = [&](int t) { // twin stream: the anchor half of step t's block
-      const Slice &sl = mb[t];
-      LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_free_[t & 1], 0)); // step t - 2's direction read it
-      if (dp)
-        tnet_->loss_grad_local(w_.get(), g2(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, 1.0 / double(sl.total));
-      else
-        tnet_->loss_grad(w_.get(), g2(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, 1.0 / double(sl.total),
-                         prm_.lambda, nullptr, nullptr);
-      LBF_HIP(hipEventRecord(ev_g2_[t & 1], tctx_->stream));
-    };
-    // the epoch's gathered rows and w are complete (the context stream was synchronised above)
+    LBF_HIP(hipStreamSynchronize(s)); // flat is a pageable temporary
+    // --- epoch -----------------------------------------------------------------------------------
     static const int host_timing = env_int("LBF_HOST_TIMING", 0);
     const auto th0 = std::chrono::steady_clock::now();
-    if (tnet_ && !pre) anchor_ahead(0);
-    for (int t = 0; t < m_inner; ++t) {
-      const Slice &sl = mb[t];
-      const double inv_b = 1.0 / double(sl.total);
-      const float *gb = g2(t);
-      if (pre) {
-        if (dp) {
-          net_->loss_grad_local(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b);
-          LBF_HIP(hipMemcpyAsync(g2(t), gpre(t), size_t(ng_) * sizeof(float), hipMemcpyDeviceToDevice, s));
-          reduce_pair(wt_.get(), w_.get(), g1(t), inv_b);
-        } else {
-          net_->loss_grad(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda, nullptr,
-                          nullptr);
-          gb = gpre(t);
-        }
-      } else if (tnet_) {
-        if (t + 1 < m_inner) anchor_ahead(t + 1);
-        if (dp)
-          net_->loss_grad_local(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b);
-        else
-          net_->loss_grad(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda, nullptr,
-                          nullptr);
-        LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_g2_[t & 1], 0));
-        if (dp) reduce_pair(wt_.get(), w_.get(), g1(t), inv_b);
-      } else {
-        eval_pair(wt_.get(), w_.get(), g1(t), sl.off, sl.cnt, inv_b);
-      }
-      GramArgs ga;
-      ga.policy = POL_SLBFGS;
-      ga.has_g = 1;
-      ga.ga = g1(t);
-      ga.gb = gb;
-      ga.gc = mu_.get();
-      ga.g_out = v_.get();
-      hist_.update(ga, 1, 1, +1.0);
-      if (tnet_ && !pre) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
-      const int slot = wh_push_slot();
-      // wt = wt - step * r ; w_history.push_back(wt)
-      hist_.combine(v_.get(), nullptr, wt_.get(), wt_.get(), wh_.get() + slot * ld, false, -prm_.step);
-      if (t > 0 && t % L == 0) {
-        int slots[64];
-        for (int i = 0; i < wh_count; ++i) slots[i] = wh_slot(i);
-        average_slots(s, n_, wh_.get(), ld, slots, wh_count, u_.get());
-        if (have_u) {
-          const Slice &hs = hb[t];
-          const double eps = prm_.fd_eps;
-          lincomb(s, n_, u_.get(), -1.0, up_.get(), s_.get()); // s = u - u_prev
-          GramArgs pa;
-          pa.policy = POL_SLBFGS;
-          pa.has_pair = 1;
-          pa.sa = u_.get();
-          pa.sb = up_.get();
-          float *gp = fdpair_.get(), *gm = fdpair_.get() + ng_;
-          if (prm_.hvp_exact) { // y = H(u) s on the b_H batch, R-operator (hvp.hip)
-            net_->hvp(u_.get(), s_.get(), X_, Y_, idx_.get() + hs.off, hs.cnt, 1.0 / double(hs.total), prm_.lambda,
-                      gp);
-            LBF_HIP(hipMemsetAsync(gm, 0, size_t(n_) * sizeof(float), s));
-            pa.yscale = 1.0;
-          } else { // s_lbfgs.hpp:88-101: central difference of two batch gradients
-            lincomb(s, n_, u_.get(), eps, s_.get(), wp_.get()); // fd_hvp_grads, the two evaluations paired
-            lincomb(s, n_, u_.get(), -eps, s_.get(), wm_.get());
-            eval_pair(wp_.get(), wm_.get(), fdpair_.get(), hs.off, hs.cnt, 1.0 / double(hs.total));
-            pa.yscale = 1.0 / (2.0 * eps);
-          }
-          pa.ya = gp;
-          pa.yb = gm;
-          hist_.update(pa, 0, 1, +1.0);
-          if (prm_.pair_trace && npairs_ < prm_.pair_trace_cap) trace_pair(iters_, t);
-        }
-        LBF_HIP(hipMemcpyAsync(up_.get(), u_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
-        have_u = true;
-      }
-    }
+    pending_graph_ = nullptr;
+    if (!(graph_on_ && epoch_graph(cur_))) epoch_steps(cur_);
     if (host_timing) { // host time to enqueue the epoch's inner steps vs the epoch on the device
       const auto th1 = std::chrono::steady_clock::now();
       LBF_HIP(hipStreamSynchronize(s));
       const auto th2 = std::chrono::steady_clock::now();
-      std::fprintf(stderr, "[lbf host] epoch %d: %d inner steps enqueued in %.3f ms, device done %.3f ms later\n",
+      std::fprintf(stderr, "[lbf host] epoch %d: %d inner steps enqueued in %.3f ms%s, device done %.3f ms later\n",
                    iters_, m_inner, std::chrono::duration<double, std::milli>(th1 - th0).count(),
-                   std::chrono::duration<double, std::milli>(th2 - th1).count());
+                   pending_graph_ ? " (graph)" : "", std::chrono::duration<double, std::milli>(th2 - th1).count());
     }
     // the next epoch's lists, drawn while the GPU runs this epoch's queued steps
-    if (iters_ + 1 < prm_.max_epochs) {
-      draw_epoch(cur.u_seen, next);
-      next_ready = true;
+    if (iters_ + 1 < target || iters_ + 1 < prm_.max_epochs) {
+      draw_epoch(cur_.u_seen, next_);
+      next_ready_ = true;
     }
     // anchor reset (s_lbfgs.hpp:265-270)
     const float *anchor = pick >= 0 ? wh_.get() + wh_slot(pick) * ld : wt_.get();
@@ -914,18 +1063,23 @@ int SlbfgsSolver::run(lbf_record *rec) {
     // recorder (s_lbfgs.hpp:274-284): full loss and gradient at the new anchor == next epoch's mu
     eval_full(w_.get(), mu_.get());
     read();
-    mu_valid = true;
+    if (pending_graph_) {
+      ctx_->prof.add_graph(pending_graph_->prof);
+      if (tctx_) tctx_->prof.add_graph(pending_graph_->tprof);
+      pending_graph_ = nullptr;
+    }
+    mu_valid_ = true;
     last_loss_ = hs_[SC_LOSS];
     last_gnorm_ = std::sqrt(hs_[SC_TGG]);
-    if (rec && rec_i < rec->cap) {
-      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-      if (rec->loss) rec->loss[rec_i] = last_loss_;
-      if (rec->grad_norm) rec->grad_norm[rec_i] = last_gnorm_;
-      if (rec->time_ms) rec->time_ms[rec_i] = ms;
-      if (rec->alpha) rec->alpha[rec_i] = prm_.step;
-      if (rec->ls_trials) rec->ls_trials[rec_i] = 0;
-      if (rec->accepted) rec->accepted[rec_i] = int(hs_[SC_COUNT]);
-      rec->size = std::max(rec->size, ++rec_i);
+    if (rec && rec_i_ < rec->cap) {
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0_).count();
+      if (rec->loss) rec->loss[rec_i_] = last_loss_;
+      if (rec->grad_norm) rec->grad_norm[rec_i_] = last_gnorm_;
+      if (rec->time_ms) rec->time_ms[rec_i_] = ms;
+      if (rec->alpha) rec->alpha[rec_i_] = prm_.step;
+      if (rec->ls_trials) rec->ls_trials[rec_i_] = 0;
+      if (rec->accepted) rec->accepted[rec_i_] = int(hs_[SC_COUNT]);
+      rec->size = std::max(rec->size, ++rec_i_);
     }
     ++iters_;
   }
@@ -935,7 +1089,7 @@ int SlbfgsSolver::run(lbf_record *rec) {
     LBF_HIP(hipStreamSynchronize(tctx_->stream));
     tctx_->prof.merge_into(ctx_->prof);
   }
-  return iters_;
+  return iters_ - done0;
 }
 
 // Diagnostics row of the pair just offered to the ring (lbf_slbfgs_params.pair_trace): synchronous.

@@ -10,6 +10,8 @@
 
 namespace lbf {
 
+class MinibatchSampler;
+
 // What the minimizer evaluates: the reference's LossGradFun (src/cuda/minimizer_base.cuh:15-16) plus the
 // dots the line search needs. eval() writes the gradient into g (n+2 floats) and SC_LOSS / SC_TGG /
 // SC_TGP (g.pdir) into the device status block scal, all on ctx()->stream.
@@ -166,10 +168,56 @@ public:
   SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_params, const float *X, const float *Y,
                long long N);
   ~SlbfgsSolver();
-  int run(lbf_record *rec);
+  int run(lbf_record *rec);                 // prm.max_epochs epochs (lbf_slbfgs_solve)
+  int iterate(int epochs, lbf_record *rec); // up to `epochs` more (lbf_slbfgs_begin / iterate / end)
   void info(lbf_solve_info *out) const;
 
 private:
+  struct Slice {
+    long long off = 0, cnt = 0, total = 0; // offset / count in this rank's flat list, whole batch size
+  };
+  // An epoch's index lists: every minibatch, the Hessian batches (only once a u exists), then the anchor
+  // pick, in the reference's RNG order (s_lbfgs.hpp:212-266); `flat` holds this rank's slices.
+  struct EpochDraw {
+    std::vector<int> flat, hflat, batch;
+    std::vector<Slice> mb, hb;
+    int pick = -1;
+    bool u_seen = false; // have_u after the epoch
+  };
+  void draw_epoch(bool u_seen, EpochDraw &d);
+  // The epoch's inner steps (s_lbfgs.hpp:218-262) enqueued on the streams: eagerly, or (epoch_graph)
+  // captured once per distinct launch sequence into a hipGraph and replayed.
+  void epoch_steps(const EpochDraw &d);
+  bool epoch_graph(const EpochDraw &d);
+  int wh_slot(int logical) const { return (wh_head_ + logical) % (prm_.L + 1); }
+  int wh_push_slot();
+  // Epoch graphs: the host enqueue of an epoch's ~5000 launches and event operations (≈ 31 ms at cfg 4)
+  // exceeds its device time, so an epoch whose launch sequence was seen once is captured (stream capture
+  // of both streams, fork / join by the same events) and then replayed with one hipGraphLaunch. Key: every
+  // input of the sequence (batch slices, buffer addresses, the profiler's configuration, have_u on entry).
+  struct EpochGraph {
+    std::vector<long long> key;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    GraphProf prof, tprof;             // the profiler's event-record nodes (bench timing)
+    long long evals = 0, rows = 0, tevals = 0, trows = 0;
+    int wh_head = 0, wh_count = 0;     // host state the epoch leaves behind
+    bool have_u = false;
+    ~EpochGraph();
+  };
+  std::vector<long long> graph_key(const EpochDraw &d) const;
+  std::vector<std::unique_ptr<EpochGraph>> graphs_;
+  std::vector<std::pair<std::vector<long long>, long long>> seen_keys_; // eager once first (allocations), marks
+  EpochGraph *pending_graph_ = nullptr; // launched this epoch: its profiler events are read after the sync
+  bool graph_on_ = false;
+  std::mt19937 rng_;
+  std::unique_ptr<MinibatchSampler> sampler_;
+  bool started_ = false, have_u_ = false, mu_valid_ = false, next_ready_ = false, converged_ = false;
+  EpochDraw cur_, next_;
+  int wh_head_ = 0, wh_count_ = 0; // ring of L+1 iterates (w_history)
+  bool pre_ = false;               // this epoch's anchor gradients precomputed (anchor_pre_)
+  int rec_i_ = 0;
+  std::chrono::steady_clock::time_point t0_;
   // Two independent batch gradients of one step (the FD pair at u +- eps s) into one [ga | gb] block
   // (gb = gab + ng_): the second on the twin's stream when there is one, joined before the next launch.
   // Data parallel: both evaluations stop before the all-reduce and ONE collective sums the block.

@@ -365,6 +365,39 @@ def slbfgs_solve(net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tenso
     return out, info
 
 
+class SlbfgsRun:
+    """Stateful S-LBFGS (begin / iterate / end) used by the benchmark: epochs of one solve across several
+    iterate() calls, so that epochs with a repeated launch sequence replay their captured hipGraph."""
+
+    def __init__(self, net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, record_cap: int = 100000,
+                 **kw):
+        self.p = slbfgs_params(**kw)
+        self.p.max_epochs = max(int(self.p.max_epochs), 1 << 30)
+        self.hist = History(record_cap)
+        self.info = SolveInfo()
+        self._keep = (net, params, X, Y)
+        h = C.c_void_p()
+        check(lib().lbf_slbfgs_begin(net.h, C.byref(self.p), ptr(params), ptr(X), ptr(Y), int(X.shape[0]),
+                                     C.byref(h)), "lbf_slbfgs_begin")
+        self.h = h
+
+    def iterate(self, epochs: int):
+        check(lib().lbf_slbfgs_iterate(self.h, epochs, C.byref(self.hist.rec), C.byref(self.info)),
+              "lbf_slbfgs_iterate")
+        return self.info
+
+    def close(self):
+        if self.h:
+            lib().lbf_slbfgs_end(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def gd_solve(net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, n_global: Optional[int] = None,
              **kw):
     """CudaGD::solve (src/cuda/gd.cuh:38-106); params updated in place. kw: lr, momentum, max_iters, tol."""
