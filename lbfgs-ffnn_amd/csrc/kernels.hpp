@@ -367,6 +367,15 @@ int tail_vpw(int m);                                // vectors per wave of the G
 // block per Gram column whose last arrival runs the history step (hist_core.hpp) from the column sums.
 constexpr int DIR_MAXM = 16;
 constexpr long long DIR_MAXN = 1LL << 22;
+struct CombineArgs {
+  HistView h;
+  const float *g = nullptr; // the vector the direction was built for
+  float *dir = nullptr;     // nullable
+  const float *x_in = nullptr;
+  float *x_out = nullptr, *x_out2 = nullptr; // x_out = x_in + alpha*dir ; x_out2 = copy of x_out
+  int alpha_from_state = 1;                  // alpha = scal[SC_ALPHA0]
+  double alpha = 1.0;
+};
 struct DirArgs {
   GramArgs g;               // operands, policy, has_pair / has_g, reset; g.h carries the abort flag
   int want_dir = 1;         // 0 (pair only) or 1
@@ -376,6 +385,16 @@ struct DirArgs {
   double *dots = nullptr;   // [dir_ncols(m)]
   int nb = 0;               // cdiv(n, dir_cols_per_block(m, n))
   unsigned *cols_done = nullptr; // arrival counter, zero between launches
+  // The direction's linear-combination sweep in the same launch (dir_fin, want_dir == 1): ncb blocks after
+  // the column blocks load their elements of g, x_in and every ring slot up front, wait for the last
+  // column block to publish the step's order and coefficients (cmb_desc, then cmb_flag = 1), and
+  // combine (combine_small's arithmetic); the last worker to have read the descriptor re-zeroes the flag
+  // and cmb_done for the next launch (so a replayed graph needs no fresh arguments). ncb = 0: no combine
+  // (a separate hist_combine follows).
+  CombineArgs cmb;
+  int ncb = 0;
+  unsigned *cmb_flag = nullptr; // [2]: the publish flag, the workers' arrival count; zero between launches
+  double *cmb_desc = nullptr;   // [2 + 3 slots]: k, slot of logical i, cs_i, cy_i, cg
 };
 bool dir_supported(int m, long long n);
 int dir_cols_per_block(int m, long long n);
@@ -389,15 +408,6 @@ constexpr int GRAM_FIN_MAXM = 52;
 bool gram_fin_supported(int m);
 void gram_fin(hipStream_t s, const DirArgs &a);
 
-struct CombineArgs {
-  HistView h;
-  const float *g = nullptr; // the vector the direction was built for
-  float *dir = nullptr;     // nullable
-  const float *x_in = nullptr;
-  float *x_out = nullptr, *x_out2 = nullptr; // x_out = x_in + alpha*dir ; x_out2 = copy of x_out
-  int alpha_from_state = 1;                  // alpha = scal[SC_ALPHA0]
-  double alpha = 1.0;
-};
 void hist_combine(hipStream_t s, const CombineArgs &a);
 void hist_reset(hipStream_t s, const HistView &h);
 

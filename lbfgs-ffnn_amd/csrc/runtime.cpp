@@ -1076,6 +1076,12 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
     ddots_.resize(size_t(dir_ncols(m)));
     dcount_.resize(1);
     LBF_HIP(hipMemsetAsync(dcount_.get(), 0, sizeof(unsigned), ctx_->stream));
+    // opt-in: measured slower (profiles/r03b/README.md: the merged launch ran 70 us per step against
+    // 16 + 12 us for the two it replaces; the 2094 waiting blocks slow the column sums and the step)
+    dir_combine_ = env_int("LBF_DIR_COMBINE", 0) != 0;
+    cflag_.resize(2);
+    cdesc_.resize(size_t(2 + 3 * slots));
+    LBF_HIP(hipMemsetAsync(cflag_.get(), 0, 2 * sizeof(unsigned), ctx_->stream));
   }
   gfin_on_ = gram_fin_supported(m) && env_int("LBF_GRAM_FIN", 1) != 0;
   if (gfin_on_) {
@@ -1161,6 +1167,52 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
   c.dsign = dsign;
   ProfScope ps(ctx_, PK_COEF);
   hist_coef(s, c);
+}
+
+void History::update_combine(const GramArgs &g0, int iter, double dsign, const float *x_in, float *x_out,
+                             float *x_out2, double alpha) {
+  GramArgs g = g0;
+  g.h = v_;
+  g.h.abort = ctx_->abort;
+  auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+  const bool aligned = al16(g.sa) && al16(g.sb) && al16(g.ya) && al16(g.yb) && al16(g.ga) && al16(g.gb) &&
+                       al16(g.gc) && al16(g.g_out);
+  const long long nb_c = cdiv(v_.n, 256);
+  if (!(dir_on_ && dir_combine_ && aligned && g.policy == POL_SLBFGS && g.has_g && g.g_out && !g.reset &&
+        v_.m <= DIR_MAXM && nb_c <= (1LL << 20))) {
+    update(g0, 1, iter, dsign);
+    combine(g0.g_out, nullptr, x_in, x_out, x_out2, false, alpha);
+    return;
+  }
+  hipStream_t s = ctx_->stream;
+  DirArgs d;
+  d.g = g;
+  d.want_dir = 1;
+  d.iter = iter;
+  d.dsign = dsign;
+  d.rows = drows_.get();
+  d.dots = ddots_.get();
+  d.nb = int(cdiv(v_.n, dir_cols_per_block(v_.m, v_.n)));
+  d.cols_done = dcount_.get();
+  CombineArgs &c = d.cmb;
+  c.h = v_;
+  c.h.abort = ctx_->abort;
+  c.g = g0.g_out;
+  c.dir = nullptr;
+  c.x_in = x_in;
+  c.x_out = x_out;
+  c.x_out2 = x_out2;
+  c.alpha_from_state = 0;
+  c.alpha = alpha;
+  d.ncb = int(nb_c);
+  d.cmb_flag = cflag_.get();
+  d.cmb_desc = cdesc_.get();
+  {
+    ProfScope ps(ctx_, PK_GRAM);
+    dir_sweep(s, d);
+  }
+  ProfScope ps(ctx_, PK_COEF);
+  dir_fin(s, d);
 }
 
 void History::combine(const float *g, float *dir, const float *x_in, float *x_out, float *x_out2,

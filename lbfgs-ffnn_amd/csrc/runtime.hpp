@@ -230,6 +230,11 @@ public:
   void update(const GramArgs &g, int want_dir, int iter, double dsign);
   void combine(const float *g, float *dir, const float *x_in, float *x_out, float *x_out2, bool alpha_from_state,
                double alpha);
+  // update(g, 1, iter, dsign) then combine(g.g_out, nullptr, x_in, x_out, x_out2, false, alpha); with
+  // LBF_DIR_COMBINE=1 on the fused S-LBFGS route the combine runs inside the column-sum launch (dir.hip;
+  // measured slower, off by default)
+  void update_combine(const GramArgs &g, int iter, double dsign, const float *x_in, float *x_out, float *x_out2,
+                      double alpha);
   double *scal() const { return v_.scal; }
   int m() const { return v_.m; }
 
@@ -243,6 +248,10 @@ private:
   DevBuf<double> drows_, ddots_;
   DevBuf<unsigned> dcount_;
   bool dir_on_ = false;
+  // in-launch combine: publish flag + worker arrival count (zero between launches), order / coefficients
+  DevBuf<unsigned> cflag_;
+  DevBuf<double> cdesc_;
+  bool dir_combine_ = false;
   // unfused path: Gram sweep (transposed partials in part_) + column sums whose last block runs the step
   DevBuf<double> gdots_;
   DevBuf<unsigned> gcount_;

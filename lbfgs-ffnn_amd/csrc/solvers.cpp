@@ -619,10 +619,77 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
       LBF_HIP(hipEventCreateWithFlags(&ev_g2_[i], hipEventDisableTiming));
       LBF_HIP(hipEventCreateWithFlags(&ev_free_[i], hipEventDisableTiming));
     }
+    if (env_int("LBF_SLBFGS_TWIN_THREAD", 1)) {
+      tw_.reset(new TwinWorker());
+      TwinWorker *w = tw_.get();
+      const int dev = ctx_->device;
+      w->th = std::thread([w, dev]() {
+        const bool dev_ok = hipSetDevice(dev) == hipSuccess;
+        for (;;) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> lk(w->mu);
+            w->cv.wait(lk, [w] { return w->stop || !w->q.empty(); });
+            if (w->q.empty()) return; // stop requested and nothing left
+            f = std::move(w->q.front());
+            w->q.pop_front();
+          }
+          try {
+            if (!dev_ok) throw Error(2, "twin thread: hipSetDevice failed");
+            bool failed;
+            {
+              std::lock_guard<std::mutex> lk(w->mu);
+              failed = w->err != nullptr;
+            }
+            if (!failed) f(); // after an error the rest is skipped (tickets still complete)
+          } catch (...) {
+            std::lock_guard<std::mutex> lk(w->mu);
+            if (!w->err) w->err = std::current_exception();
+          }
+          w->done.fetch_add(1, std::memory_order_release);
+        }
+      });
+    }
   }
 }
 
+long long SlbfgsSolver::twin_post(std::function<void()> f) {
+  if (!tw_ || tw_inline_) {
+    f();
+    return 0;
+  }
+  long long ticket;
+  {
+    std::lock_guard<std::mutex> lk(tw_->mu);
+    tw_->q.push_back(std::move(f));
+    ticket = ++tw_->posted;
+  }
+  tw_->cv.notify_one();
+  return ticket;
+}
+
+void SlbfgsSolver::twin_wait(long long ticket) {
+  if (!tw_ || ticket <= 0) return;
+  for (int spin = 0; tw_->done.load(std::memory_order_acquire) < ticket; ++spin)
+    if (spin > 64) std::this_thread::yield();
+  std::exception_ptr e;
+  {
+    std::lock_guard<std::mutex> lk(tw_->mu);
+    e = tw_->err;
+    tw_->err = nullptr;
+  }
+  if (e) std::rethrow_exception(e);
+}
+
 SlbfgsSolver::~SlbfgsSolver() {
+  if (tw_) {
+    {
+      std::lock_guard<std::mutex> lk(tw_->mu);
+      tw_->stop = true;
+    }
+    tw_->cv.notify_one();
+    if (tw_->th.joinable()) tw_->th.join();
+  }
   if (ev_fork_) (void)hipEventDestroy(ev_fork_);
   if (ev_join_) (void)hipEventDestroy(ev_join_);
   for (int i = 0; i < 2; ++i) {
@@ -658,10 +725,21 @@ void SlbfgsSolver::eval_pair(const float *wa, const float *wb, float *gab, long 
     one(net_, wb, gb);
   } else {
     LBF_HIP(hipEventRecord(ev_fork_, ctx_->stream)); // wa, wb, the gathered rows and gb's last reader are done
-    LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
-    one(tnet_.get(), wb, gb);
-    one(net_, wa, ga);
-    LBF_HIP(hipEventRecord(ev_join_, tctx_->stream));
+    const long long tk = twin_post([=]() {
+      LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
+      one(tnet_.get(), wb, gb);
+      LBF_HIP(hipEventRecord(ev_join_, tctx_->stream));
+    });
+    try {
+      one(net_, wa, ga);
+    } catch (...) { // the task refers to this frame: let it finish first
+      try {
+        twin_wait(tk);
+      } catch (...) {
+      }
+      throw;
+    }
+    twin_wait(tk); // ev_join_ recorded (and ev_fork_ waited for: it may be re-recorded after this)
     LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_join_, 0));
   }
   if (dp) reduce_pair(wa, wb, gab, inv_scale);
@@ -765,15 +843,26 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
                       gmb_.get(), ng_, dp);
   }
   auto gpre = [&](int t) { return gmb_.get() + (long long)t * ng_; };
+  // Tickets of the twin tasks (0: ran inline). Event order across the two host threads: task t + 2 (which
+  // waits on ev_free_[t & 1]) is posted at step t + 1, after step t recorded that event; step t + 2
+  // re-records it only after twin_wait(task t + 2), i.e. after that wait was enqueued. Task t records
+  // ev_g2_[t & 1] and the context thread waits on it after twin_wait(task t); task t + 2 re-records it
+  // only after being posted at step t + 1, after that wait.
+  std::vector<long long> tk(size_t(std::max(m_inner, 1)), 0);
   auto anchor_ahead = [&](int t) { // twin stream: the anchor half of step t's block
-    const Slice &sl = mb[t];
-    LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_free_[t & 1], 0)); // step t - 2's direction read it
-    if (dp)
-      tnet_->loss_grad_local(w_.get(), g2(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, 1.0 / double(sl.total));
-    else
-      tnet_->loss_grad(w_.get(), g2(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, 1.0 / double(sl.total),
-                       prm_.lambda, nullptr, nullptr);
-    LBF_HIP(hipEventRecord(ev_g2_[t & 1], tctx_->stream));
+    const Slice sl = mb[t];
+    float *gdst = g2(t);
+    const float *xr = rows_x(sl), *yr = rows_y(sl);
+    hipEvent_t efree = ev_free_[t & 1], eg2 = ev_g2_[t & 1];
+    tk[size_t(t)] = twin_post([=]() {
+      LBF_HIP(hipStreamWaitEvent(tctx_->stream, efree, 0)); // step t - 2's direction read it
+      if (dp)
+        tnet_->loss_grad_local(w_.get(), gdst, xr, yr, nullptr, sl.cnt, 1.0 / double(sl.total));
+      else
+        tnet_->loss_grad(w_.get(), gdst, xr, yr, nullptr, sl.cnt, 1.0 / double(sl.total), prm_.lambda, nullptr,
+                         nullptr);
+      LBF_HIP(hipEventRecord(eg2, tctx_->stream));
+    });
   };
   // LBF_HOST_TIMING=2: host time of each part of the inner step's enqueue (where the epoch's host-bound
   // ~130 us per step go)
@@ -817,6 +906,7 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
                         nullptr);
       tock(1, h0);
       h0 = tick();
+      twin_wait(tk[size_t(t)]); // task t recorded ev_g2_[t & 1]
       LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_g2_[t & 1], 0));
       tock(2, h0);
       if (dp) reduce_pair(wt_.get(), w_.get(), g1(t), inv_b);
@@ -831,16 +921,13 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     ga.gc = mu_.get();
     ga.g_out = v_.get();
     auto h0 = tick();
-    hist_.update(ga, 1, 1, +1.0);
+    const int slot = wh_push_slot();
+    // r = H v (two-loop), then wt = wt - step * r ; w_history.push_back(wt)
+    hist_.update_combine(ga, 1, +1.0, wt_.get(), wt_.get(), wh_.get() + slot * ld, -prm_.step);
     tock(3, h0);
     h0 = tick();
     if (tnet_ && !pre) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
     tock(2, h0);
-    h0 = tick();
-    const int slot = wh_push_slot();
-    // wt = wt - step * r ; w_history.push_back(wt)
-    hist_.combine(v_.get(), nullptr, wt_.get(), wt_.get(), wh_.get() + slot * ld, false, -prm_.step);
-    tock(4, h0);
     h0 = tick();
     if (t > 0 && t % L == 0) {
       int slots[64];
@@ -877,6 +964,7 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     }
     tock(5, h0);
   }
+  if (tw_) twin_wait(tw_->posted); // every twin task of the epoch enqueued
   if (host_timing >= 2)
     std::fprintf(stderr, "[lbf host] per inner step (us): twin %.1f, main eval %.1f, events %.1f, direction %.1f, "
                  "combine %.1f, Hessian step %.1f\n", ht[0] / m_inner, ht[1] / m_inner, ht[2] / m_inner,
@@ -932,9 +1020,12 @@ bool SlbfgsSolver::epoch_graph(const EpochDraw &d) {
     ctx_->prof.capture_begin((long long)ctx_->prof.pool.size() + marks + 64);
     if (tctx_) tctx_->prof.capture_begin((long long)tctx_->prof.pool.size() + marks + 64);
     LBF_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+    tw_inline_ = true; // the capture sees the twin's launches from this thread
     try {
       epoch_steps(d);
+      tw_inline_ = false;
     } catch (...) {
+      tw_inline_ = false;
       hipGraph_t tmp = nullptr;
       (void)hipStreamEndCapture(s, &tmp);
       if (tmp) (void)hipGraphDestroy(tmp);

@@ -4,9 +4,15 @@
 #include "../../include/lbfgs_amd.h"
 #include "runtime.hpp"
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <deque>
+#include <exception>
+#include <functional>
+#include <mutex>
 #include <random>
+#include <thread>
 
 namespace lbf {
 
@@ -256,6 +262,25 @@ private:
   // (it has no communicator) and the context stream's one collective per block sums both.
   std::unique_ptr<Ctx> tctx_;
   std::unique_ptr<Mlp> tnet_;
+  // The twin stream's launches enqueued by a helper host thread (LBF_SLBFGS_TWIN_THREAD=0: inline): the
+  // inner step's host enqueue (≈ 100-130 µs, ~40 % of it the twin's evaluation) bounds the epoch on slower
+  // hosts. Tasks run in posting order (one FIFO, so the twin stream sees the single-thread launch order);
+  // the context thread waits for a task's ticket before it waits on an event that task records, and records
+  // an event the twin waits on only after the waiting task has been enqueued (see epoch_steps).
+  struct TwinWorker {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    std::atomic<long long> done{0};
+    long long posted = 0;
+    std::exception_ptr err;
+    bool stop = false;
+  };
+  std::unique_ptr<TwinWorker> tw_;
+  bool tw_inline_ = false; // while capturing a graph: twin work on the calling thread
+  long long twin_post(std::function<void()> f);
+  void twin_wait(long long ticket); // returns once task `ticket` (1-based) has run; rethrows its error
   // this rank's slices of the epoch's sampled rows, gathered once (all minibatches and Hessian batches)
   DevBuf<float> xg_, yg_;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;

@@ -116,3 +116,30 @@ def test_graph_profiler_times_replayed_launches(ctx, pkg, monkeypatch):
         counts[graph] = n
     # the sampling phase is frozen in the graph (the capture epoch's), so the counts agree to a few launches
     assert abs(counts[True] - counts[False]) <= 3, counts
+
+
+def test_in_launch_combine_matches_separate_launch(ctx, pkg, O, monkeypatch):
+    """The S-LBFGS direction's linear combination inside the column-sum launch (dir.hip combine workers,
+    s_lbfgs.hpp:218-262: r = H v, w_t -= step r; opt-in LBF_DIR_COMBINE=1) against the separate
+    combine_small launch (the default): the same coefficients summed slot by slot instead of in logical order, so the
+    iterates agree to fp64-summation rounding; also against the fp64 oracle."""
+    dims, acts = [784, 16, 10], ["relu", "linear"]
+    N = 512
+    Xh, Yh = pkg.synth_mnist(N)
+    kw = dict(M=5, L=4, b=32, b_H=16, step=0.02)
+    out = {}
+    for comb in ("1", "0"):
+        monkeypatch.setenv("LBF_DIR_COMBINE", comb)
+        net = pkg.Mlp(ctx, dims, acts)
+        P = net.init_params(123, "cpu")
+        P0 = host(P)
+        hist, _ = pkg.slbfgs_solve(net, P, dev(Xh), dev(Yh), max_epochs=4, tol=0.0, lam=1e-4, **kw)
+        out[comb] = (hist, host(P))
+    (h1, P1), (h0, P0b) = out["1"], out["0"]
+    assert np.array_equal(h1["accepted"], h0["accepted"])
+    assert np.abs(h1["loss"] - h0["loss"]).max() <= 1e-6 * np.abs(h0["loss"]).max()
+    assert np.abs(P1 - P0b).max() <= 1e-5 * np.abs(P0b).max()
+    _, rec, _ = O.Net(dims, acts).slbfgs(P0, Xh.astype(np.float64), Yh.astype(np.float64), epochs=4, tol=0.0,
+                                         M=5, L=4, b=32, bH=16, step=0.02, lam=1e-4)
+    r = np.abs(h1["loss"] - rec[:, 0]) / np.abs(rec[:, 0])
+    assert r.max() <= 1e-3, r
