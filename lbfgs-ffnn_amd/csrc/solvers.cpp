@@ -589,6 +589,7 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
   evals0_ = net->evals();
   rows0_ = net->rows();
   anchor_pre_ = env_int("LBF_SLBFGS_ANCHOR", 0) != 0; // the twin measured ~2-3 % faster (profiles/r03)
+  free_twin_ = env_int("LBF_SLBFGS_TWIN_FREE", 1) != 0;
   rng_.seed(prm.seed);
   sampler_.reset(new MinibatchSampler(size_t(N)));
   // epoch graphs (LBF_SLBFGS_GRAPH=1; off by default): not with a communicator (the collectives stay eager)
@@ -690,6 +691,7 @@ SlbfgsSolver::~SlbfgsSolver() {
     tw_->cv.notify_one();
     if (tw_->th.joinable()) tw_->th.join();
   }
+  for (auto e : ev_anc_) (void)hipEventDestroy(e);
   if (ev_fork_) (void)hipEventDestroy(ev_fork_);
   if (ev_join_) (void)hipEventDestroy(ev_join_);
   for (int i = 0; i < 2; ++i) {
@@ -832,8 +834,23 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
   // minibatch t + 1 at w, instead of joining the two evaluations of each step. Same evaluations on the
   // same inputs: bitwise the same. Data parallel: both halves are this rank's partial sums until the
   // step's one all-reduce of the whole block.
+  // Single rank (LBF_SLBFGS_TWIN_FREE, on by default): the anchor half of step t goes to its own buffer
+  // ganc_ + t ng_ (the epoch's 234 anchor gradients, 501 MB at cfg 4), so the twin never waits for the
+  // context stream to release a block: no ev_free_ record on the context stream (≈ 5 µs of its time per
+  // step, profiles/r03/launch_floor.txt) and no wait on the twin. Data parallel keeps the packed
+  // [g(w_t) | g(w)] block of one all-reduce.
+  const bool twin_free = tnet_ && !pre_ && !dp && free_twin_;
+  if (twin_free) {
+    const size_t need = size_t(m_inner) * size_t(ng_);
+    if (ganc_.size() < need) ganc_.resize(need);
+    while (ev_anc_.size() < size_t(m_inner)) {
+      hipEvent_t e;
+      LBF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ev_anc_.push_back(e);
+    }
+  }
   auto g1 = [&](int t) { return gpair_[t & 1].get(); };
-  auto g2 = [&](int t) { return gpair_[t & 1].get() + ng_; };
+  auto g2 = [&](int t) { return twin_free ? ganc_.get() + (long long)t * ng_ : gpair_[t & 1].get() + ng_; };
   auto rows_x = [&](const Slice &sl) { return xg_.get() + sl.off * In; };
   auto rows_y = [&](const Slice &sl) { return yg_.get() + sl.off * Out; };
   const bool pre = pre_;
@@ -853,9 +870,9 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     const Slice sl = mb[t];
     float *gdst = g2(t);
     const float *xr = rows_x(sl), *yr = rows_y(sl);
-    hipEvent_t efree = ev_free_[t & 1], eg2 = ev_g2_[t & 1];
+    hipEvent_t efree = twin_free ? nullptr : ev_free_[t & 1], eg2 = twin_free ? ev_anc_[size_t(t)] : ev_g2_[t & 1];
     tk[size_t(t)] = twin_post([=]() {
-      LBF_HIP(hipStreamWaitEvent(tctx_->stream, efree, 0)); // step t - 2's direction read it
+      if (efree) LBF_HIP(hipStreamWaitEvent(tctx_->stream, efree, 0)); // step t - 2's direction read it
       if (dp)
         tnet_->loss_grad_local(w_.get(), gdst, xr, yr, nullptr, sl.cnt, 1.0 / double(sl.total));
       else
@@ -876,8 +893,14 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
   if (tnet_ && !pre) {
     // the twin may reuse block t & 1 once the direction of step t - 2 has read it: nothing of this epoch
     // has yet (recorded here so that a captured epoch's first waits are on events of the capture)
-    LBF_HIP(hipEventRecord(ev_free_[0], s));
-    LBF_HIP(hipEventRecord(ev_free_[1], s));
+    if (!twin_free) {
+      LBF_HIP(hipEventRecord(ev_free_[0], s));
+      LBF_HIP(hipEventRecord(ev_free_[1], s));
+    } else {
+      // the twin's first launch must follow this epoch's gather and w (same role as ev_free_ above)
+      LBF_HIP(hipEventRecord(ev_fork_, s));
+      LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
+    }
     anchor_ahead(0);
   }
   for (int t = 0; t < m_inner; ++t) {
@@ -906,8 +929,8 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
                         nullptr);
       tock(1, h0);
       h0 = tick();
-      twin_wait(tk[size_t(t)]); // task t recorded ev_g2_[t & 1]
-      LBF_HIP(hipStreamWaitEvent(ctx_->stream, ev_g2_[t & 1], 0));
+      twin_wait(tk[size_t(t)]); // task t recorded ev_g2_[t & 1] / ev_anc_[t]
+      LBF_HIP(hipStreamWaitEvent(ctx_->stream, twin_free ? ev_anc_[size_t(t)] : ev_g2_[t & 1], 0));
       tock(2, h0);
       if (dp) reduce_pair(wt_.get(), w_.get(), g1(t), inv_b);
     } else {
@@ -926,7 +949,8 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     hist_.update_combine(ga, 1, +1.0, wt_.get(), wt_.get(), wh_.get() + slot * ld, -prm_.step);
     tock(3, h0);
     h0 = tick();
-    if (tnet_ && !pre) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
+    if (tnet_ && !pre && !twin_free)
+      LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
     tock(2, h0);
     h0 = tick();
     if (t > 0 && t % L == 0) {

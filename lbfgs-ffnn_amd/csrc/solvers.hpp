@@ -284,6 +284,10 @@ private:
   // this rank's slices of the epoch's sampled rows, gathered once (all minibatches and Hessian batches)
   DevBuf<float> xg_, yg_;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+  // free-running twin (single rank): anchor gradient of step t in ganc_ + t ng_, its event ev_anc_[t]
+  bool free_twin_ = true;
+  DevBuf<float> ganc_;
+  std::vector<hipEvent_t> ev_anc_;
   hipEvent_t ev_g2_[2] = {nullptr, nullptr}, ev_free_[2] = {nullptr, nullptr}; // anchor gradients ahead (twin)
 };
 
