@@ -589,7 +589,7 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
   evals0_ = net->evals();
   rows0_ = net->rows();
   anchor_pre_ = env_int("LBF_SLBFGS_ANCHOR", 0) != 0; // the twin measured ~2-3 % faster (profiles/r03)
-  free_twin_ = env_int("LBF_SLBFGS_TWIN_FREE", 0) != 0;
+  free_twin_ = env_int("LBF_SLBFGS_TWIN_FREE", 1) != 0;
   rng_.seed(prm.seed);
   sampler_.reset(new MinibatchSampler(size_t(N)));
   // epoch graphs (LBF_SLBFGS_GRAPH=1; off by default): not with a communicator (the collectives stay eager)
