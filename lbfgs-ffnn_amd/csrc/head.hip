@@ -96,6 +96,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
                                                    double inv_scale, float *delta, float *slab, double *sse_part,
                                                    const int *abort) {
   if (abort && *abort) return;
+  KT(30);
   extern __shared__ __attribute__((aligned(16))) float sh[];
   const Smem sm = carve(sh, H);
   const int t = threadIdx.x, LDA = sm.LDA, Hp = sm.Hp;
@@ -114,17 +115,21 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
   }
   TileRegs tr;
   long long tl = int(blockIdx.x) / hsplit;
-  if (vec && tl < ntiles) tr.load(A, H, Hp, tl * TB, int(min((long long)TB, B - tl * TB)));
   if (vec) {
-    WRegs wr; // in flight with the first tile; stage_w's zero fill meanwhile
+    // W first, then the first tile (64 KB per workgroup), both in flight during stage_w's zero fill; the
+    // barrier orders LDS only, so staging W waits for W's loads alone (vmcnt counts in issue order), not
+    // for the tile's (phase stamps, profiles/r03b/head/head_phases_*.txt: W staged 4.8 us after entry)
+    WRegs wr;
     wr.load(P, H, Out);
+    if (tl < ntiles) tr.load(A, H, Hp, tl * TB, int(min((long long)TB, B - tl * TB)));
     for (int e = t; e < 16 * LDA; e += 256) sm.Wt[e] = 0.0f;
     for (int e = t; e < Hp * 16; e += 256) sm.Wr[e] = 0.0f;
-    __syncthreads();
+    lds_barrier();
     wr.store(sm, Out);
   } else {
     stage_w(sm, P, Out);
   }
+  KT(31);
   f32x4 cw[QM];
 #pragma unroll
   for (int q = 0; q < QM; ++q) cw[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -158,11 +163,15 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
         sm.As[r * LDA + c] = (r < rows && c < H) ? A[(b0 + r) * H + c] : 0.0f;
       }
     }
-    __syncthreads();
+    // LDS only: the next tile's prefetch (vector path) stays in flight through this tile's products
+    if (vec) lds_barrier();
+    else __syncthreads();
+    KT(32);
     tile<false, QM, false>(sm, ta, b0, rows, cw, sse, fa, hr);
   }
   if (hs != 0) sse = 0.0; // every split computed the same loss; the first one reports it
   write_partials(sm, Out, cw, sse, slab + (long long)blockIdx.x * (H + 1) * Out, sse_part + blockIdx.x, hr);
+  KT(33);
 }
 
 } // namespace
@@ -214,3 +223,9 @@ void head_fused(hipStream_t s, const float *A, int H, const float *P, int Out, c
 }
 
 } // namespace lbf
+
+#ifdef LBF_KTRACE
+extern "C" int lbf_dbg_ktrace_head(unsigned long long *host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(lbf::lbf_kt_buf), size_t(n) * 8) == hipSuccess ? 0 : 1;
+}
+#endif
