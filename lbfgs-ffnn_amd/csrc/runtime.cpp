@@ -24,7 +24,7 @@ size_t Profiler::mark(hipStream_t s) {
   if (used == pool.size()) {
     LBF_REQUIRE(!capture, "profiler: event pool exhausted inside a graph capture");
     hipEvent_t e;
-    LBF_HIP(hipEventCreate(&e));
+    LBF_HIP(hipEventCreateWithFlags(&e, hipEventDefault | event_release_flags()));
     pool.push_back(e);
   }
   if (capture) {
@@ -74,7 +74,7 @@ void Profiler::capture_begin(long long reserve) {
   resolve();
   while ((long long)pool.size() < reserve) {
     hipEvent_t e;
-    LBF_HIP(hipEventCreate(&e));
+    LBF_HIP(hipEventCreateWithFlags(&e, hipEventDefault | event_release_flags()));
     pool.push_back(e);
   }
   capture = true;

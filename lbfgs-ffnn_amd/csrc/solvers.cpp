@@ -614,11 +614,11 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
     }
     dims.push_back(net->layers().back().out);
     tnet_.reset(new Mlp(tctx_.get(), int(acts.size()), dims.data(), acts.data()));
-    LBF_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-    LBF_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    LBF_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming | event_release_flags()));
+    LBF_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming | event_release_flags()));
     for (int i = 0; i < 2; ++i) {
-      LBF_HIP(hipEventCreateWithFlags(&ev_g2_[i], hipEventDisableTiming));
-      LBF_HIP(hipEventCreateWithFlags(&ev_free_[i], hipEventDisableTiming));
+      LBF_HIP(hipEventCreateWithFlags(&ev_g2_[i], hipEventDisableTiming | event_release_flags()));
+      LBF_HIP(hipEventCreateWithFlags(&ev_free_[i], hipEventDisableTiming | event_release_flags()));
     }
     if (env_int("LBF_SLBFGS_TWIN_THREAD", 1)) {
       tw_.reset(new TwinWorker());
@@ -845,7 +845,7 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     if (ganc_.size() < need) ganc_.resize(need);
     while (ev_anc_.size() < size_t(m_inner)) {
       hipEvent_t e;
-      LBF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      LBF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | event_release_flags()));
       ev_anc_.push_back(e);
     }
   }
