@@ -1132,8 +1132,11 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
     const auto &mb = cur_.mb;
     const int pick = cur_.pick;
     idx_.ensure(std::max<size_t>(1, flat.size()));
-    if (!flat.empty())
-      LBF_HIP(hipMemcpyAsync(idx_.get(), flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    if (!flat.empty()) { // through pinned staging: an asynchronous copy (the stream was synchronised by read())
+      idx_host_.ensure(flat.size());
+      std::memcpy(idx_host_.get(), flat.data(), flat.size() * sizeof(int));
+      LBF_HIP(hipMemcpyAsync(idx_.get(), idx_host_.get(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    }
     // this rank's sampled rows of the epoch gathered once, in sampling order: step t's minibatch slice (and
     // its Hessian batch slice) is then contiguous (batch_g's column gather, unified_optimization.hpp:361-364)
     xg_.ensure(std::max<size_t>(1, flat.size()) * size_t(In));
@@ -1153,7 +1156,12 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
         LBF_HIP(hipMemsetAsync(gmb_.get(), 0, need * sizeof(float), s));
       }
     }
-    LBF_HIP(hipStreamSynchronize(s)); // flat is a pageable temporary
+    // No host synchronisation here: the upload reads pinned staging (rewritten only after the next read()),
+    // and every consumer of the gathered rows is ordered after the gathers (the context stream, and the
+    // twin through the event it waits on at the epoch's start), so the host enqueues the first inner step
+    // while the gathers run (LBF_SLBFGS_EPOCH_SYNC=1: the previous synchronisation).
+    static const int epoch_sync = env_int("LBF_SLBFGS_EPOCH_SYNC", 0);
+    if (epoch_sync) LBF_HIP(hipStreamSynchronize(s));
     // --- epoch -----------------------------------------------------------------------------------
     static const int host_timing = env_int("LBF_HOST_TIMING", 0);
     const auto th0 = std::chrono::steady_clock::now();

@@ -252,6 +252,7 @@ private:
   bool anchor_pre_ = false; // LBF_SLBFGS_ANCHOR=1
   long long ng_ = 0; // floats per gradient in a block (n + 2 loss words, rounded to 4)
   DevBuf<int> idx_;
+  PinnedBuf<int> idx_host_; // pinned staging of an epoch's index lists
   PinnedBuf<double> hs_;
   int iters_ = 0;
   double last_loss_ = 0, last_gnorm_ = 0;
