@@ -1,6 +1,6 @@
 # final tree (free-running twin on by default): full GPU suite, smoke, the default bench line, cfg 4
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r03fe
+O=$R/gpurun_out/r03ff
 mkdir -p $O
 cd $R
 timeout -k 10 400 python -u -m pytest tests/ -q -m gpu --timeout 120 --timeout-method thread > $O/final_gpu_tests.log 2>&1 || { echo "tests failed"; tail -20 $O/final_gpu_tests.log; exit 1; }
