@@ -839,7 +839,11 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
   // context stream to release a block: no ev_free_ record on the context stream (≈ 5 µs of its time per
   // step, profiles/r03/launch_floor.txt) and no wait on the twin. Data parallel keeps the packed
   // [g(w_t) | g(w)] block of one all-reduce.
-  const bool twin_free = tnet_ && !pre_ && !dp && free_twin_;
+  // (within a memory budget: m_inner gradients of n floats; LBF_SLBFGS_TWIN_FREE_MB, default 4096 MB; past it
+  // the double-buffered twin)
+  static const long long free_mb = env_int("LBF_SLBFGS_TWIN_FREE_MB", 4096);
+  const bool twin_free = tnet_ && !pre_ && !dp && free_twin_ &&
+                         double(m_inner) * double(ng_) * 4.0 <= double(free_mb) * 1024.0 * 1024.0;
   if (twin_free) {
     const size_t need = size_t(m_inner) * size_t(ng_);
     if (ganc_.size() < need) ganc_.resize(need);
