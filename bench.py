@@ -40,7 +40,7 @@ PROF_MIN_LAUNCHES = 10           # ... or more often, so that at least this many
                                  # pair costs ~10 us of GPU time: profiles/r03/launch_floor.txt)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # 400 iterations (~0.12 s at cfg 2): a few-ms host stall of the speculating thread (a shared box) is a
@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--slbfgs-step", type=float, default=0.005,
                     help="S-LBFGS step (config 4 names 0.02, which diverges to NaN on the synthetic data in the "
                          "fp64 oracle too; the work per epoch does not depend on it)")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     if a.solver == "slbfgs" and a.dims == "784,128,10":
         a.dims, a.acts = "784,512,256,10", "relu,relu,linear"
     return a
@@ -162,6 +162,16 @@ def route_graph():
     return os.environ.get("LBF_SLBFGS_GRAPH", "0") != "0" and int(os.environ.get("WORLD_SIZE", "1")) == 1
 
 
+class Device:
+    """The three torch.cuda calls the rank code makes. tests/test_bench_launch.py swaps in a host stub so
+    that the multi-rank control plane (unique-id broadcast, dominant-section broadcast, barriers, the MAX
+    of the ranks' clocks, rank-0 emission) runs on CPU under gloo."""
+    synchronize = staticmethod(lambda: torch.cuda.synchronize())
+    set_device = staticmethod(lambda i: torch.cuda.set_device(i))
+    upload = staticmethod(lambda t: t.cuda())
+
+
+DEV = Device()
 _JSON_OUT = None
 
 
@@ -188,7 +198,7 @@ def main_slbfgs(a, pkg, ctx, world, rank):
     acts = a.acts.split(",")
     N = a.samples
     Xh, Yh = pkg.synth_mnist(N, dims[0], dims[-1], 123)
-    X, Y = torch.from_numpy(Xh).cuda(), torch.from_numpy(Yh).cuda()
+    X, Y = DEV.upload(torch.from_numpy(Xh)), DEV.upload(torch.from_numpy(Yh))
     del Xh, Yh
     net = pkg.Mlp(ctx, dims, acts)
     P = net.init_params(123, "cpu")
@@ -219,13 +229,13 @@ def main_slbfgs(a, pkg, ctx, world, rank):
     run.iterate(max(a.warmup, 2))  # the second epoch of a launch sequence is the one captured
     ctx.prof_enable(True)          # clears the warmup's timings
     evals0, rows0, ep0 = float(run.info.n_evals), float(run.info.n_rows), int(run.info.iterations)
-    torch.cuda.synchronize()
+    DEV.synchronize()
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
+    DEV.synchronize()
     t0 = time.perf_counter()
     info = run.iterate(a.steps)
-    torch.cuda.synchronize()
+    DEV.synchronize()
     elapsed = time.perf_counter() - t0
     cnt = torch.tensor([elapsed, float(info.n_evals) - evals0, float(info.n_rows) - rows0], dtype=torch.float64)
     if world > 1:
@@ -286,8 +296,86 @@ def main_slbfgs(a, pkg, ctx, world, rank):
     run.close()
 
 
-def main():
-    a = parse()
+def visible_gpus() -> int:
+    """GPUs this process may use. torch.cuda.device_count() counts them without creating a HIP context,
+    so the launcher below never touches the GPU itself."""
+    return torch.cuda.device_count()
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_plan(gpus, env, argv, visible):
+    """How `bench.py --gpus N` runs.
+
+    Returns None when this process is a rank itself: N = 1, or WORLD_SIZE is set (torch.distributed.run
+    launched it; WORLD_SIZE must then equal N). Otherwise N > 1 ranks are needed and this process is only
+    their launcher: returns one (argv, env) per rank, rank r on GPU r, all rendezvousing on 127.0.0.1.
+    Raises SystemExit with a message (never falls back to one rank) when fewer than N GPUs are visible."""
+    if "WORLD_SIZE" in env:
+        ws = int(env["WORLD_SIZE"])
+        if gpus not in (1, ws):
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}; launch one rank per GPU")
+        return None
+    if gpus <= 1:
+        return None
+    if visible < gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} needs {gpus} visible GPUs, this host shows {visible}; "
+                         f"refusing to run fewer ranks")
+    port = free_port()
+    plan = []
+    for r in range(gpus):
+        e = dict(env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        plan.append(([sys.executable, os.path.abspath(__file__)] + list(argv), e))
+    return plan
+
+
+def run_children(plan, poll_s=0.2, grace_s=10.0) -> int:
+    """Start the ranks, wait for all of them; the first rank to fail takes the others down (a rank left
+    waiting in a barrier would otherwise hang). Returns the job's exit code (0 only if every rank exits 0).
+    Rank 0's stdout (the JSON line) is this process's stdout."""
+    import subprocess
+    procs = [subprocess.Popen(cmd, env=env) for cmd, env in plan]
+    code = 0
+    try:
+        while True:
+            live = [p for p in procs if p.poll() is None]
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                code = bad[0]
+                break
+            if not live:
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.time() + grace_s
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except Exception:
+                p.kill()
+                p.wait()
+    if code:
+        print(f"bench.py: a rank exited with status {code}", file=sys.stderr)
+    return code
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    plan = launch_plan(a.gpus, os.environ, argv,
+                       visible_gpus() if a.gpus > 1 and "WORLD_SIZE" not in os.environ else 0)
+    if plan is not None:
+        return run_children(plan)
     isolate_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -296,9 +384,18 @@ def main():
         # control plane only (RCCL unique id, barriers, max of the ranks' clocks): gloo over loopback, so
         # each process holds exactly one RCCL communicator, the library's own (lbf_comm_init), and the
         # data path's all-reduce is the only collective on xGMI
-        torch.cuda.set_device(local)
+        DEV.set_device(local)
         torch.distributed.init_process_group("gloo")
-    pkg = __graft_entry__.load_package()
+    try:
+        run_rank(a, world, rank, local, __graft_entry__.load_package())
+    finally:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+    return 0
+
+
+def run_rank(a, world, rank, local, pkg):
+    """One rank of the benchmark (world = 1: the whole job)."""
     dims = [int(x) for x in a.dims.split(",")]
     acts = a.acts.split(",")
     N = a.samples
@@ -312,20 +409,18 @@ def main():
         ctx.comm_init(1, 0, pkg.Context.unique_id())
     if a.solver == "slbfgs":
         main_slbfgs(a, pkg, ctx, world, rank)
-        if world > 1:
-            torch.distributed.destroy_process_group()
         return
     lo, hi = N * rank // world, N * (rank + 1) // world
     if a.data == "mnist":
         Xh, Yh = pkg.synth_mnist(N, dims[0], dims[-1], 123)
-        X = torch.from_numpy(Xh[lo:hi]).cuda()
-        Y = torch.from_numpy(Yh[lo:hi]).cuda()
+        X = DEV.upload(torch.from_numpy(Xh[lo:hi]))
+        Y = DEV.upload(torch.from_numpy(Yh[lo:hi]))
         del Xh, Yh
     else:  # this rank's shard generated in place
         X, Y = pkg.synth_regression(ctx, hi - lo, dims[0], row0=lo)
     net = pkg.Mlp(ctx, dims, acts)
     P = net.init_params(123, a.init)
-    torch.cuda.synchronize()
+    DEV.synchronize()
 
     run = pkg.LbfgsRun(net, P, X, Y, n_global=N, line_search=a.line_search, m=a.m, max_iters=1 << 30, tol=0.0,
                        record_cap=a.warmup + 2 * a.steps + 28)
@@ -362,15 +457,15 @@ def main():
     ctx.prof_enable(True)
 
     def barrier():
-        torch.cuda.synchronize()
+        DEV.synchronize()
         if world > 1:
             torch.distributed.barrier()
-        torch.cuda.synchronize()
+        DEV.synchronize()
 
     barrier()
     t0 = time.perf_counter()
     run.iterate(a.steps)
-    torch.cuda.synchronize()
+    DEV.synchronize()
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
@@ -455,9 +550,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(dims, acts, N, a.m, a.cpu_iters, a.data, min(rows, N))
         emit(out)
     run.close()
-    if world > 1:
-        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
