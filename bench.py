@@ -75,6 +75,10 @@ def parse(argv=None):
                          "is one epoch")
     ap.add_argument("--slbfgs-b", type=int, default=256, help="S-LBFGS minibatch b (config 4: 256)")
     ap.add_argument("--slbfgs-bh", type=int, default=128, help="S-LBFGS Hessian batch b_H (config 4: 128)")
+    ap.add_argument("--slbfgs-dp", choices=["replicated", "sliced"], default="replicated",
+                    help="S-LBFGS over N > 1 ranks: replicated = every rank runs the whole minibatch chain, only the "
+                         "epoch's full-batch gradient is sharded (one all-reduce per epoch); sliced = each rank "
+                         "evaluates 1/N of every minibatch (one all-reduce per inner step)")
     ap.add_argument("--slbfgs-step", type=float, default=0.005,
                     help="S-LBFGS step (config 4 names 0.02, which diverges to NaN on the synthetic data in the "
                          "fp64 oracle too; the work per epoch does not depend on it)")
@@ -157,11 +161,6 @@ def slbfgs_cpu_baseline(dims, acts, N, step, epochs=1):
                        f"{dt:.1f} s")
 
 
-def route_graph():
-    """Whether the S-LBFGS epochs ran from captured hipGraphs (single rank, LBF_SLBFGS_GRAPH unset or 1)."""
-    return os.environ.get("LBF_SLBFGS_GRAPH", "0") != "0" and int(os.environ.get("WORLD_SIZE", "1")) == 1
-
-
 class Device:
     """The three torch.cuda calls the rank code makes. tests/test_bench_launch.py swaps in a host stub so
     that the multi-rank control plane (unique-id broadcast, dominant-section broadcast, barriers, the MAX
@@ -202,10 +201,8 @@ def main_slbfgs(a, pkg, ctx, world, rank):
     del Xh, Yh
     net = pkg.Mlp(ctx, dims, acts)
     P = net.init_params(123, "cpu")
-    kw = dict(M=10, L=10, b=a.slbfgs_b, b_H=a.slbfgs_bh, step=a.slbfgs_step, lam=1e-4, tol=0.0)
-    # one stateful solve for the breakdown, the warmup and the timed epochs: an epoch whose launch sequence
-    # repeats is captured into a hipGraph on its second occurrence and replayed afterwards (the profiler's
-    # configuration is part of that sequence, so the warmup runs with the timed region's)
+    kw = dict(M=10, L=10, b=a.slbfgs_b, b_H=a.slbfgs_bh, step=a.slbfgs_step, lam=1e-4, tol=0.0, dp_mode=a.slbfgs_dp)
+    # one stateful solve for the breakdown, the warmup and the timed epochs
     run = pkg.SlbfgsRun(net, P, X, Y, **kw)
     # first epoch with every kernel section timed: the breakdown and the dominant section
     ctx.prof_select(None)
@@ -226,7 +223,7 @@ def main_slbfgs(a, pkg, ctx, world, rank):
     ctx.prof_select(dominant)
     ctx.prof_sample(PROF_EVERY)
     ctx.prof_enable(True)
-    run.iterate(max(a.warmup, 2))  # the second epoch of a launch sequence is the one captured
+    run.iterate(a.warmup)
     ctx.prof_enable(True)          # clears the warmup's timings
     evals0, rows0, ep0 = float(run.info.n_evals), float(run.info.n_rows), int(run.info.iterations)
     DEV.synchronize()
@@ -281,11 +278,11 @@ def main_slbfgs(a, pkg, ctx, world, rank):
             "config": {"workload": f"{a.dims} MLP ({a.acts}), S-LBFGS b={a.slbfgs_b} b_H={a.slbfgs_bh} L=M=10 step "
                                    f"{a.slbfgs_step} lambda 1e-4, N={N}; a step = one epoch ({N // a.slbfgs_b} inner "
                                    f"steps + the closing full-batch gradient at the new anchor)",
-                       "global_batch": N, "parallelism": f"dp{world}"},
+                       "global_batch": N,
+                       "parallelism": f"dp{world}" + (f"-{a.slbfgs_dp}" if world > 1 else "")},
             "grad_evals_per_s": round(evals_all / elapsed, 1),
             "grad_eval_gflops": round(rows_all * F / elapsed / 1e9, 1),
             "final_loss": float(info.final_loss),
-            "epoch_graphs": route_graph(),
             "roofline": roof,
             "kernel_ms_per_step": {k: round(v[0] / wep, 4) for k, v in sorted(breakdown.items())},
             "route_env": route_env(),

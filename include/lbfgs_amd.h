@@ -1,4 +1,4 @@
-/* include/lbfgs_amd.h — C ABI of the MI355X-native L-BFGS / S-LBFGS engine (liblbfgs_amd.so).
+/* include/lbfgs_amd.h — C ABI of the MI355X-native L-BFGS / S-LBFGS engine (liblbfgs_amd_abi3.so).
  *
  * Plain pointers and sizes only (no torch / HIP types in the signatures; a stream is passed as void*).
  * Every entry point names the reference interface it replaces (paths relative to SignorB/lbfgs-FFNN).
@@ -49,12 +49,14 @@ typedef struct lbf_ctx lbf_ctx;
 typedef struct lbf_mlp lbf_mlp;
 typedef struct lbf_lbfgs lbf_lbfgs;
 
-/* ABI revision of this header. Structs only ever grow at their end; a caller checks
- * lbf_abi_version() >= the LBF_ABI_VERSION it was compiled with before passing a struct the library
- * writes (lbf_solve_info), so an older library never writes past a newer caller's struct and a newer
- * library is never handed an older, smaller struct by a caller that did not check.
- * 2: lbf_solve_info.n_grad_after_loss; lbf_comm_init_local (in-process rank group). */
-#define LBF_ABI_VERSION 2
+/* ABI revision of this header. The library's file name and SONAME carry it (liblbfgs_amd_abi3.so), so a
+ * binary linked against another revision fails to load instead of handing this library structs of a
+ * different size: ABI 1 had no lbf_abi_version() to check, and lbf_solve_info / lbf_slbfgs_params have
+ * grown since. Within one revision structs never change. A caller that loads the library by path (dlopen,
+ * ctypes) checks lbf_abi_version() == LBF_ABI_VERSION before passing any struct.
+ * 2: lbf_solve_info.n_grad_after_loss; lbf_comm_init_local (in-process rank group).
+ * 3: lbf_slbfgs_params.dp_mode; the revision in the library name. */
+#define LBF_ABI_VERSION 3
 
 const char *lbf_last_error(void);
 const char *lbf_version(void);
@@ -164,8 +166,16 @@ typedef struct lbf_slbfgs_params {
    * pairs after it, 0. Reading each row back synchronises the stream: not for timed runs. */
   double *pair_trace;
   int pair_trace_cap;
+  /* ABI 3, data parallelism (a communicator on the context): LBF_SLBFGS_DP_REPLICATED (default) runs the
+   * whole minibatch chain on every rank with no collective (identical inputs, identical bits) and shards
+   * only the full-batch gradient at each epoch's anchor (s_lbfgs.hpp:206, 274-284), one all-reduce per
+   * epoch; LBF_SLBFGS_DP_SLICED evaluates this rank's 1/p slice of every minibatch and Hessian batch, one
+   * all-reduce per inner step. Ignored without a communicator. */
+  int dp_mode;
 } lbf_slbfgs_params;
 #define LBF_PAIR_TRACE_COLS 8
+#define LBF_SLBFGS_DP_REPLICATED 0
+#define LBF_SLBFGS_DP_SLICED 1
 
 /* Gradient descent with momentum == cuda_mlp::CudaGD (src/cuda/gd.cuh:38-106; setters :22-25). */
 typedef struct lbf_gd_params {
@@ -249,9 +259,7 @@ int lbf_slbfgs_solve(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params
                      const float *d_Y, long long N, lbf_record *rec, lbf_solve_info *info);
 /* Stateful S-LBFGS (benchmarking, and callers that check progress between epochs): begin copies nothing
  * yet; iterate runs up to `epochs` more epochs (returns early on convergence) with d_params updated after
- * each call; end releases the solver. One begin + iterate(max_epochs) is lbf_slbfgs_solve. With
- * LBF_SLBFGS_GRAPH=1 (single rank), an epoch whose launch sequence repeats runs from a hipGraph captured
- * from its second occurrence on (bitwise the eager epochs; measured slower on ROCm 7.2, off by default). */
+ * each call; end releases the solver. One begin + iterate(max_epochs) is lbf_slbfgs_solve. */
 typedef struct lbf_slbfgs lbf_slbfgs;
 int lbf_slbfgs_begin(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params, const float *d_X,
                      const float *d_Y, long long N, lbf_slbfgs **out);

@@ -1,6 +1,6 @@
 """lbfgs-ffnn_amd — MI355X-native L-BFGS / S-LBFGS engine for dense FFNNs.
 
-Compute lives in ``build/liblbfgs_amd.so`` (hand-written HIP kernels for gfx950 behind the C ABI
+Compute lives in ``build/liblbfgs_amd_abi3.so`` (hand-written HIP kernels for gfx950 behind the C ABI
 ``include/lbfgs_amd.h``). This package is the host-side mirror of the reference's unified API.
 The directory name contains a hyphen, so load it with :func:`load` from the repo root helpers
 (``tests/conftest.py``, ``bench.py``, ``__graft_entry__.py``) under the module name ``lbfgs_ffnn_amd``.

@@ -1,4 +1,4 @@
-"""ctypes binding of ``build/liblbfgs_amd.so`` (C ABI: ``include/lbfgs_amd.h``).
+"""ctypes binding of ``build/liblbfgs_amd_abi3.so`` (C ABI: ``include/lbfgs_amd.h``).
 
 The shared library is the product: every numeric operation below runs in its HIP kernels. There is
 no CPU fallback; a missing or unloadable library raises :class:`LbfError` immediately.
@@ -14,9 +14,9 @@ from typing import Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("LBF_LIB_PATH") or os.path.join(_HERE, "build", "liblbfgs_amd.so")
-
-ABI_VERSION = 2  # include/lbfgs_amd.h LBF_ABI_VERSION
+ABI_VERSION = 3  # include/lbfgs_amd.h LBF_ABI_VERSION (also in the library's file name)
+LIB_PATH = os.environ.get("LBF_LIB_PATH") or os.path.join(_HERE, "build", f"liblbfgs_amd_abi{ABI_VERSION}.so")
+SLBFGS_DP_REPLICATED, SLBFGS_DP_SLICED = 0, 1
 LS_WOLFE, LS_ARMIJO = 0, 1
 INIT_CPU, INIT_CUDA = 0, 1
 ACTS = {"linear": 0, "tanh": 1, "relu": 2, "sigmoid": 3}
@@ -35,7 +35,7 @@ class SlbfgsParams(C.Structure):
     _fields_ = [("max_epochs", C.c_int), ("tol", C.c_double), ("M", C.c_int), ("L", C.c_int), ("b", C.c_int),
                 ("b_H", C.c_int), ("step", C.c_double), ("reg", C.c_double), ("seed", C.c_uint),
                 ("fd_eps", C.c_double), ("hvp_exact", C.c_int), ("pair_trace", C.POINTER(C.c_double)),
-                ("pair_trace_cap", C.c_int)]
+                ("pair_trace_cap", C.c_int), ("dp_mode", C.c_int)]
 
 
 class GdParams(C.Structure):
@@ -70,7 +70,7 @@ def lib():
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
-        raise LbfError(f"liblbfgs_amd.so not built ({LIB_PATH}); run `make -C lbfgs-ffnn_amd` or "
+        raise LbfError(f"{os.path.basename(LIB_PATH)} not built ({LIB_PATH}); run `make -C lbfgs-ffnn_amd` or "
                        "__graft_entry__.build()")
     L = C.CDLL(LIB_PATH)
     sig = {
@@ -143,7 +143,7 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.lbf_abi_version() < ABI_VERSION:
+    if L.lbf_abi_version() != ABI_VERSION:
         raise LbfError(f"{LIB_PATH} implements ABI {L.lbf_abi_version()}, this binding needs {ABI_VERSION}: rebuild it")
     _lib = L
     return L

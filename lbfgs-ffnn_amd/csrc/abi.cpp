@@ -1,4 +1,4 @@
-// extern "C" surface of liblbfgs_amd.so (declared in include/lbfgs_amd.h). Every call converts
+// extern "C" surface of liblbfgs_amd_abi3.so (declared in include/lbfgs_amd.h). Every call converts
 // internal exceptions into a status code + thread-local message (the reference aborts instead:
 // src/cuda/common.cuh:18-23, cublas_handle.cuh:14-19).
 #include "../../include/lbfgs_amd.h"
@@ -439,6 +439,7 @@ void lbf_slbfgs_default_params(lbf_slbfgs_params *p) {
   p->hvp_exact = 0;
   p->pair_trace = nullptr;
   p->pair_trace_cap = 0;
+  p->dp_mode = LBF_SLBFGS_DP_REPLICATED;
 }
 
 int lbf_lbfgs_begin(lbf_mlp *net, const lbf_lbfgs_params *prm, float *d_params, const float *d_X,

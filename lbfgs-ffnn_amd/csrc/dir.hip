@@ -170,80 +170,12 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
 
 constexpr int DF_THREADS = 256;
 
-// The in-launch combine (DirArgs::ncb blocks after the column blocks; combine_small_kernel's arithmetic,
-// one element per lane). Every load of the lane (g, x_in, the element of each of the SM ring slots) is
-// issued before the wait, so the sweep's memory traffic overlaps the column sums and the history step;
-// after the publish, the per-slot coefficients are scattered through LDS (slot of logical i -> cs_i, cy_i;
-// zero for slots not live) and summed slot by slot.
-template <int SM>
-__device__ __forceinline__ void combine_worker(const DirArgs &a, int ncols) {
-  const CombineArgs &c = a.cmb;
-  const HistView &h = c.h;
-  const int S_ = h.slots, t = threadIdx.x, lane = t & 63;
-  __shared__ double cs_s[SM], cy_s[SM];
-  __shared__ double cg_s;
-  const long long e0 = (long long)(blockIdx.x - ncols) * DF_THREADS + t;
-  const bool in = e0 < h.n;
-  const long long e = in ? e0 : h.n - 1; // loads unconditional (clamped), results masked
-  const float gv = c.g[e];
-  const float xv = c.x_in[e];
-  float sv[SM], yv[SM];
-#pragma unroll
-  for (int j = 0; j < SM; ++j) {
-    const long long off = (long long)(j < S_ ? j : S_ - 1) * h.ld + e;
-    sv[j] = h.S[off];
-    yv[j] = h.Y[off];
-  }
-  if (t < SM) {
-    cs_s[t] = 0.0;
-    cy_s[t] = 0.0;
-  }
-  if (t == 0) {
-    while (__hip_atomic_load(&a.cmb_flag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-      __builtin_amdgcn_s_sleep(2);
-  }
-  __syncthreads();
-  if (t < 64) { // lane i < k: logical pair i (sc1 loads: published this launch by another block)
-    const double *d = a.cmb_desc;
-    const int k = int(__hip_atomic_load(&d[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    if (lane < k) {
-      const int slot = int(__hip_atomic_load(&d[1 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      cs_s[slot] = __hip_atomic_load(&d[1 + S_ + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      cy_s[slot] = __hip_atomic_load(&d[1 + 2 * S_ + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (lane == 0) cg_s = __hip_atomic_load(&d[1 + 3 * S_], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (t == 0 && // descriptor read by this block: the last worker re-arms the flag for the next launch
-      __hip_atomic_fetch_add(&a.cmb_flag[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == unsigned(a.ncb - 1)) {
-    __hip_atomic_store(&a.cmb_flag[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.cmb_flag[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  double acc = cg_s * double(gv);
-#pragma unroll
-  for (int j = 0; j < SM; ++j)
-    if (j < S_) acc += cs_s[j] * double(sv[j]) + cy_s[j] * double(yv[j]);
-  if (!in) return;
-  const float dd = float(acc);
-  if (c.dir) c.dir[e] = dd;
-  if (c.x_out) {
-    const float o = xv + float(c.alpha) * dd;
-    c.x_out[e] = o;
-    if (c.x_out2) c.x_out2[e] = o;
-  }
-}
-
 // Column sums, then the last block runs the history step. Hand-off without fences (tail.hip's
 // tail_cols_fin): sc1 column stores waited for before the arrival add; the last arrival reads them sc1.
-template <int SM>
 __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs a) {
   const HistView &h = a.g.h;
   if (h.abort && *h.abort) return; // uniform for the launch: nobody arrives, the counter stays 0
   const int ncols = 6 * h.m + 6; // dir_ncols(m)
-  if (int(blockIdx.x) >= ncols) {
-    combine_worker<SM>(a, ncols);
-    return;
-  }
   extern __shared__ double dyn[]; // sy [2*m*m] (SY and its transpose) | yy [m*m] | SY, YY [S*S] | rho [S]
   __shared__ HistSmem sm;
   __shared__ double ws[4];
@@ -312,28 +244,6 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs 
     hist_prologue<false>(st, sm, ist_l[IST_WSLOT]);
     hist_core<false>(st, sm, dyn, 2 * m * m, dyn + 2 * m * m, m * m);
   }
-  // wave 0 (the others left hist_core early): publish the order and coefficients to the combine blocks.
-  // Its coefficient stores are drained first (own stores, re-read through L2), the descriptor is stored
-  // write-through (sc1) and drained, then the flag (the fence-free hand-off of tail_cols_fin).
-  if (a.ncb > 0 && t < 64) {
-    const int S_s = h.slots, k = sm.k;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    double *d = a.cmb_desc;
-    if (t < k) {
-      const double cs = __hip_atomic_load(&h.coef[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const double cy = __hip_atomic_load(&h.coef[S_s + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&d[1 + t], double(sm.L[t]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&d[1 + S_s + t], cs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&d[1 + 2 * S_s + t], cy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (t == 0) {
-      const double cg = __hip_atomic_load(&h.coef[2 * S_s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&d[0], double(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&d[1 + 3 * S_s], cg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (t == 0) __hip_atomic_store(&a.cmb_flag[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 template <int C>
@@ -356,11 +266,8 @@ static int dir_vpw(int m) {
 // Columns per block: 256 (one quad per lane) or, by default, 512 (two): at n = 535,818 (cfg 4) 256-column
 // blocks are 2093, above the 1792 this kernel's 88 SGPRs admit at once (7 per CU), so the sweep ran in
 // two rounds; 1047 blocks of 512 columns run in one, with twice the loads in flight per lane.
-// (LBF_DIR_COLS=256 selects the narrow form.) m <= 16.
-static int dir_c() {
-  static const int c = env_int("LBF_DIR_COLS", 512) == 256 ? 4 : 8;
-  return c;
-}
+// m <= 16.
+static int dir_c() { return 8; }
 bool dir_supported(int m, long long n) { return m >= 0 && m <= DIR_MAXM && n > 0 && n <= DIR_MAXN; }
 int dir_cols_per_block(int m, long long n) {
   (void)m;
@@ -373,34 +280,21 @@ void dir_sweep(hipStream_t s, const DirArgs &a) {
   LBF_REQUIRE(dir_supported(a.g.h.m, a.g.h.n), "dir_sweep: history size / vector length");
   LBF_REQUIRE(a.want_dir == 0 || a.want_dir == 1, "dir_sweep: want_dir 0 / 1");
   LBF_REQUIRE(a.nb == int(cdiv(a.g.h.n, dir_cols_per_block(a.g.h.m, a.g.h.n))), "dir_sweep: block count");
-  if (dir_c() == 8) launch_sweep<8>(s, a, dir_vpw(a.g.h.m));
-  else launch_sweep<4>(s, a, dir_vpw(a.g.h.m));
+  launch_sweep<8>(s, a, dir_vpw(a.g.h.m));
   LBF_KERNEL_CHECK();
 }
 
 static void cols_fin_launch(hipStream_t s, const DirArgs &a) {
-  static bool attr_set = false;
-  const void *fns[] = {reinterpret_cast<const void *>(dir_cols_fin_kernel<1>),
-                       reinterpret_cast<const void *>(dir_cols_fin_kernel<8>),
-                       reinterpret_cast<const void *>(dir_cols_fin_kernel<12>),
-                       reinterpret_cast<const void *>(dir_cols_fin_kernel<DIR_MAXM + 1>)};
-  if (!attr_set) { // m up to GRAM_FIN_MAXM: ~100 KB of dynamic LDS
-    for (const void *f : fns)
-      LBF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 16 * 1024));
-    attr_set = true;
-  }
+  // m up to GRAM_FIN_MAXM: ~100 KB of dynamic LDS; once per process, thread-safe
+  static const bool attr_set = [] {
+    LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(dir_cols_fin_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 16 * 1024));
+    return true;
+  }();
+  (void)attr_set;
   const int m = a.g.h.m, S_ = a.g.h.slots;
   const size_t shmem = (size_t(3) * m * m + 2 * size_t(S_) * S_ + S_) * sizeof(double);
-  const dim3 grid(unsigned(dir_ncols(m) + a.ncb));
-  if (a.ncb > 0) {
-    LBF_REQUIRE(a.want_dir == 1 && S_ <= DIR_MAXM + 1 && a.cmb_flag && a.cmb_desc && a.cmb.h.slots == S_,
-                "dir_fin: in-launch combine needs want_dir 1, m <= DIR_MAXM and its buffers");
-    LBF_REQUIRE((long long)a.ncb * DF_THREADS >= a.cmb.h.n, "dir_fin: combine blocks cover n");
-  }
-  if (a.ncb == 0) hipLaunchKernelGGL(dir_cols_fin_kernel<1>, grid, dim3(DF_THREADS), shmem, s, a);
-  else if (S_ <= 8) hipLaunchKernelGGL(dir_cols_fin_kernel<8>, grid, dim3(DF_THREADS), shmem, s, a);
-  else if (S_ <= 12) hipLaunchKernelGGL(dir_cols_fin_kernel<12>, grid, dim3(DF_THREADS), shmem, s, a);
-  else hipLaunchKernelGGL(dir_cols_fin_kernel<DIR_MAXM + 1>, grid, dim3(DF_THREADS), shmem, s, a);
+  hipLaunchKernelGGL(dir_cols_fin_kernel, dim3(unsigned(dir_ncols(m))), dim3(DF_THREADS), shmem, s, a);
   LBF_KERNEL_CHECK();
 }
 
@@ -412,7 +306,6 @@ void gram_fin(hipStream_t s, const DirArgs &a) {
   LBF_REQUIRE(gram_fin_supported(a.g.h.m), "gram_fin: history size");
   LBF_REQUIRE(a.want_dir == 0 || a.want_dir == 1, "gram_fin: want_dir 0 / 1");
   LBF_REQUIRE(a.nb == gram_nwg(a.g.h.n), "gram_fin: one partial row per Gram workgroup");
-  LBF_REQUIRE(a.ncb == 0, "gram_fin: no in-launch combine");
   cols_fin_launch(s, a);
 }
 

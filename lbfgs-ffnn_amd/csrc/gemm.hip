@@ -57,9 +57,6 @@ struct GemmK {
   float *head_delta, *head_slab;
   double *head_sse;
   int head_fold, head_fold_c0;
-  unsigned *fin_cnt;
-  float *fin_out;
-  int nsplits;
 };
 
 // Side job (see GemmDesc): one 256-column group (four per lane) x 4 split stripes per block, fp64 in
@@ -248,63 +245,6 @@ __device__ __forceinline__ void store_mc(float *lds, const f32x4 (&r)[R / 32], i
 
 // Epilogues shared by both main loops: the fused output layer (EPI_HEAD) or the bias/activation/
 // derivative/slab store of the accumulators.
-typedef __attribute__((address_space(1))) float gfloat_t;
-typedef __attribute__((address_space(1))) unsigned gu32_t;
-
-// In-launch split-K reduction (GemmDesc::fin_cnt), the hand-off of MI355X_MICROARCH.md's visibility table,
-// first row (cdna_hip_programming.md's split-K recipe, sc1 variant): every split stored its slab tile with
-// sc1 (write-through) stores; each storing wave drains them (vmcnt(0)), the workgroup barrier, then ONE
-// lane's relaxed agent-scope add on the tile's counter. The workgroup whose add returns nsplits - 1 reads
-// every slab of the tile with sc1 buffer loads (no acquire fence needed for them), in split order.
-template <int BM, int BN, int KW>
-__device__ __forceinline__ void gemm_fin_reduce(const GemmK &g, float *lds, int m0, int n0) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int *flag = reinterpret_cast<int *>(lds); // the staging array is free: every k-step is done
-  if (threadIdx.x == 0) {
-    gu32_t *cnt = (gu32_t *)(g.fin_cnt + (int(blockIdx.y) * int(gridDim.x) + int(blockIdx.x)));
-    const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == unsigned(g.nsplits - 1) ? 1 : 0;
-    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // next launch (stream-ordered)
-    flag[0] = last;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); // compiler-only: the slab loads stay below
-  constexpr int NT = 256 * KW, Q = BN / 4, RP = NT / Q; // 16-B column groups per row, rows per pass
-  static_assert(NT % Q == 0 && BM % RP == 0, "fin: tile shape");
-  const int ns = g.nsplits;
-  const unsigned plane = unsigned(g.slab_stride) * 4u; // bytes per split (host-checked < 2^31 in all)
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float *>(g.C), 0, int(unsigned(ns) * plane), 0x00020000);
-#pragma unroll
-  for (int r0 = 0; r0 < BM; r0 += RP) {
-    const int m = m0 + r0 + int(threadIdx.x) / Q, n = n0 + 4 * (int(threadIdx.x) % Q);
-    const bool ok = m < g.M && n < g.N;
-    const unsigned off = ok ? unsigned((long long)m * g.ldc + n) * 4u : 0u;
-    f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-    int k = 0;
-    for (; k + 8 <= ns; k += 8) { // eight 16-B loads in flight, summed in split order
-      f32x4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, int(off + unsigned(k + u) * plane),
-                                                                                0, 16)); // aux 16 = sc1
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
-    }
-    for (; k < ns; ++k)
-      acc += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, int(off + unsigned(k) * plane), 0, 16));
-    if (ok) {
-      const f32x4 b = g.bias ? *reinterpret_cast<const f32x4 *>(g.bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
-      f32x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = act_rt(g.act, acc[j] + b[j]); // fwd_reduce_act's expression
-      *reinterpret_cast<f32x4 *>(g.fin_out + (long long)m * g.N + n) = o;
-    }
-  }
-}
-
 template <int WM, int WN, int TM, int TN, int EPI, int KW, class HPre>
 __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][TN], float *lds, HPre &hpre, int zsplit,
                                               int m0, int n0, int wm, int wn, int li, int lh, int kgrp) {
@@ -404,12 +344,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
     KTB(7);
     return;
   }
-  const bool fin = EPI == EPI_STORE && g.fin_cnt != nullptr; // uniform: every wave joins the reduction
-  if (KW > 1 && kgrp != 0) {
-    if constexpr (EPI == EPI_STORE)
-      if (fin) gemm_fin_reduce<BM, BN, KW>(g, lds, m0, n0);
-    return; // group 0 holds the sums
-  }
+  if (KW > 1 && kgrp != 0) return; // group 0 holds the sums
   // Epilogue: lanes 0-31 own consecutive columns -> each register row is a 128-B coalesced store.
   float *C = g.C + (EPI == EPI_STORE ? (long long)zsplit * g.slab_stride : 0LL);
   // EPI_DX's act' operand (the previous layer's activations) is loaded for the whole (tm, tn) block before
@@ -441,19 +376,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
           float v = acc[tm][tn][r];
           if constexpr (EPI == EPI_FWD) v = act_c<A>(v + bn);
           if constexpr (EPI == EPI_DX) v *= dact_c<A>(ax[r]);
-          if (nok && m < g.M) {
-            if (EPI == EPI_STORE && fin) // write-through for the in-launch reduction
-              __hip_atomic_store((gfloat_t *)(C + (long long)m * g.ldc + n), v, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-            else
-              C[(long long)m * g.ldc + n] = v;
-          }
+          if (nok && m < g.M) C[(long long)m * g.ldc + n] = v;
         }
       }
     }
   });
-  if constexpr (EPI == EPI_STORE)
-    if (fin) gemm_fin_reduce<BM, BN, KW>(g, lds, m0, n0);
 }
 
 // KW k-groups of 4 waves each (KW = 2: 8 waves, two per SIMD, for tiles too small to fill the chip
@@ -702,17 +629,7 @@ struct GldsPiece {
 // KW = 2 (small tiles that run one workgroup per CU, e.g. 32 x 128 for a rank's shard): eight waves, two
 // per SIMD; k-group q computes steps [8q, 8q+8) of every 32-deep tile from the same LDS stage, group 0
 // alone issues the LDS-DMA pieces, and the groups' accumulators are summed through LDS in group order.
-// PIPE (small tiles, one or two waves per SIMD): the fragments of k-tile i+1 are read from LDS while the
-// MFMAs of k-tile i run (two register sets), and tile i's buffer is refilled as soon as its fragments are
-// in registers, one k-tile further ahead than the plain loop; the single wave per SIMD then no longer
-// stalls on LDS latency at every k-tile.
-// LDR (KW = 2): the two groups specialise instead of splitting the k-steps: group 1 (waves 4-7) only
-// issues the LDS-DMA pieces, group 0 (waves 0-3) only reads fragments and runs every MFMA. A wave that
-// issues DMA stalls for ~100+ cycles per 1-KiB piece, so loader and MFMA work on the same wave serialise
-// (a 32 x 128 tile then moves ~22 GB/s per CU and its MFMAs idle half the time); on separate waves of the
-// same SIMD they overlap.
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1,
-          bool PIPE = false, bool LDR = false>
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1>
 __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(const GemmK g) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32;
   constexpr int ASZ = BM * BK, STG = (BM + BN) * BK;
@@ -785,7 +702,7 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
     pc[i] = q;
   }
   auto issue = [&](int t) {
-    if (KW > 1 && kgrp != (LDR ? 1 : 0)) return; // wave-uniform
+    if (KW > 1 && kgrp != 0) return; // wave-uniform
     float *stage = lds + (t % NS) * STG;
     const int kt = kb + t * BK;
 #pragma unroll
@@ -797,9 +714,8 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
     }
   };
   // fragments of one k-tile for this k-group: 16 / KW k-steps of every (tm, tn) operand
-  static_assert(!LDR || (KW == 2 && !PIPE), "LDR: two groups, plain loop");
-  constexpr int KWC = LDR ? 1 : KW; // k-groups sharing the MFMA work
-  const int kq0 = LDR ? 0 : kgrp;
+  constexpr int KWC = KW; // k-groups sharing the MFMA work
+  const int kq0 = kgrp;
   constexpr int SK = 16 / KWC;
   struct Frag {
     float a[TM][SK], b[TN][SK];
@@ -870,58 +786,20 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
     if (t < nk) issue(t);
-  if constexpr (PIPE) {
-    // f[i & 1] holds k-tile i's fragments. Iteration i: wait until k-tile i+1 has landed and every wave's
-    // reads of k-tile i are complete (vmcnt, lgkmcnt, barrier), refill buffer i % NS with k-tile i + NS,
-    // then k-tile i's MFMAs with the DMA issue and the LDS reads of k-tile i+1 interleaved between them
-    // (sched_group_barrier): the wave's one MFMA chain no longer waits behind that work. The refill is
-    // unconditional (k-tiles past the end read the zero chunk into a buffer nobody reads again), so the
-    // loop body is one basic block and the wait count is the constant NS-2 k-tiles.
-    static_assert(KW == 1, "PIPE: one k-group (the DMA issue must be branch-free)");
-    Frag f[2];
-    if (nk > 0) {
-      for (int t = nk; t < NS - 1; ++t) issue(t); // pad to NS-1 issued k-tiles (zero chunks)
-      vm_wait_tiles<P, NS>(NS - 2); // k-tile 0 landed
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      issue(NS - 1);
-      lds_frag(0, f[0]);
-    }
-    constexpr int NMF = SK * TM * TN;   // MFMAs per k-tile
-    constexpr int NDS = (TM + TN) * 4;  // LDS read instructions per k-tile (upper bound)
-    for (int i = 0; i < nk; i += 2) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) { // unrolled by two: the register sets are static
-        const int ii = i + u;
-        if (ii >= nk) break;
-        vm_wait_tiles<P, NS>(NS - 2); // k-tile ii+1 landed (NS-2 k-tiles issued after it)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        issue(ii + NS); // buffer ii % NS: its fragments are in f[u]
-        lds_frag((ii + 1) % NS, f[u ^ 1]);
-        mfma_frag(f[u]);
-#pragma unroll
-        for (int j = 0; j < NMF; ++j) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); // one MFMA
-          if (j < P) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0); // one DMA piece
-          if (j < NDS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); // one LDS read
-        }
-      }
-    }
-  } else {
+  {
     for (int i = 0; i < nk; ++i) {
       vm_wait_tiles<P, NS>(min(NS - 2, nk - 1 - i)); // this wave's pieces of k-tile i landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier(); // everyone's pieces landed; buffer (i - 1) % NS no longer read
       if (EPI == EPI_HEAD && i < 24) KT(1 + i);
       if (i + NS - 1 < nk) issue(i + NS - 1);
-      if (!LDR || kgrp == 0) compute(i % NS); // wave-uniform
+      compute(i % NS);
     }
   }
   if (EPI == EPI_HEAD) KT(25);
   if (EPI == EPI_HEAD) KTC(41);
   __syncthreads(); // the LDS is the epilogue's now
-  if constexpr (KW > 1 && !LDR) { // group sums through LDS, in group order (group 0 keeps the result)
+  if constexpr (KW > 1) { // group sums through LDS, in group order (group 0 keeps the result)
     float *red = lds;
     static_assert(TM * TN * 16 * 256 <= LDS_F, "k-group reduction buffer");
     for (int q = 1; q < KW; ++q) {
@@ -948,135 +826,13 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
   gemm_epilogue<WM, WN, TM, TN, EPI, KW>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, kgrp);
 }
 
-// Direct-operand GEMM for the 32 x 128 tile with a k-contiguous A (rows of X / activations) and an
-// mn-contiguous B (W as [K][N]), no gather: the MFMA operands are loaded from global memory (L2) straight
-// into registers, with no LDS staging in the main loop. The LDS-DMA kernel's 32 x 128 tile moves ~22 GB/s
-// of operands per CU (every DMA piece stalls its issuing wave ~100+ cycles), half its MFMA rate; vector
-// loads issue in a few cycles and land asynchronously. Two k-groups of four waves (KW = 2) split the 16
-// k-steps of every 32-deep k-tile exactly as gemm_glds_kernel<1, 4, 1, 1, true, false, *, false, *, 2>
-// does (lane half h consumes k = 16h + 8q + s at step s of group q, groups summed through LDS in group
-// order): the same MFMA sequence on the same values, so the results are bitwise the LDS-DMA kernel's.
-// Operands of D k-tiles are in flight per wave (registers rotate over an unrolled loop).
-template <int EPI, int D, int SETS>
-__global__ __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(1, 2))) void gemm_direct_kernel(const GemmK g) {
-  static_assert(SETS >= D, "register sets");
-  constexpr int WM = 1, WN = 4, TM = 1, TN = 1, KW = 2, BM = 32, BN = 128, BK = 32;
-  constexpr int HEAD_F = headc::smem_floats_epi(BN, BM > headc::TB ? BM : headc::TB);
-  constexpr int RED_F = TM * TN * 16 * 256;
-  constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > RED_F) ? HEAD_F : RED_F;
-  __shared__ __attribute__((aligned(16))) float lds[LDS_F];
-  if (g.abort && *g.abort) return;
-  const int zsplit = int(blockIdx.z);
-  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
-  const int kgrp = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 8));
-  const int wm = 0, wn = wave;
-  const int li = lane & 31, lh = lane >> 5;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-  const int kb = zsplit * g.k_chunk;
-  const int ke = min(g.K, kb + g.k_chunk);
-  const int nk = kb < ke ? (ke - kb + BK - 1) / BK : 0;
-  // this lane's operand streams: A row m0 + li (clamped), B column n0 + 32 wn + li (clamped)
-  const int row = min(m0 + li, g.M - 1);
-  const int col = min(n0 + wn * 32 + li, g.N - 1);
-  const float *Ar = g.A + (long long)row * g.lda;
-  const float *Bc = g.B + col;
-  // rows past M and columns past N read clamped addresses but must contribute exact zeros, as the LDS-DMA
-  // kernel's zero chunk does: the EPI_HEAD epilogue (delta, the fold's partial rows) consumes the
-  // accumulators of the whole tile, not only the stored entries
-  const bool row_ok = m0 + li < g.M, col_ok = n0 + wn * 32 + li < g.N;
-  const int kl = 16 * lh + 8 * kgrp; // first k of this lane's 8 within a k-tile
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.0f;
-  headc::EpiPrefetch<BN, BM, 256 * KW> hpre;
-  if constexpr (EPI == EPI_HEAD) {
-    hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
-    if (g.head_fold > 0) hpre.load_fold(g.A, g.lda, g.a_idx, g.head_fold_c0, g.head_fold, m0, g.M);
-  }
-  struct Ops {
-    f32x4 a0, a1;
-    float b[8];
-  };
-  // k-tile t's operands: unconditional loads from clamped addresses (k >= ke reads an earlier k of the
-  // same row / column), the out-of-range values zeroed when used
-  auto load = [&](int t, Ops &o) {
-    const int k0 = kb + t * BK + kl;
-    const int ka = k0 + 4 <= ke ? k0 : kb, kc = k0 + 8 <= ke ? k0 + 4 : kb;
-    o.a0 = *reinterpret_cast<const f32x4 *>(Ar + ka);
-    o.a1 = *reinterpret_cast<const f32x4 *>(Ar + kc);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int k = k0 + s;
-      o.b[s] = Bc[(long long)(k < ke ? k : kb) * g.ldb];
-    }
-  };
-  auto mask = [&](Ops &o) { // after the loads have landed (the selects consume them)
-    if (!row_ok) {
-      o.a0 = (f32x4){0.f, 0.f, 0.f, 0.f};
-      o.a1 = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-    if (!col_ok)
-#pragma unroll
-      for (int s = 0; s < 8; ++s) o.b[s] = 0.0f;
-  };
-  auto mma = [&](int t, Ops &o) {
-    mask(o);
-    const int k0 = kb + t * BK + kl;
-    const bool full = k0 + 8 <= ke; // wave-uniform only per lane half; masks are per element
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      float a = s < 4 ? o.a0[s] : o.a1[s - 4];
-      float b = o.b[s];
-      if (!full && k0 + s >= ke) {
-        a = 0.0f;
-        b = 0.0f;
-      }
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[0][0], 0, 0, 0);
-    }
-  };
-  // The loop runs a multiple of D k-tiles and every load is unconditional (k-tiles past the end read
-  // clamped addresses and contribute zero products, which leave the sums bitwise unchanged): straight-line
-  // code, so the compiler's wait counts keep D - 1 k-tiles in flight instead of draining at a branch.
-  // SETS > D register sets: a set is refilled SETS - D + 1 k-tiles after its MFMAs were issued, not
-  // right behind them (the refill's loads must not land in registers a queued MFMA has yet to read).
-  Ops ops[SETS];
-  if (nk > 0) {
-    const int nkp = (nk + SETS - 1) / SETS * SETS;
-#pragma unroll
-    for (int t = 0; t < D - 1; ++t) load(t, ops[t]);
-    for (int i = 0; i < nkp; i += SETS) {
-#pragma unroll
-      for (int u = 0; u < SETS; ++u) { // unrolled by SETS: the register sets are static
-        load(i + u + D - 1, ops[(u + D - 1) % SETS]);
-        __builtin_amdgcn_sched_barrier(0); // the loads stay ahead of this k-tile's MFMAs (no sinking)
-        mma(i + u, ops[u]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-  // k-group sums through LDS, in group order (group 0 keeps the result): gemm_glds_kernel's
-  float *red = lds;
-  if (kgrp == 1) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[r * 256 + (threadIdx.x & 255)] = acc[0][0][r];
-  }
-  __syncthreads();
-  if (kgrp == 0) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[0][0][r] += red[r * 256 + threadIdx.x];
-  }
-  __syncthreads();
-  gemm_epilogue<WM, WN, TM, TN, EPI, KW>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, kgrp);
-}
-
 namespace {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // NS > 0: the LDS-DMA kernel with NS tile buffers where the shape allows it (FAST shapes, no gathered
 // mn-contiguous operand); otherwise the register-staged kernel (KW k-groups, PF register sets).
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int KW = 1, int PF = 1, int NS = 0,
-          bool PIPE = false, bool LDR = false>
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int KW = 1, int PF = 1, int NS = 0>
 void launch(hipStream_t s, const GemmDesc &d) {
   // FAST loads: K % 4 == 0, vector-aligned operands, column counts % 4 == 0
   const bool fast = d.K % 4 == 0 && (d.lda % 4 == 0) && (d.ldb % 4 == 0) &&
@@ -1124,27 +880,14 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.head_sse = d.head_sse;
   k.head_fold = d.head_fold;
   k.head_fold_c0 = d.head_fold_c0;
-  k.fin_cnt = d.fin_cnt;
-  k.fin_out = d.fin_out;
-  k.nsplits = d.splits > 1 ? d.splits : 1;
   dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
-  static const bool glds_on = env_int("LBF_GEMM_GLDS", 1) != 0;
-  if constexpr (WM == 1 && WN == 4 && TM == 1 && TN == 1 && AKC && !BKC && KW == 2 && EPI != EPI_DX) {
-    // the 32 x 128 forward tile with operands straight from L2 into registers (gemm_direct_kernel)
-    if (d.direct && fast && !d.a_idx && k.side_planes == 0 && d.K >= 8) {
-      static const int var = env_int("LBF_GEMM_DIRECT_SETS", 4);
-      if (var == 3) hipLaunchKernelGGL((gemm_direct_kernel<EPI, 3, 3>), grid, dim3(512), 0, s, k);
-      else hipLaunchKernelGGL((gemm_direct_kernel<EPI, 3, 4>), grid, dim3(512), 0, s, k);
-      return;
-    }
-  }
   if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
-    if (fast && glds_on && (AKC || !d.a_idx)) {
+    if (fast && (AKC || !d.a_idx)) {
       const dim3 gb(256 * KW);
       if (d.a_idx)
-        hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, NS, KW, PIPE, LDR>), grid, gb, 0, s, k);
+        hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, NS, KW>), grid, gb, 0, s, k);
       else
-        hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, KW, PIPE, LDR>), grid, gb, 0, s, k);
+        hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, KW>), grid, gb, 0, s, k);
       return;
     }
   }
@@ -1159,23 +902,19 @@ void launch(hipStream_t s, const GemmDesc &d) {
 }
 
 template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const GemmDesc &d) {
-  static const int pf_big = env_int("LBF_GEMM_PF", 2), pf_small = env_int("LBF_GEMM_PF_SMALL", 2);
-  // LDS-DMA stages: as many tile buffers as fit two workgroups per CU (80 KB each)
+  // LDS-DMA stages: as many tile buffers as fit two workgroups per CU (80 KB each); the register-staged
+  // fallback (gathered mn-contiguous operands, odd shapes) keeps two k-tiles of loads in flight
   if (d.tile == TILE_32x128) { // 32 x 128 (20 KB per stage), one 8-wave workgroup (two k-groups) per CU
-    // (six stages measured no faster: profiles/r02/small_tile_variants.txt)
-    // (PIPE / LDR variants measured no faster: profiles/r02/gemm_small_tiles.txt; these tiles are bound by
-    // the per-CU operand delivery rate, ~22 GB/s per CU, not by the loop's instruction schedule)
-    if (pf_small >= 2) launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 2, 4>(s, d);
-    else launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 1, 4>(s, d);
+    // (six stages, a software-pipelined loop, dedicated loader waves and a direct-from-L2 operand path all
+    // measured no faster: profiles/r02/gemm_small_tiles.txt, profiles/r03/bench_7500_direct.json; these
+    // tiles are bound by the per-CU operand delivery rate, ~22 GB/s per CU)
+    launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 2, 4>(s, d);
   } else if (d.tile == TILE_64x128) { // 64 x 128 (24 KB per stage), two workgroups per CU
-    if (pf_small >= 2) launch<2, 2, 1, 2, AKC, BKC, EPI, 1, 2, 3>(s, d);
-    else launch<2, 2, 1, 2, AKC, BKC, EPI, 1, 1, 3>(s, d);
+    launch<2, 2, 1, 2, AKC, BKC, EPI, 1, 2, 3>(s, d);
   } else if (d.tile == TILE_64x64) { // 64 x 64 (16 KB per stage)
-    if (pf_small >= 2) launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 2, 5>(s, d);
-    else launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 1, 5>(s, d);
+    launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 2, 5>(s, d);
   } else if (d.N > 64) { // 128 x 128 (32 KB per stage)
-    if (pf_big >= 2) launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 2, 2>(s, d);
-    else launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 1, 2>(s, d);
+    launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 2, 2>(s, d);
   } else if (d.N > 32) launch<2, 2, 2, 1, AKC, BKC, EPI, 1, 1, 3>(s, d); // 128 x 64 (24 KB per stage)
   else launch<4, 1, 1, 1, AKC, BKC, EPI, 1, 1, 3>(s, d);                 // 128 x 32 (20 KB per stage)
 }
@@ -1216,14 +955,6 @@ long long gemm_tiles(const GemmDesc &d) {
 
 void gemm(hipStream_t s, const GemmDesc &d) {
   if (d.M <= 0 || d.N <= 0) return;
-  if (d.fin_cnt) {
-    const long long bytes = (long long)(d.splits > 1 ? d.splits : 1) * d.slab_stride * 4;
-    if (d.epi != EPI_STORE || d.splits < 2 || d.N % 4 || d.ldc != d.N || !d.fin_out || !aligned16(d.C) ||
-        !aligned16(d.fin_out) || (d.bias && !aligned16(d.bias)) || d.slab_stride % 4 || bytes >= (1LL << 31) ||
-        d.side_slab)
-      throw std::runtime_error("gemm: in-launch split-K reduction needs EPI_STORE, >= 2 splits, N % 4 == 0, "
-                               "dense aligned slabs under 2 GiB, no side job");
-  }
   if (d.epi == EPI_HEAD) {
     int BM, BN;
     gemm_tile_for(d.N, d.tile, &BM, &BN);

@@ -198,15 +198,16 @@ void head_fused(hipStream_t s, const float *A, int H, const float *P, int Out, c
                 long long B, int act_out, int act_prev, double inv_scale, float *delta, float *slab,
                 double *sse_part, const int *abort) {
   const size_t shmem = size_t(smem_floats(H)) * sizeof(float);
-  static bool set = false;
-  if (!set) {
+  // once per process, thread-safe (rank threads of an in-process group launch concurrently)
+  static const bool attr_set = [] {
     const void *fns[] = {reinterpret_cast<const void *>(head_kernel<1>), reinterpret_cast<const void *>(head_kernel<2>),
                          reinterpret_cast<const void *>(head_kernel<3>), reinterpret_cast<const void *>(head_kernel<4>),
                          reinterpret_cast<const void *>(head_kernel<5>)};
     for (const void *f : fns)
       LBF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048));
-    set = true;
-  }
+    return true;
+  }();
+  (void)attr_set;
   const dim3 grid(head_nwg(B, H)), block(256);
 #define LBF_HEAD_LAUNCH(Q)                                                                                    \
   hipLaunchKernelGGL(head_kernel<Q>, grid, block, shmem, s, A, H, P, Out, Y, idx, B, act_out, act_prev, inv_scale, \

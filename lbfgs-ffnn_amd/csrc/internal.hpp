@@ -1,4 +1,4 @@
-// Internal runtime support for liblbfgs_amd.so: error type, HIP checks, RAII device buffers.
+// Internal runtime support for liblbfgs_amd_abi3.so: error type, HIP checks, RAII device buffers.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -96,11 +96,8 @@ inline int env_int(const char *name, int dflt) {
 // Extra flags for the library's events: every event orders work on ONE device (profiling marks, the
 // S-LBFGS twin's fork / join), so a device-scope release is enough. The default system-scope release writes
 // back and invalidates the caches at each record, which costs the recording stream time and leaves the next
-// kernel with a cold L2 (LBF_EVENT_SYSTEM_RELEASE=1 restores it).
-inline unsigned event_release_flags() {
-  static const unsigned f = env_int("LBF_EVENT_SYSTEM_RELEASE", 0) ? 0u : unsigned(hipEventReleaseToDevice);
-  return f;
-}
+// kernel with a cold L2.
+inline unsigned event_release_flags() { return unsigned(hipEventReleaseToDevice); }
 
 // Phase timestamps for kernel tuning (debug build only: make ktrace). KT(slot) stores the 100 MHz
 // wall clock from thread 0 of block (0,0,0); lbf_dbg_ktrace() copies the slots to the host.

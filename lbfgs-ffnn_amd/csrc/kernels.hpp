@@ -69,18 +69,7 @@ struct GemmDesc {
   // accumulated in the epilogue and written in front of the head's rows: the slab per workgroup is
   // then [(head_fold + 1) x N | (N+1) x head_out], and the dW GEMM covers rows < head_fold_c0 only.
   int head_fold = -1, head_fold_c0 = 0;
-  // In-launch split-K reduction (EPI_STORE with splits > 1, N % 4 == 0): every split stores its slab
-  // tile write-through (sc1) and adds to fin_cnt[tile]; the split that arrives last sums the tile's
-  // slabs in split order (bitwise fwd_reduce_act), adds the bias, applies `act` and writes fin_out
-  // ([M][N]). fin_cnt: one zeroed word per output tile (the last arrival re-zeroes its own).
-  unsigned *fin_cnt = nullptr;
-  float *fin_out = nullptr;
-  // 32 x 128 tiles with a k-contiguous A and mn-contiguous B: the direct-operand kernel (operands from L2
-  // straight into registers) instead of the LDS-DMA one; bitwise the same results
-  bool direct = false;
 };
-// Output tiles of a GEMM launch (the fin_cnt words it needs)
-long long gemm_tiles(const GemmDesc &d);
 // Row tiles of the forward GEMM for M rows and N columns (== EPI_HEAD partial slabs).
 int gemm_row_tiles(int M, int tile);
 
@@ -354,12 +343,10 @@ struct TailArgs {
   double *dots = nullptr; // [nc]
   int tcg0[RA_MAXSEG] = {}; // first TAIL_COLS column group of each segment
   int nb = 0, nc = 0;       // nb: TAIL_COLS column groups over all segments (one block each)
-  // Non-null: the last tail_cols block to finish (arrival counter, zero between launches) runs
-  // tail_fin's body itself, and tail_fin() must not be launched.
+  // Arrival counter (zero between launches): the last tail_cols block to finish runs the one-block fin.
   unsigned *cols_done = nullptr;
 };
-void tail_reduce(hipStream_t s, const TailArgs &a); // tail_reduce + tail_cols (+ fin) launches
-void tail_fin(hipStream_t s, const TailArgs &a);    // one block
+void tail_reduce(hipStream_t s, const TailArgs &a); // tail_reduce + tail_cols_fin launches
 int tail_vpw(int m);                                // vectors per wave of the Gram sweep (0: unsupported)
 
 // S-LBFGS history update in two launches (dir.hip): a one-round-trip Gram sweep of the new s / y / g
@@ -385,16 +372,6 @@ struct DirArgs {
   double *dots = nullptr;   // [dir_ncols(m)]
   int nb = 0;               // cdiv(n, dir_cols_per_block(m, n))
   unsigned *cols_done = nullptr; // arrival counter, zero between launches
-  // The direction's linear-combination sweep in the same launch (dir_fin, want_dir == 1): ncb blocks after
-  // the column blocks load their elements of g, x_in and every ring slot up front, wait for the last
-  // column block to publish the step's order and coefficients (cmb_desc, then cmb_flag = 1), and
-  // combine (combine_small's arithmetic); the last worker to have read the descriptor re-zeroes the flag
-  // and cmb_done for the next launch (so a replayed graph needs no fresh arguments). ncb = 0: no combine
-  // (a separate hist_combine follows).
-  CombineArgs cmb;
-  int ncb = 0;
-  unsigned *cmb_flag = nullptr; // [2]: the publish flag, the workers' arrival count; zero between launches
-  double *cmb_desc = nullptr;   // [2 + 3 slots]: k, slot of logical i, cs_i, cy_i, cg
 };
 bool dir_supported(int m, long long n);
 int dir_cols_per_block(int m, long long n);

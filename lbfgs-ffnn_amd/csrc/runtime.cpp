@@ -22,28 +22,11 @@ Profiler::~Profiler() {
 
 size_t Profiler::mark(hipStream_t s) {
   if (used == pool.size()) {
-    LBF_REQUIRE(!capture, "profiler: event pool exhausted inside a graph capture");
     hipEvent_t e;
     LBF_HIP(hipEventCreateWithFlags(&e, hipEventDefault | event_release_flags()));
     pool.push_back(e);
   }
-  if (capture) {
-    // an event-record node of the graph being captured, appended behind the stream's current capture
-    // dependencies and made the new one (hipEventRecordWithFlags(..., hipEventRecordExternal) is refused
-    // inside a capture by this ROCm)
-    hipStreamCaptureStatus st;
-    hipGraph_t g = nullptr;
-    const hipGraphNode_t *deps = nullptr;
-    size_t ndeps = 0;
-    LBF_HIP(hipStreamGetCaptureInfo_v2(s, &st, nullptr, &g, &deps, &ndeps));
-    LBF_REQUIRE(st == hipStreamCaptureStatusActive && g, "profiler: stream not capturing");
-    hipGraphNode_t node;
-    LBF_HIP(hipGraphAddEventRecordNode(&node, g, deps, ndeps, pool[used]));
-    LBF_HIP(hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies));
-  } else {
-    LBF_HIP(hipEventRecord(pool[used], s));
-  }
-  ++marks;
+  LBF_HIP(hipEventRecord(pool[used], s));
   return used++;
 }
 
@@ -70,43 +53,6 @@ void Profiler::resolve() {
   used = 0;
 }
 
-void Profiler::capture_begin(long long reserve) {
-  resolve();
-  while ((long long)pool.size() < reserve) {
-    hipEvent_t e;
-    LBF_HIP(hipEventCreateWithFlags(&e, hipEventDefault | event_release_flags()));
-    pool.push_back(e);
-  }
-  capture = true;
-}
-
-GraphProf Profiler::capture_end() {
-  capture = false;
-  GraphProf g;
-  g.ev.assign(pool.begin(), pool.begin() + long(used));
-  g.recs = recs;
-  pool.erase(pool.begin(), pool.begin() + long(used));
-  recs.clear();
-  used = 0;
-  return g;
-}
-
-void Profiler::add_graph(const GraphProf &g) {
-  if (g.recs.empty()) return;
-  LBF_HIP(hipEventSynchronize(g.ev.back()));
-  for (const auto &r : g.recs) {
-    float t = 0.f;
-    LBF_HIP(hipEventElapsedTime(&t, g.ev[r.a], g.ev[r.b]));
-    add(r, t);
-  }
-}
-
-void GraphProf::release() {
-  for (auto e : ev) (void)hipEventDestroy(e);
-  ev.clear();
-  recs.clear();
-}
-
 void Profiler::merge_into(Profiler &dst) {
   resolve();
   if (dst.ms.size() < ms.size()) {
@@ -127,7 +73,7 @@ void Profiler::merge_into(Profiler &dst) {
 void Ctx::set_device() const { LBF_HIP(hipSetDevice(device)); }
 
 void Ctx::allreduce(float *buf, size_t count) {
-  if (!comm) return;
+  if (!dp()) return;
   comm->allreduce(buf, count, stream);
 }
 
@@ -149,16 +95,7 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
     layers_.push_back(L);
   }
   nparams_ = off;
-  const char *nh = std::getenv("LBF_NO_HEAD");
-  use_head_ = !(nh && nh[0] == '1');
-  const char *ng = std::getenv("LBF_NO_GEMM_HEAD");
-  use_gemm_head_ = !(ng && ng[0] == '1');
-  if (const char *e = std::getenv("LBF_FWD_TILE32")) fwd_small_ = e[0] != '0';
-  if (const char *e = std::getenv("LBF_DW_TILE64")) dw64_ = e[0] != '0';
-  if (const char *e = std::getenv("LBF_NO_FOLD")) fold_on_ = e[0] != '1';
-  tail_split_ = env_int("LBF_TAIL_SPLIT", 0) != 0; // 1: tail_fin as its own launch (A/B and tests)
-  gemm_direct_ = env_int("LBF_GEMM_DIRECT", 0) != 0; // measured slower (profiles/r03/bench_7500_direct.json)
-  fwd_fin_ = env_int("LBF_FWD_FIN", 0) != 0; // measured slower at S-LBFGS minibatches (profiles/r03)
+  if (const char *e = std::getenv("LBF_NO_FOLD")) fold_on_ = e[0] != '1'; // tests: the unfolded route
 }
 
 // Split-K factor for `tiles` output tiles over a K of `K` rows: the GEMM tiles run two workgroups per
@@ -193,7 +130,7 @@ void Mlp::plan(long long B) {
   if (planned_ == B) return;
   size_t slab = 0, fslab = 0;
   const int nl = int(layers_.size());
-  const bool fused = use_head_ && nl >= 2 && head_supported(layers_[nl - 1].in, layers_[nl - 1].out);
+  const bool fused = nl >= 2 && head_supported(layers_[nl - 1].in, layers_[nl - 1].out);
   const long long slots = 2LL * ctx_->cus;
   for (auto &L : layers_) {
     // forward GEMM: with fewer row tiles than CUs (a data-parallel rank's shard), split K so the chip
@@ -219,11 +156,11 @@ void Mlp::plan(long long B) {
       const long long n = cdiv(cdiv(B, bm), cus);
       return double(n) * per_ktile * double(nkt) + double(cdiv(n, per_round)) * epi;
     };
-    if (fwd_small_ && L.out > 64 && L.out <= 128) {
+    if (L.out > 64 && L.out <= 128) {
       const double t32 = est_us(32, 0.93, 1, 8.0), t64 = est_us(64, 1.25, 2, 12.0), t128 = est_us(128, 2.3, 2, 20.0);
       if (t32 <= t64 && t32 <= t128) L.ftile = TILE_32x128; // full rows (the head can still fuse), no split
       else if (t64 <= t128) L.ftile = TILE_64x128;
-    } else if (fwd_small_ && L.out <= 64 && cdiv(B, 128) < 256) {
+    } else if (L.out <= 64 && cdiv(B, 128) < 256) {
       L.ftile = TILE_32x128;
     }
     if (L.ftile != TILE_AUTO) {
@@ -234,7 +171,7 @@ void Mlp::plan(long long B) {
       // workgroup per CU) and the slabs are a quarter of the bytes of 128 x 128 tiles at the same count.
       const long long tiles32 = cdiv(B, 32) * cdiv(L.out, 128);
       long long fs;
-      if (fwd_small_ && 2 * tiles32 <= cus) {
+      if (2 * tiles32 <= cus) {
         L.ftile = TILE_32x128;
         fs = std::max(2LL, std::min(cus / tiles32, cdiv(L.in, 64))); // splits of >= 2 k-tiles
       } else {
@@ -252,8 +189,7 @@ void Mlp::plan(long long B) {
     // (only for short K: at long K the 128x128 tile's reuse wins over the slab savings). Small batches
     // (S-LBFGS minibatches, K = 128 / 256 rows) take 64x64 tiles at any width: four times the tiles of
     // 128x128 at the same K, where 128x128 tiles filled a fifth of the chip (784 -> 512: 56 workgroups).
-    L.dtile = (dw64_ && ((L.out <= 128 && L.in + 1 <= 1024 && B <= 16384) || B <= DW_SMALL_BATCH)) ? TILE_64x64
-                                                                                                 : TILE_AUTO;
+    L.dtile = ((L.out <= 128 && L.in + 1 <= 1024 && B <= 16384) || B <= DW_SMALL_BATCH) ? TILE_64x64 : TILE_AUTO;
   }
   // The last hidden layer's dW GEMM has in + 1 rows; when they pass a multiple of its tile height by
   // at most 16 input columns + the bias row (784 + 1 = 6 x 128 + 17 at cfg 2), those rows go to the
@@ -287,9 +223,7 @@ void Mlp::plan(long long B) {
       if (fold_ >= 0 && l == nl - 2) cols += (long long)(fold_ + 1) * L.out;
       side = cdiv(cdiv(cols, 256), tiles) * tiles; // gemm.hip SIDE_COLS per side block
     }
-    static const int legacy = env_int("LBF_SPLIT_LEGACY", 0);
-    long long splits = legacy ? std::max(1LL, std::min(cdiv(512, tiles), cdiv(B, min_chunk)))
-                              : split_factor(tiles, B, min_chunk, std::max(slots - side, slots / 2), M * L.out);
+    long long splits = split_factor(tiles, B, min_chunk, std::max(slots - side, slots / 2), M * L.out);
     long long kc = cdiv(cdiv(B, splits), 32) * 32;
     if (kc <= 0) kc = 32;
     splits = std::max(1LL, cdiv(B, kc));
@@ -322,7 +256,7 @@ int Mlp::dx_tile(long long B, int N) const {
 
 bool Mlp::gemm_head_on() const {
   const int nl = int(layers_.size());
-  if (!(use_head_ && use_gemm_head_ && nl >= 2)) return false;
+  if (nl < 2) return false;
   const Layer &Lo = layers_[size_t(nl - 1)];
   return head_supported(Lo.in, Lo.out) && layers_[size_t(nl - 2)].fsplits == 1 && Lo.in <= 128;
 }
@@ -384,7 +318,6 @@ GemmDesc Mlp::fwd_desc(size_t l, const float *P, const float *in, const int *idx
   d.act = L.act;
   d.abort = ctx_->abort;
   d.tile = L.ftile;
-  d.direct = gemm_direct_;
   return d;
 }
 
@@ -402,25 +335,11 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
       d.splits = L.fsplits;
       d.k_chunk = L.fk_chunk;
       d.slab_stride = B * L.out;
-      // the slabs summed inside the launch by each tile's last split (no fwd_reduce_act launch)
-      const bool fin = fwd_fin_ && L.out % 4 == 0 && (B * L.out) % 4 == 0 &&
-                       (long long)L.fsplits * B * L.out * 4 < (1LL << 31);
-      if (fin) {
-        const size_t tiles = size_t(gemm_tiles(d));
-        if (fin_cnt_.size() < tiles) {
-          fin_cnt_.resize(tiles);
-          LBF_HIP(hipMemsetAsync(fin_cnt_.get(), 0, tiles * sizeof(unsigned), s));
-        }
-        d.fin_cnt = fin_cnt_.get();
-        d.fin_out = A_[l].get();
-      }
-      static const int poison = env_int("LBF_DBG_POISON_FSLAB", 0); // debug: unwritten slab entries read as NaN
-      if (poison)
-        LBF_HIP(hipMemsetAsync(fslab_.get(), 0xff, size_t(L.fsplits) * size_t(B) * L.out * sizeof(float), s));
+      // (an in-launch reduction by each tile's last split measured slower: the reducer's serial slab read
+      // lengthened the GEMM more than the launch it saved, profiles/r03/bench_cfg4_*_fin.json)
       ProfScope ps(ctx_, PK_FWD, int(l), double(B));
       gemm(s, d);
-      if (!fin)
-        fwd_reduce_act(s, fslab_.get(), L.fsplits, B * L.out, int(B), L.out, d.bias, L.act, A_[l].get(), ctx_->abort);
+      fwd_reduce_act(s, fslab_.get(), L.fsplits, B * L.out, int(B), L.out, d.bias, L.act, A_[l].get(), ctx_->abort);
     } else {
       ProfScope ps(ctx_, PK_FWD, int(l), double(B));
       gemm(s, d);
@@ -438,7 +357,7 @@ void Mlp::forward_phase(const float *P, const float *X, const float *Y, const in
   hipStream_t s = ctx_->stream;
   const int nl = int(layers_.size());
   const Layer &Lo = layers_[nl - 1];
-  const bool fused = use_head_ && nl >= 2 && head_supported(Lo.in, Lo.out);
+  const bool fused = nl >= 2 && head_supported(Lo.in, Lo.out);
   ensure(B);
   // the output layer inside the last hidden layer's forward GEMM (EPI_HEAD), when that GEMM is one
   // unsplit tile column: its activations then never reach HBM
@@ -745,20 +664,14 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     tdots_.ensure(size_t(ta.nc));
     ta.rows = trows_.get();
     ta.dots = tdots_.get();
-    if (!tail_split_) {
-      if (!cols_done_.get()) {
-        cols_done_.resize(1);
-        LBF_HIP(hipMemsetAsync(cols_done_.get(), 0, sizeof(unsigned), s));
-      }
-      ta.cols_done = cols_done_.get();
+    if (!cols_done_.get()) {
+      cols_done_.resize(1);
+      LBF_HIP(hipMemsetAsync(cols_done_.get(), 0, sizeof(unsigned), s));
     }
+    ta.cols_done = cols_done_.get();
     {
       ProfScope ps(ctx_, PK_GRAM, 1);
-      tail_reduce(s, ta); // + tail_fin in the last tail_cols block (cols_done)
-    }
-    if (tail_split_) {
-      ProfScope ps(ctx_, PK_COEF, 1);
-      tail_fin(s, ta);
+      tail_reduce(s, ta); // + the fin in the last tail_cols block (cols_done)
     }
     ++evals_;
     rows_ += B;
@@ -1069,19 +982,13 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
   // the ring vectors are only ever read for live slots, but keep them defined
   LBF_HIP(hipMemsetAsync(S_.get(), 0, S_.size() * sizeof(float), ctx_->stream));
   LBF_HIP(hipMemsetAsync(Y_.get(), 0, Y_.size() * sizeof(float), ctx_->stream));
-  dir_on_ = dir_supported(m, n) && env_int("LBF_DIR_FUSED", 1) != 0;
+  dir_on_ = dir_supported(m, n);
   if (dir_on_) {
     const int nb = int(cdiv(n, dir_cols_per_block(m, n)));
     drows_.resize(size_t(dir_ncols(m)) * size_t(nb));
     ddots_.resize(size_t(dir_ncols(m)));
     dcount_.resize(1);
     LBF_HIP(hipMemsetAsync(dcount_.get(), 0, sizeof(unsigned), ctx_->stream));
-    // opt-in: measured slower (profiles/r03b/README.md: the merged launch ran 70 us per step against
-    // 16 + 12 us for the two it replaces; the 2094 waiting blocks slow the column sums and the step)
-    dir_combine_ = env_int("LBF_DIR_COMBINE", 0) != 0;
-    cflag_.resize(2);
-    cdesc_.resize(size_t(2 + 3 * slots));
-    LBF_HIP(hipMemsetAsync(cflag_.get(), 0, 2 * sizeof(unsigned), ctx_->stream));
   }
   gfin_on_ = gram_fin_supported(m) && env_int("LBF_GRAM_FIN", 1) != 0;
   if (gfin_on_) {
@@ -1171,48 +1078,10 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
 
 void History::update_combine(const GramArgs &g0, int iter, double dsign, const float *x_in, float *x_out,
                              float *x_out2, double alpha) {
-  GramArgs g = g0;
-  g.h = v_;
-  g.h.abort = ctx_->abort;
-  auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
-  const bool aligned = al16(g.sa) && al16(g.sb) && al16(g.ya) && al16(g.yb) && al16(g.ga) && al16(g.gb) &&
-                       al16(g.gc) && al16(g.g_out);
-  const long long nb_c = cdiv(v_.n, 256);
-  if (!(dir_on_ && dir_combine_ && aligned && g.policy == POL_SLBFGS && g.has_g && g.g_out && !g.reset &&
-        v_.m <= DIR_MAXM && nb_c <= (1LL << 20))) {
-    update(g0, 1, iter, dsign);
-    combine(g0.g_out, nullptr, x_in, x_out, x_out2, false, alpha);
-    return;
-  }
-  hipStream_t s = ctx_->stream;
-  DirArgs d;
-  d.g = g;
-  d.want_dir = 1;
-  d.iter = iter;
-  d.dsign = dsign;
-  d.rows = drows_.get();
-  d.dots = ddots_.get();
-  d.nb = int(cdiv(v_.n, dir_cols_per_block(v_.m, v_.n)));
-  d.cols_done = dcount_.get();
-  CombineArgs &c = d.cmb;
-  c.h = v_;
-  c.h.abort = ctx_->abort;
-  c.g = g0.g_out;
-  c.dir = nullptr;
-  c.x_in = x_in;
-  c.x_out = x_out;
-  c.x_out2 = x_out2;
-  c.alpha_from_state = 0;
-  c.alpha = alpha;
-  d.ncb = int(nb_c);
-  d.cmb_flag = cflag_.get();
-  d.cmb_desc = cdesc_.get();
-  {
-    ProfScope ps(ctx_, PK_GRAM);
-    dir_sweep(s, d);
-  }
-  ProfScope ps(ctx_, PK_COEF);
-  dir_fin(s, d);
+  // (the combine inside the column-sum launch measured slower: its waiting blocks slowed the column sums
+  // and the one-block step, profiles/r03b/README.md)
+  update(g0, 1, iter, dsign);
+  combine(g0.g_out, nullptr, x_in, x_out, x_out2, false, alpha);
 }
 
 void History::combine(const float *g, float *dir, const float *x_in, float *x_out, float *x_out2,

@@ -1,4 +1,4 @@
-// Host runtime of liblbfgs_amd.so: context (device, stream, RCCL communicator), the MLP evaluation
+// Host runtime of liblbfgs_amd_abi3.so: context (device, stream, RCCL communicator), the MLP evaluation
 // plan, the device-resident L-BFGS history, and the solver drivers.
 #pragma once
 
@@ -15,20 +15,11 @@ namespace lbf {
 enum ProfKind : int { PK_FWD = 0, PK_DW = 1, PK_DX = 2, PK_LOSS = 3, PK_SLAB = 4, PK_FINAL = 5, PK_GRAM = 6,
                       PK_COEF = 7, PK_COMBINE = 8, PK_AXPY = 9, PK_ALLREDUCE = 10 };
 struct ProfRec { int id; size_t a, b; double work; };
-// Timed sections captured into a hipGraph: event-record nodes on events the graph owns, read after each
-// replay (Profiler::add_graph).
-struct GraphProf {
-  std::vector<hipEvent_t> ev;
-  std::vector<ProfRec> recs;
-  void release();
-};
 struct Profiler {
   bool on = false;
   int only = -1; // section filter (-1: all)
   int every = 1;  // sample every k-th launch of a wanted section
   long long seen = 0;
-  long long marks = 0;    // events recorded so far (sizes a capture's event pool)
-  bool capture = false;   // marks are external event-record nodes of the graph being captured
   bool want(int id) {
     if (!on || (only >= 0 && only != id)) return false;
     return every <= 1 || (seen++ % every) == 0;
@@ -45,11 +36,6 @@ struct Profiler {
   void resolve();
   void merge_into(Profiler &dst); // resolve this one and add its totals to dst's
   void add(const Rec &r, float t);
-  // Capture: resolve, then (capture_begin) create `reserve` events up front (no event creation inside the
-  // capture) and record the marks as graph nodes; capture_end hands the events and records to the graph.
-  void capture_begin(long long reserve);
-  GraphProf capture_end();
-  void add_graph(const GraphProf &g); // after a replay has completed
 };
 
 struct Ctx {
@@ -61,6 +47,8 @@ struct Ctx {
   std::unique_ptr<Comm> comm; // RCCL (lbf_comm_init) or an in-process rank group (lbf_comm_init_local)
   int rank = 0, nranks = 1;
   const int *abort = nullptr; // set by a solver while it runs speculatively (see LbfgsSolver)
+  // evaluate as a single rank although a communicator exists (replicated S-LBFGS inner steps, LocalOnly)
+  bool local_only = false;
   // scratch for the BLAS-1 ABI helpers
   DevBuf<double> part, red;
   PinnedBuf<double> host;
@@ -68,8 +56,18 @@ struct Ctx {
   void set_device() const;
   // data-parallel evaluation path: taken whenever a communicator exists, including a 1-rank one
   // (lbf_comm_init(ctx, 1, 0, id)), which is how the RCCL path is exercised on a single GPU
-  bool dp() const { return comm != nullptr; }
+  bool dp() const { return comm != nullptr && !local_only; }
   void allreduce(float *buf, size_t count);
+};
+
+// Scoped Ctx::local_only (when `on`).
+struct LocalOnly {
+  Ctx *c;
+  bool prev;
+  LocalOnly(Ctx *ctx, bool on) : c(ctx), prev(ctx->local_only) {
+    if (on) c->local_only = true;
+  }
+  ~LocalOnly() { c->local_only = prev; }
 };
 
 // Fused optimizer tail request (speculative L-BFGS fast path, tail.hip): the pair inputs, the
@@ -164,10 +162,6 @@ public:
     evals_ -= k;
     rows_ -= k * B;
   }
-  void add_counts(long long evals, long long rows) { // evaluations a replayed graph ran
-    evals_ += evals;
-    rows_ += rows;
-  }
 
 private:
   void forward_phase(const float *P, const float *X, const float *Y, const int *idx, long long B, double inv_scale);
@@ -190,17 +184,7 @@ private:
   long long cap_ = -1, planned_ = -1;
   std::vector<DevBuf<float>> A_, D_;
   DevBuf<float> slab_, head_slab_, fslab_;
-  // arrival counters of the forward GEMMs' in-launch split-K reduction (GemmDesc::fin_cnt), one per
-  // output tile; each launch leaves them zero
-  DevBuf<unsigned> fin_cnt_;
-  bool gemm_direct_ = false; // LBF_GEMM_DIRECT=1: gemm_direct_kernel for the 32 x 128 forward tiles (opt-in)
-  bool fwd_fin_ = false; // LBF_FWD_FIN=1: in-launch reduction (the reducer's serial slab read costs more than the launch it saves)
-  bool use_head_ = true;      // fused output layer when the shape allows (LBF_NO_HEAD=1 disables)
-  bool use_gemm_head_ = true; // ... inside the forward GEMM's epilogue (LBF_NO_GEMM_HEAD=1 disables)
-  int fwd_small_ = 1;         // 32x128 forward tiles for few row tiles (LBF_FWD_TILE32=0 disables)
-  int dw64_ = 1;              // 64x64 dW tiles with fewer splits (LBF_DW_TILE64=0 disables)
-  bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1 disables)
-  bool tail_split_ = false;   // tail_fin as a separate launch (LBF_TAIL_SPLIT=1)
+  bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1: the unfolded route, tests)
   // Planned fold: the last hidden layer's [dW ; db] rows fold_c0_ .. in (fold_ input columns and the
   // bias row) are computed in the forward GEMM's EPI_HEAD epilogue instead of a mostly empty last
   // row tile of its dW GEMM; fold_ = -1: none.
@@ -230,9 +214,7 @@ public:
   void update(const GramArgs &g, int want_dir, int iter, double dsign);
   void combine(const float *g, float *dir, const float *x_in, float *x_out, float *x_out2, bool alpha_from_state,
                double alpha);
-  // update(g, 1, iter, dsign) then combine(g.g_out, nullptr, x_in, x_out, x_out2, false, alpha); with
-  // LBF_DIR_COMBINE=1 on the fused S-LBFGS route the combine runs inside the column-sum launch (dir.hip;
-  // measured slower, off by default)
+  // update(g, 1, iter, dsign) then combine(g.g_out, nullptr, x_in, x_out, x_out2, false, alpha)
   void update_combine(const GramArgs &g, int iter, double dsign, const float *x_in, float *x_out, float *x_out2,
                       double alpha);
   double *scal() const { return v_.scal; }
@@ -248,10 +230,6 @@ private:
   DevBuf<double> drows_, ddots_;
   DevBuf<unsigned> dcount_;
   bool dir_on_ = false;
-  // in-launch combine: publish flag + worker arrival count (zero between launches), order / coefficients
-  DevBuf<unsigned> cflag_;
-  DevBuf<double> cdesc_;
-  bool dir_combine_ = false;
   // unfused path: Gram sweep (transposed partials in part_) + column sums whose last block runs the step
   DevBuf<double> gdots_;
   DevBuf<unsigned> gcount_;

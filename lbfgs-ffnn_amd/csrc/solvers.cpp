@@ -18,35 +18,6 @@ namespace {
 long long round4(long long n) { return cdiv(n, 4) * 4; }
 } // namespace
 
-MinibatchSampler::MinibatchSampler(size_t N) : perm_(N) { std::iota(perm_.begin(), perm_.end(), size_t(0)); }
-
-size_t MinibatchSampler::draw(size_t b, std::mt19937 &rng, std::vector<int> &out) {
-  // s_lbfgs.hpp:141-160: partial Fisher-Yates over iota(N), uniform_int_distribution<size_t>(i, N-1).
-  const size_t N = perm_.size();
-  if (N == 0 || b == 0) return 0;
-  if (b >= N) { // the whole identity, no draws
-    for (size_t i = 0; i < N; ++i) out.push_back(int(i));
-    return N;
-  }
-  touched_.resize(b);
-  for (size_t i = 0; i < b; ++i) {
-    std::uniform_int_distribution<size_t> dist(i, N - 1);
-    const size_t j = dist(rng);
-    touched_[i] = j;
-    std::swap(perm_[i], perm_[j]);
-  }
-  for (size_t i = 0; i < b; ++i) out.push_back(int(perm_[i]));
-  for (size_t i = b; i-- > 0;) std::swap(perm_[i], perm_[touched_[i]]); // undo in reverse: identity again
-  return b;
-}
-
-std::vector<size_t> sample_minibatch(size_t N, size_t b, std::mt19937 &rng) {
-  MinibatchSampler smp(N);
-  std::vector<int> v;
-  smp.draw(b, rng, v);
-  return std::vector<size_t>(v.begin(), v.end());
-}
-
 // ================================================================================================
 // Full-batch L-BFGS
 // ================================================================================================
@@ -588,17 +559,16 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
   hs_.ensure(SC_N);
   evals0_ = net->evals();
   rows0_ = net->rows();
-  anchor_pre_ = env_int("LBF_SLBFGS_ANCHOR", 0) != 0; // the twin measured ~2-3 % faster (profiles/r03)
-  free_twin_ = env_int("LBF_SLBFGS_TWIN_FREE", 1) != 0;
   rng_.seed(prm.seed);
   sampler_.reset(new MinibatchSampler(size_t(N)));
-  // epoch graphs (LBF_SLBFGS_GRAPH=1; off by default): not with a communicator (the collectives stay eager)
-  // nor with the synchronous pair trace. Measured slower than the eager epochs on ROCm 7.2
-  // (profiles/r03b/README.md): hipGraphLaunch spends about as much host time per node as an eager launch
-  // (≈ 20 ms per cfg-4 epoch), and the replay runs every node on one queue, so the twin's anchor
-  // gradients no longer overlap the context stream's chain (kernel trace: 5503 launches on one stream).
-  graph_on_ = env_int("LBF_SLBFGS_GRAPH", 0) != 0 && !ctx_->dp() && !prm.pair_trace;
-  if (env_int("LBF_SLBFGS_TWIN", 1)) {
+  repl_ = ctx_->dp() && prm.dp_mode == LBF_SLBFGS_DP_REPLICATED;
+  LBF_REQUIRE(prm.dp_mode == LBF_SLBFGS_DP_REPLICATED || prm.dp_mode == LBF_SLBFGS_DP_SLICED, "dp_mode 0 / 1");
+  // Twin evaluator (see tnet_). Epoch hipGraphs of both streams were built and measured slower on ROCm
+  // 7.2: hipGraphLaunch spends about as much host time per node as an eager launch, and the replay runs
+  // every node on one queue, so the twin's anchor gradients stopped overlapping the context stream's chain
+  // (profiles/r03b/cfg4_graph*). Precomputing an epoch's anchor gradients in one evaluation measured no
+  // faster than the twin (profiles/r03/bench_cfg4_{pre,twin}_*.json).
+  {
     tctx_.reset(new Ctx());
     tctx_->device = ctx_->device;
     tctx_->cus = ctx_->cus;
@@ -620,77 +590,25 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
       LBF_HIP(hipEventCreateWithFlags(&ev_g2_[i], hipEventDisableTiming | event_release_flags()));
       LBF_HIP(hipEventCreateWithFlags(&ev_free_[i], hipEventDisableTiming | event_release_flags()));
     }
-    if (env_int("LBF_SLBFGS_TWIN_THREAD", 1)) {
-      tw_.reset(new TwinWorker());
-      TwinWorker *w = tw_.get();
-      const int dev = ctx_->device;
-      w->th = std::thread([w, dev]() {
-        const bool dev_ok = hipSetDevice(dev) == hipSuccess;
-        for (;;) {
-          std::function<void()> f;
-          {
-            std::unique_lock<std::mutex> lk(w->mu);
-            w->cv.wait(lk, [w] { return w->stop || !w->q.empty(); });
-            if (w->q.empty()) return; // stop requested and nothing left
-            f = std::move(w->q.front());
-            w->q.pop_front();
-          }
-          try {
-            if (!dev_ok) throw Error(2, "twin thread: hipSetDevice failed");
-            bool failed;
-            {
-              std::lock_guard<std::mutex> lk(w->mu);
-              failed = w->err != nullptr;
-            }
-            if (!failed) f(); // after an error the rest is skipped (tickets still complete)
-          } catch (...) {
-            std::lock_guard<std::mutex> lk(w->mu);
-            if (!w->err) w->err = std::current_exception();
-          }
-          w->done.fetch_add(1, std::memory_order_release);
-        }
-      });
-    }
+    const int dev = ctx_->device;
+    tw_.reset(new TaskFifo([dev]() { LBF_HIP(hipSetDevice(dev)); }));
   }
 }
 
 long long SlbfgsSolver::twin_post(std::function<void()> f) {
-  if (!tw_ || tw_inline_) {
+  if (!tw_) {
     f();
     return 0;
   }
-  long long ticket;
-  {
-    std::lock_guard<std::mutex> lk(tw_->mu);
-    tw_->q.push_back(std::move(f));
-    ticket = ++tw_->posted;
-  }
-  tw_->cv.notify_one();
-  return ticket;
+  return tw_->post(std::move(f));
 }
 
 void SlbfgsSolver::twin_wait(long long ticket) {
-  if (!tw_ || ticket <= 0) return;
-  for (int spin = 0; tw_->done.load(std::memory_order_acquire) < ticket; ++spin)
-    if (spin > 64) std::this_thread::yield();
-  std::exception_ptr e;
-  {
-    std::lock_guard<std::mutex> lk(tw_->mu);
-    e = tw_->err;
-    tw_->err = nullptr;
-  }
-  if (e) std::rethrow_exception(e);
+  if (tw_) tw_->wait(ticket);
 }
 
 SlbfgsSolver::~SlbfgsSolver() {
-  if (tw_) {
-    {
-      std::lock_guard<std::mutex> lk(tw_->mu);
-      tw_->stop = true;
-    }
-    tw_->cv.notify_one();
-    if (tw_->th.joinable()) tw_->th.join();
-  }
+  tw_.reset(); // runs what is queued, joins the helper thread
   for (auto e : ev_anc_) (void)hipEventDestroy(e);
   if (ev_fork_) (void)hipEventDestroy(ev_fork_);
   if (ev_join_) (void)hipEventDestroy(ev_join_);
@@ -716,7 +634,7 @@ void SlbfgsSolver::eval_pair(const float *wa, const float *wb, float *gab, long 
   const int In = net_->layers().front().in, Out = net_->layers().back().out;
   const float *X = xg_.get() + off * In, *Y = yg_.get() + off * Out;
   float *ga = gab, *gb = gab + ng_;
-  const bool dp = ctx_->dp();
+  const bool dp = dp_inner();
   // gradients only: nobody reads a minibatch evaluation's loss or dots (scal = nullptr skips them)
   auto one = [&](Mlp *m, const float *w, float *g) {
     if (dp) m->loss_grad_local(w, g, X, Y, nullptr, count, inv_scale);
@@ -757,11 +675,12 @@ int SlbfgsSolver::run(lbf_record *rec) {
 }
 
 // An epoch's index lists in the reference's RNG order (s_lbfgs.hpp:212-266). Every rank draws the same
-// lists and keeps only its slice [b*rk/nr, b*(rk+1)/nr) of each batch. The minibatch slices come first
+// lists; with sliced data parallelism it keeps only its slice [b*rk/nr, b*(rk+1)/nr) of each batch (a
+// replicated rank keeps every index). The minibatch slices come first
 // in `flat` (minibatch t's rows right after minibatch t-1's, as Mlp::batch_grads reads them), the
 // Hessian-batch slices after them; the draws stay in RNG order.
 void SlbfgsSolver::draw_epoch(bool u_seen, EpochDraw &d) {
-  const int nr = ctx_->nranks, rk = ctx_->rank;
+  const int nr = dp_inner() ? ctx_->nranks : 1, rk = dp_inner() ? ctx_->rank : 0;
   const int m_inner = int(std::max(1LL, N_ / prm_.b));
   const int L = prm_.L;
   d.flat.clear();
@@ -818,7 +737,7 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
   const long long ld = round4(n_);
   const int m_inner = int(std::max(1LL, N_ / prm_.b));
   const int L = prm_.L;
-  const bool dp = ctx_->dp();
+  const bool dp = dp_inner();
   const auto &mb = d.mb, &hb = d.hb;
   LBF_HIP(hipMemcpyAsync(wt_.get(), w_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
   wh_head_ = 0;
@@ -828,25 +747,36 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     LBF_HIP(hipMemcpyAsync(wh_.get() + slot * ld, wt_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice,
                            s));
   }
-  // With the twin stream, the minibatch gradients at the anchor w (fixed for the epoch, and independent
-  // of the iterates) run one step ahead on it, double-buffered in the second half of gpair_[t & 1]: step
-  // t's evaluation at w_t and its direction on the context stream then overlap the twin's gradient of
-  // minibatch t + 1 at w, instead of joining the two evaluations of each step. Same evaluations on the
-  // same inputs: bitwise the same. Data parallel: both halves are this rank's partial sums until the
-  // step's one all-reduce of the whole block.
-  // Single rank (LBF_SLBFGS_TWIN_FREE, on by default): the anchor half of step t goes to its own buffer
-  // ganc_ + t ng_ (the epoch's 234 anchor gradients, 501 MB at cfg 4), so the twin never waits for the
-  // context stream to release a block: no ev_free_ record on the context stream (≈ 5 µs of its time per
-  // step, profiles/r03/launch_floor.txt) and no wait on the twin. Data parallel keeps the packed
-  // [g(w_t) | g(w)] block of one all-reduce.
-  // (within a memory budget: m_inner gradients of n floats; LBF_SLBFGS_TWIN_FREE_MB, default 4096 MB; past it
-  // the double-buffered twin)
-  static const long long free_mb = env_int("LBF_SLBFGS_TWIN_FREE_MB", 4096);
-  const bool twin_free = tnet_ && !pre_ && !dp && free_twin_ &&
-                         double(m_inner) * double(ng_) * 4.0 <= double(free_mb) * 1024.0 * 1024.0;
+  // The minibatch gradients at the anchor w (fixed for the epoch, and independent of the iterates) run one
+  // step ahead on the twin stream: step t's evaluation at w_t and its direction on the context stream then
+  // overlap the twin's gradient of minibatch t + 1 at w, instead of joining the two evaluations of each
+  // step. Same evaluations on the same inputs: bitwise the same.
+  // Free-running (no per-step collective): the anchor half of step t goes to its own buffer ganc_ + t ng_
+  // (the epoch's 234 anchor gradients, 501 MB at cfg 4), so the twin never waits for the context stream to
+  // release a block: no ev_free_ record on the context stream (≈ 5 µs of its time per step,
+  // profiles/r03/launch_floor.txt) and no wait on the twin. When that buffer does not fit in free device
+  // memory (keeping a quarter of it free), or its allocation fails, the twin falls back for good to two
+  // blocks, double-buffered in the second half of gpair_[t & 1]. Sliced data parallelism keeps that packed
+  // [g(w_t) | g(w)] block: both halves are this rank's partial sums until the step's one all-reduce.
+  bool twin_free = !dp && free_twin_;
   if (twin_free) {
     const size_t need = size_t(m_inner) * size_t(ng_);
-    if (ganc_.size() < need) ganc_.resize(need);
+    if (ganc_.size() < need) {
+      size_t fr = 0, tot = 0;
+      const bool fits = hipMemGetInfo(&fr, &tot) == hipSuccess &&
+                        double(need - ganc_.size()) * sizeof(float) <= 0.75 * double(fr);
+      try {
+        if (fits) ganc_.resize(need);
+      } catch (const Error &) {
+        (void)hipGetLastError();
+      }
+      if (ganc_.size() < need) {
+        ganc_.resize(0);
+        free_twin_ = twin_free = false;
+      }
+    }
+  }
+  if (twin_free) {
     while (ev_anc_.size() < size_t(m_inner)) {
       hipEvent_t e;
       LBF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | event_release_flags()));
@@ -857,13 +787,6 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
   auto g2 = [&](int t) { return twin_free ? ganc_.get() + (long long)t * ng_ : gpair_[t & 1].get() + ng_; };
   auto rows_x = [&](const Slice &sl) { return xg_.get() + sl.off * In; };
   auto rows_y = [&](const Slice &sl) { return yg_.get() + sl.off * Out; };
-  const bool pre = pre_;
-  if (pre) {
-    const long long cnt0 = mb[0].cnt;
-    net_->batch_grads(w_.get(), xg_.get(), yg_.get(), m_inner, cnt0, 1.0 / double(mb[0].total), prm_.lambda,
-                      gmb_.get(), ng_, dp);
-  }
-  auto gpre = [&](int t) { return gmb_.get() + (long long)t * ng_; };
   // Tickets of the twin tasks (0: ran inline). Event order across the two host threads: task t + 2 (which
   // waits on ev_free_[t & 1]) is posted at step t + 1, after step t recorded that event; step t + 2
   // re-records it only after twin_wait(task t + 2), i.e. after that wait was enqueued. Task t records
@@ -894,34 +817,22 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
   auto tock = [&](int i, hclk::time_point a) {
     if (host_timing >= 2) ht[i] += std::chrono::duration<double, std::micro>(hclk::now() - a).count();
   };
-  if (tnet_ && !pre) {
+  if (!twin_free) {
     // the twin may reuse block t & 1 once the direction of step t - 2 has read it: nothing of this epoch
-    // has yet (recorded here so that a captured epoch's first waits are on events of the capture)
-    if (!twin_free) {
-      LBF_HIP(hipEventRecord(ev_free_[0], s));
-      LBF_HIP(hipEventRecord(ev_free_[1], s));
-    } else {
-      // the twin's first launch must follow this epoch's gather and w (same role as ev_free_ above)
-      LBF_HIP(hipEventRecord(ev_fork_, s));
-      LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
-    }
-    anchor_ahead(0);
+    // has yet
+    LBF_HIP(hipEventRecord(ev_free_[0], s));
+    LBF_HIP(hipEventRecord(ev_free_[1], s));
+  } else {
+    // the twin's first launch must follow this epoch's gather and w (same role as ev_free_ above)
+    LBF_HIP(hipEventRecord(ev_fork_, s));
+    LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
   }
+  anchor_ahead(0);
   for (int t = 0; t < m_inner; ++t) {
     const Slice &sl = mb[t];
     const double inv_b = 1.0 / double(sl.total);
     const float *gb = g2(t);
-    if (pre) {
-      if (dp) {
-        net_->loss_grad_local(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b);
-        LBF_HIP(hipMemcpyAsync(g2(t), gpre(t), size_t(ng_) * sizeof(float), hipMemcpyDeviceToDevice, s));
-        reduce_pair(wt_.get(), w_.get(), g1(t), inv_b);
-      } else {
-        net_->loss_grad(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda, nullptr,
-                        nullptr);
-        gb = gpre(t);
-      }
-    } else if (tnet_) {
+    {
       auto h0 = tick();
       if (t + 1 < m_inner) anchor_ahead(t + 1);
       tock(0, h0);
@@ -937,8 +848,6 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
       LBF_HIP(hipStreamWaitEvent(ctx_->stream, twin_free ? ev_anc_[size_t(t)] : ev_g2_[t & 1], 0));
       tock(2, h0);
       if (dp) reduce_pair(wt_.get(), w_.get(), g1(t), inv_b);
-    } else {
-      eval_pair(wt_.get(), w_.get(), g1(t), sl.off, sl.cnt, inv_b);
     }
     GramArgs ga;
     ga.policy = POL_SLBFGS;
@@ -953,8 +862,7 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     hist_.update_combine(ga, 1, +1.0, wt_.get(), wt_.get(), wh_.get() + slot * ld, -prm_.step);
     tock(3, h0);
     h0 = tick();
-    if (tnet_ && !pre && !twin_free)
-      LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
+    if (!twin_free) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
     tock(2, h0);
     h0 = tick();
     if (t > 0 && t % L == 0) {
@@ -992,99 +900,11 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     }
     tock(5, h0);
   }
-  if (tw_) twin_wait(tw_->posted); // every twin task of the epoch enqueued
+  if (tw_) tw_->wait_all(); // every twin task of the epoch enqueued
   if (host_timing >= 2)
     std::fprintf(stderr, "[lbf host] per inner step (us): twin %.1f, main eval %.1f, events %.1f, direction %.1f, "
                  "combine %.1f, Hessian step %.1f\n", ht[0] / m_inner, ht[1] / m_inner, ht[2] / m_inner,
                  ht[3] / m_inner, ht[4] / m_inner, ht[5] / m_inner);
-}
-
-SlbfgsSolver::EpochGraph::~EpochGraph() {
-  if (exec) (void)hipGraphExecDestroy(exec);
-  if (graph) (void)hipGraphDestroy(graph);
-  prof.release();
-  tprof.release();
-}
-
-std::vector<long long> SlbfgsSolver::graph_key(const EpochDraw &d) const {
-  std::vector<long long> k;
-  auto ptr = [](const void *p) { return (long long)reinterpret_cast<uintptr_t>(p); };
-  k.insert(k.end(), {have_u_ ? 1LL : 0LL, pre_ ? 1LL : 0LL, (long long)d.mb.size(), ptr(xg_.get()), ptr(yg_.get()),
-                     ptr(idx_.get()), ptr(gmb_.get())});
-  for (const Slice &sl : d.mb) k.insert(k.end(), {sl.off, sl.cnt, sl.total});
-  for (const Slice &sl : d.hb) k.insert(k.end(), {sl.off, sl.cnt, sl.total});
-  for (const Ctx *c : {ctx_, tctx_.get()}) {
-    if (!c) continue;
-    const Profiler &p = c->prof;
-    k.insert(k.end(), {p.on ? 1LL : 0LL, (long long)p.only, (long long)p.every});
-  }
-  return k;
-}
-
-// Runs this epoch's inner steps from a graph when its launch sequence was captured before (or is seen
-// for the second time now: captured, then launched). Returns false when the steps must run eagerly
-// (first sight: the eager run allocates whatever workspace the sequence needs, which a capture must not).
-bool SlbfgsSolver::epoch_graph(const EpochDraw &d) {
-  hipStream_t s = ctx_->stream;
-  const std::vector<long long> key = graph_key(d);
-  EpochGraph *G = nullptr;
-  for (auto &g : graphs_)
-    if (g->key == key) G = g.get();
-  if (!G) {
-    long long marks = -1;
-    for (auto &sk : seen_keys_)
-      if (sk.first == key) marks = sk.second;
-    if (marks < 0) { // first sight: eager, remembering how many profiler events the sequence records
-      const long long m0 = ctx_->prof.marks + (tctx_ ? tctx_->prof.marks : 0);
-      epoch_steps(d);
-      seen_keys_.emplace_back(key, ctx_->prof.marks + (tctx_ ? tctx_->prof.marks : 0) - m0);
-      if (seen_keys_.size() > 8) seen_keys_.erase(seen_keys_.begin());
-      return true;
-    }
-    std::unique_ptr<EpochGraph> g(new EpochGraph());
-    g->key = key;
-    const long long e0 = net_->evals(), r0 = net_->rows();
-    const long long te0 = tnet_ ? tnet_->evals() : 0, tr0 = tnet_ ? tnet_->rows() : 0;
-    ctx_->prof.capture_begin((long long)ctx_->prof.pool.size() + marks + 64);
-    if (tctx_) tctx_->prof.capture_begin((long long)tctx_->prof.pool.size() + marks + 64);
-    LBF_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
-    tw_inline_ = true; // the capture sees the twin's launches from this thread
-    try {
-      epoch_steps(d);
-      tw_inline_ = false;
-    } catch (...) {
-      tw_inline_ = false;
-      hipGraph_t tmp = nullptr;
-      (void)hipStreamEndCapture(s, &tmp);
-      if (tmp) (void)hipGraphDestroy(tmp);
-      ctx_->prof.capture_end().release();
-      if (tctx_) tctx_->prof.capture_end().release();
-      throw;
-    }
-    LBF_HIP(hipStreamEndCapture(s, &g->graph));
-    g->prof = ctx_->prof.capture_end();
-    if (tctx_) g->tprof = tctx_->prof.capture_end();
-    LBF_HIP(hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0));
-    g->evals = net_->evals() - e0;
-    g->rows = net_->rows() - r0;
-    g->tevals = tnet_ ? tnet_->evals() - te0 : 0;
-    g->trows = tnet_ ? tnet_->rows() - tr0 : 0;
-    g->wh_head = wh_head_;
-    g->wh_count = wh_count_;
-    g->have_u = have_u_;
-    if (graphs_.size() >= 4) graphs_.erase(graphs_.begin());
-    graphs_.push_back(std::move(g));
-    G = graphs_.back().get();
-  } else { // replay: the host state and counters the captured epoch leaves behind
-    wh_head_ = G->wh_head;
-    wh_count_ = G->wh_count;
-    have_u_ = G->have_u;
-    net_->add_counts(G->evals, G->rows);
-    if (tnet_) tnet_->add_counts(G->tevals, G->trows);
-  }
-  LBF_HIP(hipGraphLaunch(G->exec, s));
-  pending_graph_ = G;
-  return true;
 }
 
 int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
@@ -1133,7 +953,6 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
     else draw_epoch(have_u_, cur_);
     next_ready_ = false;
     const std::vector<int> &flat = cur_.flat;
-    const auto &mb = cur_.mb;
     const int pick = cur_.pick;
     idx_.ensure(std::max<size_t>(1, flat.size()));
     if (!flat.empty()) { // through pinned staging: an asynchronous copy (the stream was synchronised by read())
@@ -1147,37 +966,25 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
     yg_.ensure(std::max<size_t>(1, flat.size()) * size_t(Out));
     gather_rows(s, X_, In, idx_.get(), (long long)flat.size(), int(In), xg_.get());
     gather_rows(s, Y_, Out, idx_.get(), (long long)flat.size(), int(Out), yg_.get());
-    // Anchor gradients of the whole epoch up front (every minibatch slice of this rank the same size, a
-    // multiple of 32 rows): one evaluation over the epoch's minibatch rows at w (see gmb_).
-    const long long cnt0 = mb[0].cnt;
-    pre_ = anchor_pre_ && cnt0 > 0 && cnt0 % 32 == 0;
-    for (int t = 1; t < m_inner && pre_; ++t) pre_ = mb[t].cnt == cnt0 && mb[t].off == t * cnt0;
-    if (pre_) {
-      const size_t need = size_t(m_inner) * size_t(ng_);
-      if (gmb_.size() < need) {
-        gmb_.resize(need);
-        // the two loss words and the pad of each row are never written: zero (the DP copy sums them)
-        LBF_HIP(hipMemsetAsync(gmb_.get(), 0, need * sizeof(float), s));
-      }
-    }
     // No host synchronisation here: the upload reads pinned staging (rewritten only after the next read()),
     // and every consumer of the gathered rows is ordered after the gathers (the context stream, and the
     // twin through the event it waits on at the epoch's start), so the host enqueues the first inner step
-    // while the gathers run (LBF_SLBFGS_EPOCH_SYNC=1: the previous synchronisation).
-    static const int epoch_sync = env_int("LBF_SLBFGS_EPOCH_SYNC", 0);
-    if (epoch_sync) LBF_HIP(hipStreamSynchronize(s));
+    // while the gathers run.
     // --- epoch -----------------------------------------------------------------------------------
     static const int host_timing = env_int("LBF_HOST_TIMING", 0);
     const auto th0 = std::chrono::steady_clock::now();
-    pending_graph_ = nullptr;
-    if (!(graph_on_ && epoch_graph(cur_))) epoch_steps(cur_);
+    {
+      // replicated data parallelism: the inner steps evaluate without the communicator
+      LocalOnly lo_guard(ctx_, repl_);
+      epoch_steps(cur_);
+    }
     if (host_timing) { // host time to enqueue the epoch's inner steps vs the epoch on the device
       const auto th1 = std::chrono::steady_clock::now();
       LBF_HIP(hipStreamSynchronize(s));
       const auto th2 = std::chrono::steady_clock::now();
-      std::fprintf(stderr, "[lbf host] epoch %d: %d inner steps enqueued in %.3f ms%s, device done %.3f ms later\n",
+      std::fprintf(stderr, "[lbf host] epoch %d: %d inner steps enqueued in %.3f ms, device done %.3f ms later\n",
                    iters_, m_inner, std::chrono::duration<double, std::milli>(th1 - th0).count(),
-                   pending_graph_ ? " (graph)" : "", std::chrono::duration<double, std::milli>(th2 - th1).count());
+                   std::chrono::duration<double, std::milli>(th2 - th1).count());
     }
     // the next epoch's lists, drawn while the GPU runs this epoch's queued steps
     if (iters_ + 1 < target || iters_ + 1 < prm_.max_epochs) {
@@ -1190,11 +997,6 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
     // recorder (s_lbfgs.hpp:274-284): full loss and gradient at the new anchor == next epoch's mu
     eval_full(w_.get(), mu_.get());
     read();
-    if (pending_graph_) {
-      ctx_->prof.add_graph(pending_graph_->prof);
-      if (tctx_) tctx_->prof.add_graph(pending_graph_->tprof);
-      pending_graph_ = nullptr;
-    }
     mu_valid_ = true;
     last_loss_ = hs_[SC_LOSS];
     last_gnorm_ = std::sqrt(hs_[SC_TGG]);

@@ -2,7 +2,9 @@
 #pragma once
 
 #include "../../include/lbfgs_amd.h"
+#include "host_sync.hpp"
 #include "runtime.hpp"
+#include "sampler.hpp"
 
 #include <atomic>
 #include <chrono>
@@ -15,8 +17,6 @@
 #include <thread>
 
 namespace lbf {
-
-class MinibatchSampler;
 
 // What the minimizer evaluates: the reference's LossGradFun (src/cuda/minimizer_base.cuh:15-16) plus the
 // dots the line search needs. eval() writes the gradient into g (n+2 floats) and SC_LOSS / SC_TGG /
@@ -191,38 +191,22 @@ private:
     bool u_seen = false; // have_u after the epoch
   };
   void draw_epoch(bool u_seen, EpochDraw &d);
-  // The epoch's inner steps (s_lbfgs.hpp:218-262) enqueued on the streams: eagerly, or (epoch_graph)
-  // captured once per distinct launch sequence into a hipGraph and replayed.
+  // The epoch's inner steps (s_lbfgs.hpp:218-262) enqueued on the streams.
   void epoch_steps(const EpochDraw &d);
-  bool epoch_graph(const EpochDraw &d);
   int wh_slot(int logical) const { return (wh_head_ + logical) % (prm_.L + 1); }
   int wh_push_slot();
-  // Epoch graphs: the host enqueue of an epoch's ~5000 launches and event operations (≈ 31 ms at cfg 4)
-  // exceeds its device time, so an epoch whose launch sequence was seen once is captured (stream capture
-  // of both streams, fork / join by the same events) and then replayed with one hipGraphLaunch. Key: every
-  // input of the sequence (batch slices, buffer addresses, the profiler's configuration, have_u on entry).
-  struct EpochGraph {
-    std::vector<long long> key;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    GraphProf prof, tprof;             // the profiler's event-record nodes (bench timing)
-    long long evals = 0, rows = 0, tevals = 0, trows = 0;
-    int wh_head = 0, wh_count = 0;     // host state the epoch leaves behind
-    bool have_u = false;
-    ~EpochGraph();
-  };
-  std::vector<long long> graph_key(const EpochDraw &d) const;
-  std::vector<std::unique_ptr<EpochGraph>> graphs_;
-  std::vector<std::pair<std::vector<long long>, long long>> seen_keys_; // eager once first (allocations), marks
-  EpochGraph *pending_graph_ = nullptr; // launched this epoch: its profiler events are read after the sync
-  bool graph_on_ = false;
   std::mt19937 rng_;
   std::unique_ptr<MinibatchSampler> sampler_;
   bool started_ = false, have_u_ = false, mu_valid_ = false, next_ready_ = false, converged_ = false;
   EpochDraw cur_, next_;
   int wh_head_ = 0, wh_count_ = 0; // ring of L+1 iterates (w_history)
-  bool pre_ = false;               // this epoch's anchor gradients precomputed (anchor_pre_)
   int rec_i_ = 0;
+  // Data parallel (a communicator), LBF_SLBFGS_DP_REPLICATED: every rank runs the epoch's whole inner-step
+  // chain (identical inputs, identical bits) with no collective; only the full-batch gradient at the
+  // anchor (s_lbfgs.hpp:206, 274-284) is sharded, one all-reduce per epoch. LBF_SLBFGS_DP_SLICED: each rank
+  // evaluates its 1/p slice of every minibatch and Hessian batch, one all-reduce per inner step.
+  bool repl_ = false;
+  bool dp_inner() const { return ctx_->dp() && !repl_; }
   std::chrono::steady_clock::time_point t0_;
   // Two independent batch gradients of one step (the FD pair at u +- eps s) into one [ga | gb] block
   // (gb = gab + ng_): the second on the twin's stream when there is one, joined before the next launch.
@@ -244,12 +228,6 @@ private:
   // [g(w_t) | g(w)] of an inner step, double-buffered (the twin fills the anchor half one step ahead),
   // and [g(u + eps s) | g(u - eps s)] of a Hessian step: one all-reduce per block under data parallelism
   DevBuf<float> gpair_[2], fdpair_;
-  // Anchor gradients of a whole epoch (LBF_SLBFGS_ANCHOR=1; default off): w is fixed for the epoch and so
-  // are its minibatches, so g(w) of every minibatch is computed up front in one evaluation over the
-  // epoch's rows (Mlp::batch_grads), minibatch t at gmb_ + t ng_. The inner steps then evaluate only
-  // g(w_t): no twin, no per-step cross-stream events.
-  DevBuf<float> gmb_;
-  bool anchor_pre_ = false; // LBF_SLBFGS_ANCHOR=1
   long long ng_ = 0; // floats per gradient in a block (n + 2 loss words, rounded to 4)
   DevBuf<int> idx_;
   PinnedBuf<int> idx_host_; // pinned staging of an epoch's index lists
@@ -263,29 +241,18 @@ private:
   // (it has no communicator) and the context stream's one collective per block sums both.
   std::unique_ptr<Ctx> tctx_;
   std::unique_ptr<Mlp> tnet_;
-  // The twin stream's launches enqueued by a helper host thread (LBF_SLBFGS_TWIN_THREAD=0: inline): the
-  // inner step's host enqueue (≈ 100-130 µs, ~40 % of it the twin's evaluation) bounds the epoch on slower
+  // The twin stream's launches enqueued by a helper host thread: the inner step's host enqueue (≈ 100-130 µs, ~40 % of it the twin's evaluation) bounds the epoch on slower
   // hosts. Tasks run in posting order (one FIFO, so the twin stream sees the single-thread launch order);
   // the context thread waits for a task's ticket before it waits on an event that task records, and records
   // an event the twin waits on only after the waiting task has been enqueued (see epoch_steps).
-  struct TwinWorker {
-    std::thread th;
-    std::mutex mu;
-    std::condition_variable cv;
-    std::deque<std::function<void()>> q;
-    std::atomic<long long> done{0};
-    long long posted = 0;
-    std::exception_ptr err;
-    bool stop = false;
-  };
-  std::unique_ptr<TwinWorker> tw_;
-  bool tw_inline_ = false; // while capturing a graph: twin work on the calling thread
+  std::unique_ptr<TaskFifo> tw_; // host_sync.hpp
   long long twin_post(std::function<void()> f);
   void twin_wait(long long ticket); // returns once task `ticket` (1-based) has run; rethrows its error
   // this rank's slices of the epoch's sampled rows, gathered once (all minibatches and Hessian batches)
   DevBuf<float> xg_, yg_;
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
-  // free-running twin (single rank): anchor gradient of step t in ganc_ + t ng_, its event ev_anc_[t]
+  // free-running twin (no per-step collective): anchor gradient of step t in ganc_ + t ng_, its event
+  // ev_anc_[t]; off for good once its buffer does not fit in free device memory (double-buffered twin)
   bool free_twin_ = true;
   DevBuf<float> ganc_;
   std::vector<hipEvent_t> ev_anc_;
@@ -305,19 +272,5 @@ void fd_hvp_grads(Mlp *net, const float *u, const float *s, const float *X, cons
                   long long count, double inv_scale, double lambda, double eps, float *wp, float *wm, float *gp,
                   float *gm, double *scal);
 
-// libstdc++ partial Fisher-Yates (s_lbfgs.hpp:141-160) over a reusable identity permutation of N: a draw
-// swaps b positions, reads them, and swaps them back (O(b) per minibatch instead of the reference's iota(N),
-// which cost ~15 ms of host time per cfg-4 epoch); the draws and results are the reference's.
-class MinibatchSampler {
- public:
-  explicit MinibatchSampler(size_t N);
-  // appends the minibatch (min(b, N) indices) to out; returns how many
-  size_t draw(size_t b, std::mt19937 &rng, std::vector<int> &out);
-
- private:
-  std::vector<size_t> perm_, touched_;
-};
-// One draw with a fresh sampler (the ABI helper).
-std::vector<size_t> sample_minibatch(size_t N, size_t b, std::mt19937 &rng);
 
 } // namespace lbf

@@ -1,14 +1,15 @@
 // Fused optimizer tail of a speculative L-BFGS iteration (see TailArgs in kernels.hpp).
 //
 // Replaces, on the fast path (first trial accepted), the sequence reduce_all -> finish -> ls_ctl ->
-// gram sweep -> history step by three launches:
-//   tail_reduce  (one block per 64-column group): the gradient column from its split-K slabs (or as
-//                written), s = x_t - x_prev and y = g_t - g_prev stored into the ring's write slot,
-//                and the Gram sweep of (s, y, g_t) against every live history vector -> one row of
-//                partial dots per block;
-//   tail_cols    (one block per dot column): fixed-order reduction of the rows;
-//   tail_fin     (one block): loss and status block, the line-search decision with its host record
-//                (ls_ctl's rule), and on acceptance the push + two-loop coefficients (hist_core.hpp).
+// gram sweep -> history step by two launches:
+//   tail_reduce    (one block per 128-column group): the gradient column from its split-K slabs (or as
+//                  written), s = x_t - x_prev and y = g_t - g_prev stored into the ring's write slot,
+//                  and the Gram sweep of (s, y, g_t) against every live history vector -> one row of
+//                  partial dots per block;
+//   tail_cols_fin  (one block per dot column): fixed-order reduction of the rows; the last block to
+//                  arrive then runs the one-block fin: loss and status block, the line-search decision
+//                  with its host record (ls_ctl's rule), and on acceptance the push + two-loop
+//                  coefficients (hist_core.hpp).
 // The reference's counterpart is one LBFGS::solve iteration after its line search
 // (lbfgs.hpp:77-98 / lbfgs.cuh:143-190) with the gradient of MLPObjective / CudaNetwork.
 #include "hist_core.hpp"
@@ -214,10 +215,10 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
 }
 
 // dots[c] = sum over rows in row order (per-thread strided rows, then a fixed tree); rows are stored
-// transposed ([nc][nb]), so each block reads one contiguous column. HANDOFF (tail_cols_fin): the sum is
+// transposed ([nc][nb]), so each block reads one contiguous column. The sum is
 // stored write-through (agent-scope relaxed store = sc1) and waited for, so the arrival counter's add
 // publishes it without a release fence (MI355X_MICROARCH.md hand-off table, first row).
-template <bool HANDOFF> __device__ __forceinline__ void tail_cols_body(const TailArgs &a) {
+__device__ __forceinline__ void tail_cols_body(const TailArgs &a) {
   __shared__ double ws[4];
   const int c = blockIdx.x, t = threadIdx.x;
   const int count0 = a.h.ist[IST_COUNT];
@@ -240,18 +241,9 @@ template <bool HANDOFF> __device__ __forceinline__ void tail_cols_body(const Tai
   lds_barrier();
   if (t == 0) {
     const double d = ((ws[0] + ws[1]) + ws[2]) + ws[3];
-    if constexpr (HANDOFF) {
-      __hip_atomic_store(&a.dots[c], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      a.dots[c] = d;
-    }
+    __hip_atomic_store(&a.dots[c], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-}
-
-__global__ __launch_bounds__(256) void tail_cols_kernel(const TailArgs a) {
-  if (a.ra.abort && *a.ra.abort) return;
-  tail_cols_body<false>(a);
 }
 
 constexpr int TF_THREADS = 256;
@@ -384,18 +376,13 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
   KT(44);
 }
 
-__global__ __launch_bounds__(TF_THREADS) void tail_fin_kernel(const TailArgs a) {
-  if (a.ra.abort && *a.ra.abort) return;
-  tail_fin_body(a);
-}
-
 // tail_cols, then (cols_done) the last block to finish runs the one-block fin: one launch fewer on
 // the iteration's critical path. Hand-off without fences (the guide prices __threadfence at ~3.5 us):
 // each block's column sum is an sc1 (write-through) store waited for with vmcnt(0) before the same lane's
 // agent-scope add; the block whose add returns the last count reads the sums with sc1 loads.
 __global__ __launch_bounds__(TF_THREADS) void tail_cols_fin_kernel(const TailArgs a) {
   if (a.ra.abort && *a.ra.abort) return; // uniform for the launch: nobody arrives, the counter stays 0
-  tail_cols_body<true>(a);
+  tail_cols_body(a);
   __shared__ int s_last;
   if (threadIdx.x == 0)
     s_last = __hip_atomic_fetch_add(a.cols_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
@@ -427,17 +414,8 @@ void tail_reduce(hipStream_t s, const TailArgs &a) {
   default: throw Error(2, "tail_reduce: history size not supported by the fused tail");
   }
   LBF_KERNEL_CHECK();
-  if (a.cols_done) {
-    hipLaunchKernelGGL(tail_cols_fin_kernel, dim3(unsigned(a.nc)), dim3(TF_THREADS), fin_shmem(a), s, a);
-  } else {
-    hipLaunchKernelGGL(tail_cols_kernel, dim3(unsigned(a.nc)), dim3(256), 0, s, a);
-  }
-  LBF_KERNEL_CHECK();
-}
-
-void tail_fin(hipStream_t s, const TailArgs &a) {
-  if (a.cols_done) throw Error(2, "tail_fin: already run by the last tail_cols block");
-  hipLaunchKernelGGL(tail_fin_kernel, dim3(1), dim3(TF_THREADS), fin_shmem(a), s, a);
+  if (!a.cols_done) throw Error(2, "tail_reduce: needs the arrival counter (cols_done)");
+  hipLaunchKernelGGL(tail_cols_fin_kernel, dim3(unsigned(a.nc)), dim3(TF_THREADS), fin_shmem(a), s, a);
   LBF_KERNEL_CHECK();
 }
 

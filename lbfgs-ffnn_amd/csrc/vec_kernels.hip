@@ -774,11 +774,9 @@ __device__ __forceinline__ f32x4 hist_load(const float *p) {
 static bool hist_nt(const HistView &h) { return double(2 * h.m) * double(h.ld) * 4.0 > 512.0 * 1024 * 1024; }
 
 static constexpr int GRAM_THREADS = 512;
-// Largest chunk per workgroup (3 x chunk x 4 B of LDS); LBF_GRAM_CHUNK overrides (multiple of 1024).
-static long long gram_max_chunk() {
-  static const long long c = std::max(1024, std::min(8192, env_int("LBF_GRAM_CHUNK", 4096))) / 1024 * 1024;
-  return c;
-}
+// Largest chunk per workgroup (3 x chunk x 4 B of LDS; 1024-8192-element chunks measured alike,
+// profiles/r02/c4_chunk*.json).
+static long long gram_max_chunk() { return 4096; }
 
 int gram_ncols(int m) { return 6 * m + 6; }
 int gram_nwg(long long n) {
@@ -968,35 +966,27 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials, int transpo
   const int nwg = gram_nwg(a.h.n);
   const long long chunk = gram_chunk(a.h.n, nwg);
   const size_t shmem = size_t(3 * chunk) * sizeof(float);
-  // 16-B loads in flight per lane while streaming a history vector (LBF_GRAM_U: 4 or 8)
-  static const int U = env_int("LBF_GRAM_U", 4) >= 8 ? 8 : 4;
-  static bool attr_set = false;
-  if (!attr_set && shmem > 64 * 1024) {
-    for (const void *f : {reinterpret_cast<const void *>(gram_kernel<4, false>),
-                          reinterpret_cast<const void *>(gram_kernel<4, true>),
-                          reinterpret_cast<const void *>(gram_kernel<8, false>),
-                          reinterpret_cast<const void *>(gram_kernel<8, true>)})
-      LBF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
-    attr_set = true;
+  // 16-B loads in flight per lane while streaming a history vector (8 measured the same as 4,
+  // profiles/r03/two_loop_gramU8.jsonl)
+  if (shmem > 64 * 1024) { // once per process, thread-safe
+    static const bool attr_set = [] {
+      for (const void *f : {reinterpret_cast<const void *>(gram_kernel<4, false>),
+                            reinterpret_cast<const void *>(gram_kernel<4, true>)})
+        LBF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+      return true;
+    }();
+    (void)attr_set;
   }
   const bool nt = hist_nt(a.h);
   auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }; // null passes
-  static const int vec_on = env_int("LBF_GRAM_VEC", 1);
-  const int vec = vec_on && (a.ga || a.sa) && chunk % 4 == 0 && a.h.ld % 4 == 0 && al16(a.h.S) && al16(a.h.Y) &&
+  const int vec = (a.ga || a.sa) && chunk % 4 == 0 && a.h.ld % 4 == 0 && al16(a.h.S) && al16(a.h.Y) &&
                   al16(a.sa) && al16(a.sb) && al16(a.ya) && al16(a.yb) && al16(a.ga) && al16(a.gb) && al16(a.gc) &&
                   al16(a.g_out);
   const int tr = transposed ? 1 : 0;
-  if (U == 8) {
-    if (nt)
-      hipLaunchKernelGGL((gram_kernel<8, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
-    else
-      hipLaunchKernelGGL((gram_kernel<8, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
-  } else {
-    if (nt)
-      hipLaunchKernelGGL((gram_kernel<4, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
-    else
-      hipLaunchKernelGGL((gram_kernel<4, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
-  }
+  if (nt)
+    hipLaunchKernelGGL((gram_kernel<4, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
+  else
+    hipLaunchKernelGGL((gram_kernel<4, false>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
   LBF_KERNEL_CHECK();
 }
 
@@ -1123,21 +1113,19 @@ int hist_stage_rows(int m) {
 
 void hist_coef(hipStream_t s, const CoefArgs &a) {
   LBF_REQUIRE(a.h.m <= COEF_MAXK, "history size m must be <= 128");
-  static bool attr_set = false;
-  if (!attr_set) {
+  static const bool attr_set = [] { // once per process, thread-safe
     LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(hist_step_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024 - HIST_STATIC_LDS));
-    attr_set = true;
-  }
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - HIST_STATIC_LDS));
+    return true;
+  }();
+  (void)attr_set;
   CoefArgs c = a;
   const long long total = (160 * 1024 - HIST_STATIC_LDS) / 8, m2 = (long long)a.h.m * a.h.m;
   const long long need_stage = 6LL * a.h.m + 6;
   const long long S = a.h.slots, pre = 2 * S * S + S;
   // fused history step (LDS-prefetched sources, stores off wave 0) when the direction is wanted and
   // SY (with its transpose), a full staging area and the prefetch all fit
-  static const int fused_on = env_int("LBF_HIST_FUSED", 1);
-  c.fused = (fused_on && a.want_dir == 1 && S * S <= 256LL * HIST_PRE_UNROLL &&
+  c.fused = (a.want_dir == 1 && S * S <= 256LL * HIST_PRE_UNROLL &&
              2 * m2 + HIST_STAGE_DOUBLES + pre <= total) ? 1 : 0;
   const long long avail = total - (c.fused ? pre : 0);
   // SY and its transpose when they fit beside a full staging area; else (m = 100) hist_core's compact
@@ -1271,8 +1259,7 @@ __global__ __launch_bounds__(256) void combine_small_kernel(const CombineArgs a)
 
 void hist_combine(hipStream_t s, const CombineArgs &a) {
   LBF_REQUIRE(a.h.ld % 4 == 0, "history slot stride must be a multiple of 4");
-  static const int small_max = env_int("LBF_COMBINE_SMALL_N", 1 << 21);
-  if (a.h.n <= small_max && a.h.m <= 32) {
+  if (a.h.n <= (1LL << 21) && a.h.m <= 32) {
     const dim3 g1(unsigned(cdiv(a.h.n, 256)));
     if (a.h.m <= 16)
       hipLaunchKernelGGL(combine_small_kernel<16>, g1, dim3(256), 0, s, a);

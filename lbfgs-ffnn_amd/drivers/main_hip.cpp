@@ -1,7 +1,7 @@
 // C++ driver through include/lbfgs_amd/hip_backend.hpp, structured like the reference's
 // tests/mnist/main-gpu.cpp (UnifiedLauncher<Backend> + UnifiedConfig + train/test) with
 // Backend = HipBackend. The MNIST images are absent from the reference snapshot, so it uses the
-// synthetic MNIST-shaped data of SURVEY.md §8(d) (lbf_synth_mnist). Plain C++17, links liblbfgs_amd.so.
+// synthetic MNIST-shaped data of SURVEY.md §8(d) (lbf_synth_mnist). Plain C++17, links liblbfgs_amd_abi3.so.
 //   usage: main_hip [N_train] [max_iters] [mnist_dir]
 #include "lbfgs_amd/hip_backend.hpp"
 

@@ -1,4 +1,4 @@
-"""Object layer over the C ABI: context, MLP, solvers (all compute in liblbfgs_amd.so).
+"""Object layer over the C ABI: context, MLP, solvers (all compute in liblbfgs_amd_abi3.so).
 
 Mirrors the reference's GPU-side pieces: ``CublasHandle`` -> :class:`Context`,
 ``CudaNetwork`` -> :class:`Mlp` (src/cuda/network.cuh), ``CudaLBFGS::solve`` -> :func:`lbfgs_solve`
@@ -13,8 +13,8 @@ from typing import Optional, Sequence
 import numpy as np
 import torch
 
-from ._lib import (ACTS, INIT_CPU, INIT_CUDA, LS_ARMIJO, LS_WOLFE, GdParams, LbfError, LbfgsParams, Record,
-                   SgdParams, SlbfgsParams, SolveInfo, check, lib, ptr)
+from ._lib import (ACTS, INIT_CPU, INIT_CUDA, LS_ARMIJO, LS_WOLFE, SLBFGS_DP_REPLICATED, SLBFGS_DP_SLICED, GdParams,
+                   LbfError, LbfgsParams, Record, SgdParams, SlbfgsParams, SolveInfo, check, lib, ptr)
 
 
 class Context:
@@ -197,7 +197,12 @@ class Mlp:
                     inv_scale: Optional[float] = None, l2: float = 0.0) -> torch.Tensor:
         """Gradients of nmb consecutive minibatches of X / Y (X.shape[0] // nmb rows each, a multiple of 32) at
         one point, in one evaluation (lbf_mlp_batch_grads): returns an (nmb, nparams) tensor."""
-        cnt = int(X.shape[0]) // nmb
+        rows = int(X.shape[0])
+        if nmb <= 0 or rows % nmb:
+            raise LbfError(f"batch_grads: {rows} rows do not split into {nmb} equal minibatches")
+        cnt = rows // nmb
+        if cnt % 32:
+            raise LbfError(f"batch_grads: {cnt} rows per minibatch, need a multiple of 32")
         if inv_scale is None:
             inv_scale = 1.0 / cnt
         self._check_data(X, Y)
@@ -296,6 +301,8 @@ def lbfgs_params(line_search: str = "wolfe", **kw) -> LbfgsParams:
 def slbfgs_params(**kw) -> SlbfgsParams:
     p = SlbfgsParams()
     lib().lbf_slbfgs_default_params(C.byref(p))
+    if isinstance(kw.get("dp_mode"), str):
+        kw["dp_mode"] = {"replicated": SLBFGS_DP_REPLICATED, "sliced": SLBFGS_DP_SLICED}[kw["dp_mode"]]
     for k, v in kw.items():
         if v is not None:
             setattr(p, "reg" if k == "lam" else k, v)
@@ -366,8 +373,8 @@ def slbfgs_solve(net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tenso
 
 
 class SlbfgsRun:
-    """Stateful S-LBFGS (begin / iterate / end) used by the benchmark: epochs of one solve across several
-    iterate() calls, so that epochs with a repeated launch sequence replay their captured hipGraph."""
+    """Stateful S-LBFGS (begin / iterate / end) used by the benchmark: the epochs of one solve across several
+    iterate() calls (the breakdown, warmup and timed epochs), bitwise one lbf_slbfgs_solve."""
 
     def __init__(self, net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, record_cap: int = 100000,
                  **kw):

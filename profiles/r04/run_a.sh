@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 4: GPU suite + smoke + benches on the current tree (pruned routes, ABI 3)
+set -o pipefail
+O=gpurun_out/r04a
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 &&
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
+timeout -k 10 180 python bench.py --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err &&
+timeout -k 10 120 python bench.py --steps 400 --no-cpu-baseline > $O/bench_400.json 2> $O/bench_400.err &&
+timeout -k 10 120 python bench.py --steps 400 --samples 7500 --no-cpu-baseline > $O/bench_7500.json 2> $O/bench_7500.err &&
+timeout -k 10 180 python bench.py --solver slbfgs --steps 6 --no-cpu-baseline > $O/bench_cfg4.json 2> $O/bench_cfg4.err

@@ -325,10 +325,9 @@ def test_lbfgs_full_size_decreases(ctx, pkg):
     assert hist["loss"][-1] < 0.5 * hist["loss"][0]
 
 
-def _spec_run(pkg, ctx, monkeypatch, depth, line_search, tol, iters, chunks=1, fused=True, m=5, tail_split=False):
+def _spec_run(pkg, ctx, monkeypatch, depth, line_search, tol, iters, chunks=1, fused=True, m=5):
     monkeypatch.setenv("LBF_SPEC_DEPTH", str(depth))
     monkeypatch.setenv("LBF_FUSED_TAIL", "1" if fused else "0")
-    monkeypatch.setenv("LBF_TAIL_SPLIT", "1" if tail_split else "0")
     dims, acts = [784, 32, 10], ["relu", "linear"]
     Xh, Yh = pkg.synth_mnist(256)
     net = pkg.Mlp(ctx, dims, acts)
@@ -390,17 +389,6 @@ def test_fused_tail_matches_host_loop(ctx, pkg, monkeypatch, line_search, m):
     h, info, _ = _spec_run(pkg, ctx, monkeypatch, 4, line_search, tol, 30, m=m)
     assert info[:2] == ref_ci[:2]
     assert np.allclose(h["loss"], ref_c["loss"], rtol=1e-9, atol=0)
-
-
-@pytest.mark.parametrize("line_search", ["wolfe", "armijo"])
-def test_tail_fin_in_last_block_equals_separate_launch(ctx, pkg, monkeypatch, line_search):
-    """The fused tail's finish runs in the last tail_cols block to arrive (arrival counter); the separate
-    tail_fin launch (LBF_TAIL_SPLIT=1) is the same code on the same data: records, evaluation counts and
-    final parameters are bitwise equal."""
-    a, ai, aP = _spec_run(pkg, ctx, monkeypatch, 3, line_search, 0.0, 30, m=10, tail_split=False)
-    b, bi, bP = _spec_run(pkg, ctx, monkeypatch, 3, line_search, 0.0, 30, m=10, tail_split=True)
-    assert _same(a, b)
-    assert ai == bi and np.array_equal(aP, bP)
 
 
 @pytest.mark.parametrize("dims,acts", NETS[:6])
