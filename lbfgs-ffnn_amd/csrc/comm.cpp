@@ -1,14 +1,13 @@
 // Communicators (see comm.hpp).
 #include "comm.hpp"
 
+#include "host_sync.hpp"
 #include "kernels.hpp"
 
 #include <rccl/rccl.h>
 
-#include <chrono>
-#include <condition_variable>
 #include <cstring>
-#include <mutex>
+#include <memory>
 
 namespace lbf {
 
@@ -27,16 +26,11 @@ struct RcclComm : Comm {
 };
 
 // Shared state of an in-process group: one slot per rank for the current collective, and a reusable
-// generation barrier. A rank that never arrives (an error on its thread) turns into an error on the
-// others after kTimeout instead of a hang.
+// generation barrier (host_sync.hpp). A rank that never arrives (an error on its thread) turns into an error
+// on the others after RankBarrier's timeout instead of a hang.
 struct LocalGroup {
-  static constexpr std::chrono::seconds kTimeout{120};
   int n = 0, device = 0;
-  std::mutex mu;
-  std::condition_variable cv;
-  int arrived = 0;
-  unsigned long long gen = 0;
-  bool broken = false;
+  std::unique_ptr<RankBarrier> bar;
   std::vector<float *> bufs;
   std::vector<size_t> counts;
   std::vector<hipEvent_t> ready, read; // per rank: its buffer is complete / its sum has read every buffer
@@ -48,30 +42,15 @@ struct LocalGroup {
       if (e) (void)hipEventDestroy(e);
   }
   void fail(const std::string &why) {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      broken = true;
-    }
-    cv.notify_all();
+    bar->break_all();
     throw Error(3, "local rank group: " + why);
   }
   void barrier() {
-    std::unique_lock<std::mutex> lk(mu);
-    if (broken) throw Error(3, "local rank group: broken by another rank");
-    const unsigned long long g = gen;
-    if (++arrived == n) {
-      arrived = 0;
-      ++gen;
-      cv.notify_all();
-      return;
+    try {
+      bar->arrive_and_wait();
+    } catch (const std::runtime_error &e) {
+      throw Error(3, e.what());
     }
-    const bool ok = cv.wait_for(lk, kTimeout, [&] { return gen != g || broken; });
-    if (gen != g) return;
-    broken = true;
-    lk.unlock();
-    cv.notify_all();
-    throw Error(3, ok ? "local rank group: broken by another rank"
-                      : "local rank group: a rank did not reach the collective (timeout)");
   }
 };
 
@@ -123,6 +102,7 @@ std::vector<std::unique_ptr<Comm>> make_local_group(int nranks, int device) {
   LBF_REQUIRE(nranks >= 1 && nranks <= kMaxLocalRanks, "local rank group: 1..16 ranks");
   auto g = std::make_shared<LocalGroup>();
   g->n = nranks;
+  g->bar.reset(new RankBarrier(nranks));
   g->device = device;
   g->bufs.assign(size_t(nranks), nullptr);
   g->counts.assign(size_t(nranks), 0);
