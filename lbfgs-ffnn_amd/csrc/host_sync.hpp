@@ -38,7 +38,11 @@ public:
       cv_.notify_all();
       return;
     }
-    const bool ok = cv_.wait_for(lk, timeout_, [&] { return gen_ != g || broken_; });
+    // a system_clock deadline: libstdc++ waits on it with pthread_cond_timedwait, which ThreadSanitizer
+    // intercepts (wait_for's steady clock maps to pthread_cond_clockwait, which gcc 11's TSan does not, and
+    // then reports a bogus double lock); a clock jump only moves the timeout
+    const auto deadline = std::chrono::system_clock::now() + timeout_;
+    const bool ok = cv_.wait_until(lk, deadline, [&] { return gen_ != g || broken_; });
     if (gen_ != g) return;
     broken_ = true;
     lk.unlock();
