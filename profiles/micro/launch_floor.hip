@@ -159,7 +159,13 @@ int main() {
       hipLaunchKernelGGL(empty_k, 1, 64, 0, s);
       hipLaunchKernelGGL(empty_k, 1, 64, 0, s);
     });
+    // teardown in dependency order: every event recorded on s2 and the word both streams wait on go before
+    // s2 itself (round 3 left them, and s, a, b, m, buf, out, to the runtime's exit-time teardown)
+    CK(hipStreamSynchronize(s));
     CK(hipStreamSynchronize(s2));
+    CK(hipEventDestroy(e1));
+    CK(hipEventDestroy(e2));
+    CK(hipFree(flag));
     CK(hipStreamDestroy(s2));
   }
   // dependent chains of 10 launches at several grid sizes: eager, and the same chain as one hipGraph
@@ -206,8 +212,23 @@ int main() {
       auto t1 = std::chrono::steady_clock::now();
       CK(hipStreamSynchronize(s));
       printf("%-58s %8.2f us/call (host)\n", name, std::chrono::duration<double, std::micro>(t1 - t0).count() / R2);
+      // CK's `return 1` makes this lambda return int: without this line the normal path flowed off the end
+      // of a non-void function (undefined behaviour; clang -O3 compiles it as unreachable), which is the
+      // core dump right after this line's output in profiles/r03/launch_floor.txt (hipcc warned:
+      // -Wreturn-type, "non-void lambda does not return a value in all control paths")
+      return 0;
     };
-    host_rate("host: hipLaunchKernelGGL empty<<<1,64>>>", [&] { hipLaunchKernelGGL(empty_k, 1, 64, 0, s); });
+    if (host_rate("host: hipLaunchKernelGGL empty<<<1,64>>>", [&] { hipLaunchKernelGGL(empty_k, 1, 64, 0, s); }))
+      return 1;
   }
+  CK(hipStreamSynchronize(s));
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  CK(hipEventDestroy(m));
+  CK(hipStreamDestroy(s));
+  CK(hipFree(buf));
+  CK(hipFree(out));
+  CK(hipDeviceSynchronize());
+  printf("teardown ok\n");
   return 0;
 }
