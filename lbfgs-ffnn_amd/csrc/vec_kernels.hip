@@ -779,11 +779,31 @@ static constexpr int GRAM_THREADS = 512;
 static long long gram_max_chunk() { return 4096; }
 
 int gram_ncols(int m) { return 6 * m + 6; }
+template <int U, bool NT>
+__global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, long long chunk, double *partials, int tr,
+                                                            int vec);
+// Workgroups of the Gram sweep resident on the whole chip at the largest chunk (LDS-bound: 3 per CU), once.
+static long long gram_slots() {
+  static const long long slots = [] {
+    int dev = 0, cus = 0, per = 0;
+    LBF_HIP(hipGetDevice(&dev));
+    LBF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gram_kernel<4, true>, GRAM_THREADS,
+                                                         size_t(3 * gram_max_chunk()) * sizeof(float)));
+    return (long long)std::max(1, cus) * std::max(1, per);
+  }();
+  return slots;
+}
 int gram_nwg(long long n) {
   long long w = cdiv(n, 1024);
   if (w > 2048) w = 2048;
   long long need = cdiv(n, gram_max_chunk());
   if (w < need) w = need;
+  // More workgroups than the chip holds at once: a whole number of rounds, every round full (n = 10.49M:
+  // 2561 chunks of 4096 were 3.33 rounds of 768 resident workgroups, the last a third full; now 3072 of
+  // 3416), chunks still <= 4096.
+  const long long slots = gram_slots();
+  if (w > slots) w = cdiv(need, slots) * slots;
   return int(w < 1 ? 1 : w);
 }
 static long long gram_chunk(long long n, int nwg) { return cdiv(cdiv(n, nwg), 4) * 4; }
@@ -1161,8 +1181,10 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
   __syncthreads();
   const double cg = h.coef[2 * S_];
   const double alpha = a.alpha_from_state ? h.scal[SC_ALPHA0] : a.alpha;
-  const long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (e >= h.n) return;
+  // grid-stride over 16-B quads: the grid is the chip's resident workgroups, so every one takes the same
+  // number of quads (within one) and there is no partly filled last round
+  const long long stride = (long long)gridDim.x * blockDim.x * 4;
+  for (long long e = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4; e < h.n; e += stride) {
   if (e + 3 < h.n) {
     const f32x4 g4 = *reinterpret_cast<const f32x4 *>(a.g + e);
     const f32x4 x4 = *reinterpret_cast<const f32x4 *>((a.x_out ? a.x_in : a.g) + e); // unconditional: no early wait
@@ -1210,6 +1232,7 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
         if (a.x_out2) a.x_out2[q] = o;
       }
     }
+  }
   }
 }
 
@@ -1268,7 +1291,15 @@ void hist_combine(hipStream_t s, const CombineArgs &a) {
     LBF_KERNEL_CHECK();
     return;
   }
-  const dim3 grid(unsigned(cdiv(cdiv(a.h.n, 4), 256)));
+  static const long long resident = [] { // workgroups of combine_kernel the chip holds at once, once
+    int dev = 0, cus = 0, p8 = 0, p4 = 0;
+    LBF_HIP(hipGetDevice(&dev));
+    LBF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p8, combine_kernel<8, true>, 256, 0));
+    LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p4, combine_kernel<4, false>, 256, 0));
+    return (long long)std::max(1, cus) * std::max(1, std::min(p8, p4));
+  }();
+  const dim3 grid(unsigned(std::min(cdiv(cdiv(a.h.n, 4), 256), resident)));
   if (hist_nt(a.h))
     hipLaunchKernelGGL((combine_kernel<8, true>), grid, dim3(256), 0, s, a);
   else

@@ -8,4 +8,6 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 timeout -k 10 180 python bench.py --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err &&
 timeout -k 10 120 python bench.py --steps 400 --no-cpu-baseline > $O/bench_400.json 2> $O/bench_400.err &&
 timeout -k 10 120 python bench.py --steps 400 --samples 7500 --no-cpu-baseline > $O/bench_7500.json 2> $O/bench_7500.err &&
-timeout -k 10 180 python bench.py --solver slbfgs --steps 6 --no-cpu-baseline > $O/bench_cfg4.json 2> $O/bench_cfg4.err
+timeout -k 10 180 python bench.py --solver slbfgs --steps 6 --no-cpu-baseline > $O/bench_cfg4.json 2> $O/bench_cfg4.err &&
+timeout -k 10 120 ./profiles/micro/launch_floor > $O/launch_floor.txt 2>&1 &&
+timeout -k 10 300 python bench_two_loop.py > $O/two_loop.jsonl 2> $O/two_loop.err
