@@ -185,6 +185,7 @@ private:
   std::vector<DevBuf<float>> A_, D_;
   DevBuf<float> slab_, head_slab_, fslab_;
   bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1: the unfolded route, tests)
+  bool dw_k2_ = true;
   // Planned fold: the last hidden layer's [dW ; db] rows fold_c0_ .. in (fold_ input columns and the
   // bias row) are computed in the forward GEMM's EPI_HEAD epilogue instead of a mostly empty last
   // row tile of its dW GEMM; fold_ = -1: none.

@@ -7,6 +7,8 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
 timeout -k 10 180 python bench.py --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err &&
 timeout -k 10 120 python bench.py --steps 400 --no-cpu-baseline > $O/bench_400.json 2> $O/bench_400.err &&
+LBF_DW_K2=0 timeout -k 10 120 python bench.py --steps 400 --no-cpu-baseline > $O/bench_400_nok2.json 2> $O/bench_400_nok2.err &&
+timeout -k 10 120 python bench.py --steps 400 --no-cpu-baseline > $O/bench_400_b.json 2> $O/bench_400_b.err &&
 timeout -k 10 120 python bench.py --steps 400 --samples 7500 --no-cpu-baseline > $O/bench_7500.json 2> $O/bench_7500.err &&
 timeout -k 10 180 python bench.py --solver slbfgs --steps 6 --no-cpu-baseline > $O/bench_cfg4.json 2> $O/bench_cfg4.err &&
 timeout -k 10 120 ./profiles/micro/launch_floor > $O/launch_floor.txt 2>&1 &&
