@@ -77,11 +77,37 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
   if (wave == 0) { // the new vectors of the group (null operands read ga / sa and are masked)
     const float *dflt = g.has_g ? g.ga : g.sa;
     const float ysc = float(g.yscale);
+    // g.ga from its split-K slabs (gred_on): this lane's 4Q columns, every slab value loaded before the sums
+    f32x4 gfin[Q];
+    if (a.gred_on) {
+      const RedAllArgs &R = a.gred;
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const long long e = e4[q] + c;
+          int si = 0;
+          while (si + 1 < R.nseg && R.seg[si + 1].goff <= e) ++si;
+          const RedSeg &S = R.seg[si];
+          const long long col = min(e - S.goff, S.count - 1); // padding columns (masked later) stay in bounds
+          float gv;
+          if (S.splits > 0) {
+            double st[4] = {0.0, 0.0, 0.0, 0.0};
+            const float *src = S.slab + col;
+            for (int k = 0; k < S.splits; ++k) st[k & 3] += double(src[(long long)k * S.stride]);
+            gv = float(((st[0] + st[1]) + st[2]) + st[3]);
+          } else {
+            gv = R.G[e];
+          }
+          if (R.l2 && R.lambda != 0.0) gv = gv + float(R.lambda) * R.w[e]; // finalize_kernel's update
+          gfin[q][c] = gv;
+        }
+    }
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       auto ld4 = [&](const float *p) { return *reinterpret_cast<const f32x4 *>((p ? p : dflt) + e4[q]); };
       const f32x4 sa = ld4(g.sa), sb = ld4(g.sb), ya = ld4(g.ya), yb = ld4(g.yb);
-      const f32x4 ga = ld4(g.ga), gb = ld4(g.gb), gc = ld4(g.gc);
+      const f32x4 ga = a.gred_on ? gfin[q] : ld4(g.ga), gb = ld4(g.gb), gc = ld4(g.gc);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int qq = 256 * q + 4 * lane + c;

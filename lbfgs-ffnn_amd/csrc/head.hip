@@ -22,6 +22,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 namespace lbf {
 
 __host__ __device__ int head_hsplit(long long B, int H);
@@ -174,7 +176,153 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
   KT(33);
 }
 
+// Row head (RowHeadArgs): wave w of the block takes rows (4 blockIdx + w) rpw + r; lane l owns hidden
+// columns l + 64 j, j < NJ. Per row: the activations from the split-K slabs (every slab value of the row
+// loaded before the sums), Z = a W + b reduced across the wave in fp64 (DPP), the loss and dZ (every
+// lane holds the row's dZ), delta = (dZ W^T) .* act_prev'(a) stored, [dW ; db] accumulated per lane in
+// fp32; at the end the four waves' partials are summed in wave order into the block's slab.
+template <int NJ>
+__global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
+  if (a.abort && *a.abort) return;
+  extern __shared__ __attribute__((aligned(16))) float red[]; // [4][(H + 1) * Out]
+  __shared__ double ssew[4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int H = a.H, Out = a.Out, per = (H + 1) * Out;
+  const long long rbase = ((long long)blockIdx.x * 4 + wave) * a.rpw;
+  // the output layer's weights of this lane's columns, both biases (clamped loads, masked values)
+  float w2[NJ][HMAX_OUT], hb[NJ];
+  bool cv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = lane + 64 * j;
+    cv[j] = c < H;
+    const int cc = cv[j] ? c : H - 1;
+    hb[j] = a.hbias[cc];
+#pragma unroll
+    for (int o = 0; o < HMAX_OUT; ++o) {
+      const float v = a.P[(long long)cc * Out + (o < Out ? o : Out - 1)];
+      w2[j][o] = (cv[j] && o < Out) ? v : 0.0f;
+    }
+  }
+  float b2[HMAX_OUT];
+#pragma unroll
+  for (int o = 0; o < HMAX_OUT; ++o) b2[o] = a.P[(long long)H * Out + (o < Out ? o : Out - 1)];
+  float acc[NJ][HMAX_OUT], dbacc[HMAX_OUT];
+#pragma unroll
+  for (int o = 0; o < HMAX_OUT; ++o) {
+    dbacc[o] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j][o] = 0.0f;
+  }
+  double sse = 0.0;
+  for (int r = 0; r < a.rpw; ++r) {
+    const long long b = rbase + r;
+    if (b >= a.B) break; // wave-uniform
+    // ---- activations: fwd_reduce_act's arithmetic (slabs summed in split order, fp32) ----
+    float av[NJ];
+    with_act(a.act_prev, [&](auto AC) __attribute__((always_inline)) {
+      constexpr int A = decltype(AC)::value;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int cc = cv[j] ? lane + 64 * j : H - 1;
+        const float *src = a.fslab + b * H + cc;
+        float sum = 0.0f;
+        int k = 0;
+        for (; k + 8 <= a.splits; k += 8) { // eight loads in flight, summed in split order
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = src[(long long)(k + u) * a.stride];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) sum += v[u];
+        }
+        for (; k < a.splits; ++k) sum += src[(long long)k * a.stride];
+        av[j] = cv[j] ? act_c<A>(sum + hb[j]) : 0.0f;
+      }
+    });
+    // ---- Z = a W + b (fp64 partials, fixed DPP tree), loss, dZ: identical on every lane ----
+    const long long yrow = a.idx ? (long long)a.idx[b] : b;
+    float dz[HMAX_OUT];
+    with_act(a.act_out, [&](auto AC) __attribute__((always_inline)) {
+      constexpr int A = decltype(AC)::value;
+#pragma unroll
+      for (int o = 0; o < HMAX_OUT; ++o) {
+        dz[o] = 0.0f;
+        if (o < Out) { // uniform
+          double zp = 0.0;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) zp += double(av[j]) * double(w2[j][o]);
+          const float z = float(wave_sum_f64(zp));
+          const float outv = act_c<A>(z + b2[o]);
+          const float d = outv - a.Y[yrow * Out + o];
+          sse += double(d) * double(d);
+          dz[o] = d * dact_c<A>(outv) * float(a.inv_scale);
+        }
+      }
+    });
+    // ---- delta = (dZ W^T) .* act_prev'(a), [dW ; db] += [a | 1]^T dZ ----
+    with_act(a.act_prev, [&](auto AC) __attribute__((always_inline)) {
+      constexpr int A = decltype(AC)::value;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float dd = 0.0f;
+#pragma unroll
+        for (int o = 0; o < HMAX_OUT; ++o) dd += dz[o] * w2[j][o];
+        if (cv[j]) a.delta[b * H + lane + 64 * j] = dd * dact_c<A>(av[j]);
+#pragma unroll
+        for (int o = 0; o < HMAX_OUT; ++o) acc[j][o] += av[j] * dz[o];
+      }
+    });
+#pragma unroll
+    for (int o = 0; o < HMAX_OUT; ++o) dbacc[o] += dz[o];
+  }
+  // ---- the block's slab: the four waves' partials summed in wave order ----
+  float *mine = red + wave * per;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+    if (cv[j])
+#pragma unroll
+      for (int o = 0; o < HMAX_OUT; ++o)
+        if (o < Out) mine[(lane + 64 * j) * Out + o] = acc[j][o];
+  if (lane == 0) {
+#pragma unroll
+    for (int o = 0; o < HMAX_OUT; ++o)
+      if (o < Out) mine[H * Out + o] = dbacc[o];
+    ssew[wave] = sse; // every lane holds the same sum
+  }
+  lds_barrier();
+  float *slab = a.slab + (long long)blockIdx.x * per;
+  for (int e = t; e < per; e += 256) slab[e] = ((red[e] + red[per + e]) + red[2 * per + e]) + red[3 * per + e];
+  if (t == 0) a.sse_part[blockIdx.x] = ((ssew[0] + ssew[1]) + ssew[2]) + ssew[3];
+}
+
 } // namespace
+
+bool rowhead_supported(int H, int Out) { return H >= 1 && H <= HMAX && Out >= 1 && Out <= HMAX_OUT; }
+// rows per wave: one while the grid stays within 256 workgroups, then enough that it does (bounded slabs)
+int rowhead_rpw(long long B) { return int(std::max(1LL, cdiv(std::max(1LL, B), 4LL * 256))); }
+int rowhead_nwg(long long B) { return int(cdiv(std::max(1LL, B), 4LL * rowhead_rpw(B))); }
+
+void rowhead(hipStream_t s, const RowHeadArgs &a) {
+  LBF_REQUIRE(rowhead_supported(a.H, a.Out) && a.splits >= 1 && a.rpw == rowhead_rpw(a.B), "rowhead: shape");
+  const size_t shmem = size_t(4) * (a.H + 1) * a.Out * sizeof(float);
+  static const bool attr_set = [] { // once per process, thread-safe
+    const void *fns[] = {reinterpret_cast<const void *>(rowhead_kernel<1>),
+                         reinterpret_cast<const void *>(rowhead_kernel<2>),
+                         reinterpret_cast<const void *>(rowhead_kernel<3>),
+                         reinterpret_cast<const void *>(rowhead_kernel<4>)};
+    for (const void *f : fns) LBF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+    return true;
+  }();
+  (void)attr_set;
+  const dim3 grid(unsigned(rowhead_nwg(a.B))), block(256);
+  switch ((a.H + 63) / 64) {
+  case 1: hipLaunchKernelGGL(rowhead_kernel<1>, grid, block, shmem, s, a); break;
+  case 2: hipLaunchKernelGGL(rowhead_kernel<2>, grid, block, shmem, s, a); break;
+  case 3: hipLaunchKernelGGL(rowhead_kernel<3>, grid, block, shmem, s, a); break;
+  default: hipLaunchKernelGGL(rowhead_kernel<4>, grid, block, shmem, s, a); break;
+  }
+  LBF_KERNEL_CHECK();
+}
 
 bool head_supported(int H, int Out) { return Out >= 1 && Out <= HMAX_OUT && H >= 1 && H <= HMAX; }
 int head_tile(int) { return TB; }

@@ -102,6 +102,33 @@ void head_fused(hipStream_t s, const float *A, int H, const float *P, int Out, c
                 long long B, int act_out, int act_prev, double inv_scale, float *delta, float *slab,
                 double *sse_part, const int *abort = nullptr);
 
+// The same output layer fed straight from the last hidden layer's forward split-K slabs (small batches,
+// e.g. S-LBFGS's 256-row minibatches on 784-512-256-10): one wave per sample row finishes the row's
+// activations exactly as fwd_reduce_act would (fp32 split order, + bias, act_prev) and runs the head on
+// them, so the last hidden layer's reduce launch and the tile-based head become one launch. One
+// [dW ; db] partial slab ((H + 1) x Out) and SSE partial per workgroup, like head_fused.
+struct RowHeadArgs {
+  const float *fslab = nullptr; // [splits][B][H] forward partial slabs of the last hidden layer
+  int splits = 0;
+  long long stride = 0;         // floats per split (B * H)
+  const float *hbias = nullptr; // the hidden layer's bias
+  int act_prev = 0;
+  const float *P = nullptr;     // the output layer's [W (H x Out) | b]
+  int H = 0, Out = 0, act_out = 0;
+  const float *Y = nullptr;
+  const int *idx = nullptr;
+  long long B = 0;
+  int rpw = 1;                  // rows per wave
+  double inv_scale = 1.0;
+  float *delta = nullptr, *slab = nullptr;
+  double *sse_part = nullptr;
+  const int *abort = nullptr;
+};
+bool rowhead_supported(int H, int Out);
+int rowhead_rpw(long long B);
+int rowhead_nwg(long long B); // workgroups == partial slabs
+void rowhead(hipStream_t s, const RowHeadArgs &a);
+
 // grad[e] = sum_s slab[s*stride + e] * scale (fixed order), e in [0, count)
 // Forward split-K finish: out = act(sum_s slab[s] + bias), slabs summed in split order (fp32, like
 // the GEMM's own accumulation).
@@ -373,6 +400,11 @@ struct DirArgs {
   double *dots = nullptr;   // [dir_ncols(m)]
   int nb = 0;               // cdiv(n, dir_cols_per_block(m, n))
   unsigned *cols_done = nullptr; // arrival counter, zero between launches
+  // gred_on: g.ga's values are finished here from split-K slabs (reduce_all's arithmetic: per column the
+  // splits in four stripes k = 0, 4, ..., then ((s0 + s1) + s2) + s3 in fp64, float, + lambda w in fp32)
+  // instead of read; segments without splits (finished by the dW launch's side blocks) read gred.G
+  RedAllArgs gred;
+  int gred_on = 0;
 };
 bool dir_supported(int m, long long n);
 int dir_cols_per_block(int m, long long n);

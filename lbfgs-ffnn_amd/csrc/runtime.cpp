@@ -97,6 +97,7 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
   nparams_ = off;
   if (const char *e = std::getenv("LBF_NO_FOLD")) fold_on_ = e[0] != '1'; // tests: the unfolded route
   dw_k2_ = env_int("LBF_DW_K2", 1) != 0; // A/B of TILE_128x128K2 (round 4 measurement; removed after)
+  rowhead_on_ = env_int("LBF_ROWHEAD", 1) != 0; // A/B of the row head (round 4 measurement; removed after)
 }
 
 // Split-K factor for `tiles` output tiles over a K of `K` rows: the GEMM tiles run two workgroups per
@@ -261,6 +262,13 @@ int Mlp::dx_tile(long long B, int N) const {
   return TILE_AUTO;
 }
 
+bool Mlp::rowhead_on(long long B) const {
+  const int nl = int(layers_.size());
+  if (nl < 2 || B <= 0) return false;
+  const Layer &Lo = layers_[size_t(nl - 1)], &Lh = layers_[size_t(nl - 2)];
+  return Lh.fsplits > 1 && rowhead_supported(Lo.in, Lo.out) && head_supported(Lo.in, Lo.out) && rowhead_on_;
+}
+
 bool Mlp::gemm_head_on() const {
   const int nl = int(layers_.size());
   if (nl < 2) return false;
@@ -283,8 +291,8 @@ void Mlp::ensure(long long B) {
   const Layer &Lo = layers_[nl - 1];
   size_t nloss = size_t(loss_partials_wg(std::max(1LL, B), Lo.out));
   if (nl >= 2 && head_supported(Lo.in, Lo.out)) {
-    const size_t hw =
-        size_t(std::max(head_nwg(B, Lo.in), gemm_row_tiles(int(std::max(1LL, B)), layers_[nl - 2].ftile)));
+    const size_t hw = size_t(std::max({head_nwg(B, Lo.in), gemm_row_tiles(int(std::max(1LL, B)), layers_[nl - 2].ftile),
+                                       rowhead_nwg(B)}));
     nloss = std::max(nloss, hw);
     head_slab_.ensure(hw * (size_t(Lo.in + 1) * Lo.out + (fold_ >= 0 ? size_t(fold_ + 1) * Lo.in : 0)));
   }
@@ -328,7 +336,7 @@ GemmDesc Mlp::fwd_desc(size_t l, const float *P, const float *in, const int *idx
   return d;
 }
 
-const float *Mlp::forward(const float *P, const float *X, const int *idx, long long B, int nrun) {
+const float *Mlp::forward(const float *P, const float *X, const int *idx, long long B, int nrun, bool raw_last) {
   ensure(B);
   hipStream_t s = ctx_->stream;
   const float *in = X;
@@ -346,7 +354,8 @@ const float *Mlp::forward(const float *P, const float *X, const int *idx, long l
       // lengthened the GEMM more than the launch it saved, profiles/r03/bench_cfg4_*_fin.json)
       ProfScope ps(ctx_, PK_FWD, int(l), double(B));
       gemm(s, d);
-      fwd_reduce_act(s, fslab_.get(), L.fsplits, B * L.out, int(B), L.out, d.bias, L.act, A_[l].get(), ctx_->abort);
+      if (!(raw_last && l + 1 == nr))
+        fwd_reduce_act(s, fslab_.get(), L.fsplits, B * L.out, int(B), L.out, d.bias, L.act, A_[l].get(), ctx_->abort);
     } else {
       ProfScope ps(ctx_, PK_FWD, int(l), double(B));
       gemm(s, d);
@@ -373,9 +382,39 @@ void Mlp::forward_phase(const float *P, const float *X, const float *Y, const in
   // nets) takes the unfolded route instead
   const float *head_in = nl >= 3 ? A_[nl - 3].get() : X;
   const int fold = (gemm_head && (reinterpret_cast<uintptr_t>(head_in) & 15u) == 0) ? fold_ : -1;
-  forward(P, X, idx, B, fused ? (gemm_head ? nl - 2 : nl - 1) : nl);
+  const bool row_head = fused && !gemm_head && rowhead_on(B);
+  forward(P, X, idx, B, fused ? (gemm_head ? nl - 2 : nl - 1) : nl, row_head);
   int nloss, lstart;
-  if (gemm_head) {
+  if (row_head) {
+    // last layer straight from the last hidden layer's split-K slabs: its fwd_reduce_act and the tile head
+    // in one launch (head.hip rowhead)
+    const Layer &Lh = layers_[nl - 2];
+    RowHeadArgs r;
+    r.fslab = fslab_.get();
+    r.splits = Lh.fsplits;
+    r.stride = B * Lh.out;
+    r.hbias = P + Lh.off + size_t(Lh.in) * Lh.out;
+    r.act_prev = Lh.act;
+    r.P = P + Lo.off;
+    r.H = Lo.in;
+    r.Out = Lo.out;
+    r.act_out = Lo.act;
+    r.Y = Y;
+    r.idx = idx;
+    r.B = B;
+    r.rpw = rowhead_rpw(B);
+    r.inv_scale = inv_scale;
+    r.delta = D_[nl - 2].get();
+    r.slab = head_slab_.get();
+    r.sse_part = loss_part_.get();
+    r.abort = ctx_->abort;
+    nloss = rowhead_nwg(B);
+    {
+      ProfScope ps(ctx_, PK_LOSS);
+      rowhead(s, r);
+    }
+    lstart = nl - 2;
+  } else if (gemm_head) {
     nloss = gemm_row_tiles(int(B), layers_[nl - 2].ftile);
     GemmDesc d = fwd_desc(size_t(nl - 2), P, head_in, idx, B);
     d.epi = EPI_HEAD;
@@ -449,6 +488,15 @@ void Mlp::loss_grad(const float *P, float *G, const float *X, const float *Y, co
   backward_phase(P, G, X, idx, B, inv_scale, lambda, pdir, scal, tf, false, nullptr);
 }
 
+void Mlp::loss_grad_deferred(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
+                             double inv_scale, double lambda, RedAllArgs *red) {
+  LBF_REQUIRE(B >= 0 && red, "loss_grad_deferred: batch / output");
+  LBF_REQUIRE(!ctx_->dp(), "loss_grad_deferred: single rank (or replicated) only");
+  red->nseg = 0;
+  if (B > 0) forward_phase(P, X, Y, idx, B, inv_scale);
+  backward_phase(P, G, X, idx, B, inv_scale, lambda, nullptr, nullptr, nullptr, false, nullptr, red);
+}
+
 void Mlp::loss_grad_local(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
                           double inv_scale) {
   LBF_REQUIRE(B >= 0, "negative batch");
@@ -470,7 +518,7 @@ void Mlp::grad_after_loss(const float *P, float *G, const float *X, const int *i
 // finish (+ all-reduce, dots, status block) or the fused optimizer tail.
 void Mlp::backward_phase(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
                          double lambda, const float *pdir, double *scal, const TailFuse *tf, bool local,
-                         const float *hilo_in) {
+                         const float *hilo_in, RedAllArgs *defer) {
   hipStream_t s = ctx_->stream;
   const int nl = int(layers_.size());
   const Layer &Lo = layers_[nl - 1];
@@ -687,6 +735,14 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
   ++evals_;
   rows_ += B;
   if (!reduced) {
+    if (defer && !ra.dots) {
+      bool one_pass = true;
+      for (int l = 0; l < nl; ++l) one_pass = one_pass && ra.seg[l].parts == 1;
+      if (one_pass) { // the consumer finishes the gradient from the slabs (Mlp::loss_grad_deferred)
+        *defer = ra;
+        return;
+      }
+    }
     ProfScope ps(ctx_, PK_SLAB, 0);
     reduce_all(s, ra);
     return;
@@ -1007,7 +1063,7 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
 
 void History::reset() { hist_reset(ctx_->stream, v_); }
 
-void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
+void History::update(const GramArgs &g0, int want_dir, int iter, double dsign, const RedAllArgs *gred) {
   GramArgs g = g0;
   g.h = v_;
   g.h.abort = ctx_->abort;
@@ -1015,11 +1071,21 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
   auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
   const bool aligned = al16(g.sa) && al16(g.sb) && al16(g.ya) && al16(g.yb) && al16(g.ga) && al16(g.gb) &&
                        al16(g.gc) && al16(g.g_out); // 16-B lanes in dir_sweep (null pointers pass)
-  if (dir_on_ && aligned && g.policy == POL_SLBFGS && (want_dir == 0 || want_dir == 1)) {
+  const bool defer = gred && gred->nseg > 0;
+  const bool dir = dir_on_ && aligned && g.policy == POL_SLBFGS && (want_dir == 0 || want_dir == 1);
+  if (defer && !(dir && g.has_g && gred->G == g.ga)) { // only the fused sweep finishes deferred slabs
+    ProfScope ps(ctx_, PK_SLAB, 0);
+    reduce_all(s, *gred);
+  }
+  if (dir) {
     // S-LBFGS: sweep + column sums whose last block runs the step (dir.hip), two launches instead of
     // gram -> fold -> hist_step
     DirArgs d;
     d.g = g;
+    if (defer && g.has_g && gred->G == g.ga) { // g.ga finished inside the sweep from its split-K slabs
+      d.gred = *gred;
+      d.gred_on = 1;
+    }
     d.want_dir = want_dir;
     d.iter = iter;
     d.dsign = dsign;
@@ -1084,10 +1150,10 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign) {
 }
 
 void History::update_combine(const GramArgs &g0, int iter, double dsign, const float *x_in, float *x_out,
-                             float *x_out2, double alpha) {
+                             float *x_out2, double alpha, const RedAllArgs *gred) {
   // (the combine inside the column-sum launch measured slower: its waiting blocks slowed the column sums
   // and the one-block step, profiles/r03b/README.md)
-  update(g0, 1, iter, dsign);
+  update(g0, 1, iter, dsign, gred);
   combine(g0.g_out, nullptr, x_in, x_out, x_out2, false, alpha);
 }
 

@@ -118,7 +118,9 @@ public:
   Ctx *ctx() const { return ctx_; }
 
   // Forward only: activations of every layer into the workspace; returns the output buffer.
-  const float *forward(const float *P, const float *X, const int *idx, long long B, int nrun = -1);
+  // raw_last: the last layer run stays as its split-K slabs in fslab_ (no fwd_reduce_act; rowhead reads them)
+  const float *forward(const float *P, const float *X, const int *idx, long long B, int nrun = -1,
+                       bool raw_last = false);
   // Fused loss + gradient (+ all-reduce over the communicator) + line-search dots.
   //   G    : gradient output, must hold nparams()+2 floats (two extra words carry the loss for the
   //          all-reduce).
@@ -126,6 +128,12 @@ public:
   //   scal : device fp64 status block (SC_LOSS, SC_TGG, SC_TGP, SC_WW, SC_SSE written).
   void loss_grad(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
                  double inv_scale, double lambda, const float *pdir, double *scal, const TailFuse *tf = nullptr);
+  // loss_grad without the last launch (a single rank's gradient only: scal == nullptr): the split-K slabs
+  // are left for the consumer, which finishes each gradient value with reduce_all's arithmetic (the S-LBFGS
+  // direction sweep, dir.hip). *red describes the slabs; red->nseg == 0 when a segment needs the multi-part
+  // reduction (then G is complete as with loss_grad).
+  void loss_grad_deferred(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
+                          double inv_scale, double lambda, RedAllArgs *red);
   // The same evaluation in two steps (a line-search trial needs f first and the gradient only once
   // Armijo holds, full_batch_minimizer.hpp:136-146): loss_only runs the forward phase and writes
   // SC_SSE / SC_LOSS (lambda == 0); grad_after_loss then runs the backward phase of that same forward
@@ -167,7 +175,7 @@ private:
   void forward_phase(const float *P, const float *X, const float *Y, const int *idx, long long B, double inv_scale);
   void backward_phase(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
                       double lambda, const float *pdir, double *scal, const TailFuse *tf, bool local,
-                      const float *hilo_in);
+                      const float *hilo_in, RedAllArgs *defer = nullptr);
   struct FwdState {
     long long B = -1;
     bool fused = false;
@@ -186,6 +194,8 @@ private:
   DevBuf<float> slab_, head_slab_, fslab_;
   bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1: the unfolded route, tests)
   bool dw_k2_ = true;
+  bool rowhead_on_ = true;
+  bool rowhead_on(long long B) const; // the standalone head fed by the last hidden layer's slabs
   // Planned fold: the last hidden layer's [dW ; db] rows fold_c0_ .. in (fold_ input columns and the
   // bias row) are computed in the forward GEMM's EPI_HEAD epilogue instead of a mostly empty last
   // row tile of its dW GEMM; fold_ = -1: none.
@@ -212,12 +222,14 @@ public:
   HistView view() const { return v_; }
   void reset();
   // Gram sweep + bookkeeping (+ direction coefficients when want_dir > 0).
-  void update(const GramArgs &g, int want_dir, int iter, double dsign);
+  // gred (nullable, nseg > 0): g.ga's values are still split-K slabs (Mlp::loss_grad_deferred); the fused
+  // S-LBFGS sweep finishes them in place of reduce_all, other routes launch reduce_all first.
+  void update(const GramArgs &g, int want_dir, int iter, double dsign, const RedAllArgs *gred = nullptr);
   void combine(const float *g, float *dir, const float *x_in, float *x_out, float *x_out2, bool alpha_from_state,
                double alpha);
   // update(g, 1, iter, dsign) then combine(g.g_out, nullptr, x_in, x_out, x_out2, false, alpha)
   void update_combine(const GramArgs &g, int iter, double dsign, const float *x_in, float *x_out, float *x_out2,
-                      double alpha);
+                      double alpha, const RedAllArgs *gred = nullptr);
   double *scal() const { return v_.scal; }
   int m() const { return v_.m; }
 

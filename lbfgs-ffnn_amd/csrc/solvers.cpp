@@ -828,6 +828,7 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
   }
   anchor_ahead(0);
+  RedAllArgs gred; // the main evaluation's split-K slabs, finished by the direction sweep
   for (int t = 0; t < m_inner; ++t) {
     const Slice &sl = mb[t];
     const double inv_b = 1.0 / double(sl.total);
@@ -839,9 +840,9 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
       h0 = tick();
       if (dp)
         net_->loss_grad_local(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b);
-      else
-        net_->loss_grad(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda, nullptr,
-                        nullptr);
+      else // the gradient's last reduction runs inside the direction sweep (one launch fewer per step)
+        net_->loss_grad_deferred(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda,
+                                 &gred);
       tock(1, h0);
       h0 = tick();
       twin_wait(tk[size_t(t)]); // task t recorded ev_g2_[t & 1] / ev_anc_[t]
@@ -859,7 +860,7 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     auto h0 = tick();
     const int slot = wh_push_slot();
     // r = H v (two-loop), then wt = wt - step * r ; w_history.push_back(wt)
-    hist_.update_combine(ga, 1, +1.0, wt_.get(), wt_.get(), wh_.get() + slot * ld, -prm_.step);
+    hist_.update_combine(ga, 1, +1.0, wt_.get(), wt_.get(), wh_.get() + slot * ld, -prm_.step, dp ? nullptr : &gred);
     tock(3, h0);
     h0 = tick();
     if (!twin_free) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
