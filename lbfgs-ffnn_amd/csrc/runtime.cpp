@@ -196,7 +196,7 @@ void Mlp::plan(long long B) {
     // k-groups, one workgroup per CU, so each output element is summed from half the split-K slabs that two
     // 4-wave workgroups per CU need (cfg 2: 39 slabs instead of 82, 33 -> 16 MB for the tail to read); the
     // MFMA work per CU is the same
-    if (L.dtile == TILE_AUTO && L.out > 64 && B > 16384 && dw_k2_) L.dtile = TILE_128x128K2;
+    if (L.dtile == TILE_AUTO && L.out > 64 && B > 16384 && B % 4 == 0 && dw_k2_) L.dtile = TILE_128x128K2;
   }
   // The last hidden layer's dW GEMM has in + 1 rows; when they pass a multiple of its tile height by
   // at most 16 input columns + the bias row (784 + 1 = 6 x 128 + 17 at cfg 2), those rows go to the
