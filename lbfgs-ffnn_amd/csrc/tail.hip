@@ -47,7 +47,7 @@ __host__ __device__ constexpr int tail_vpw_maxm(int vpw) { return vpw <= 2 ? 2 :
 constexpr int tail_max(int a, int b) { return a > b ? a : b; }
 
 template <int VPW>
-__global__ __launch_bounds__(256, VPW <= 8 ? 4 : 2) void tail_reduce_kernel(const TailArgs a) {
+__global__ __launch_bounds__(256, 4) void tail_reduce_kernel(const TailArgs a) {
   constexpr int TC = TAIL_COLS, C = TAIL_COLS / 64;
   const RedAllArgs &ra = a.ra;
   if (ra.abort && *ra.abort) return;
