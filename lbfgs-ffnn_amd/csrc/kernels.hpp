@@ -371,13 +371,10 @@ struct TailArgs {
   double *dots = nullptr; // [nc]
   int tcg0[RA_MAXSEG] = {}; // first TAIL_COLS column group of each segment
   int nb = 0, nc = 0;       // nb: TAIL_COLS column groups over all segments (one block each)
-  // Arrival counters (cdiv(nb, TAIL_GROUP) + 1, zero between launches) and the group rows
-  // [nc][cdiv(nb, TAIL_GROUP)] of the in-launch two-level column sums; the block that finishes runs the fin.
+  // Arrival counter (zero between launches): the last tail_cols block to finish runs the one-block fin.
   unsigned *cols_done = nullptr;
-  double *grows = nullptr;
 };
-constexpr int TAIL_GROUP = 32; // partial rows per first-level sum
-void tail_reduce(hipStream_t s, const TailArgs &a); // one launch: sweep, column sums, fin
+void tail_reduce(hipStream_t s, const TailArgs &a); // tail_reduce + tail_cols_fin launches
 int tail_vpw(int m);                                // vectors per wave of the Gram sweep (0: unsupported)
 
 // S-LBFGS history update in two launches (dir.hip): a one-round-trip Gram sweep of the new s / y / g

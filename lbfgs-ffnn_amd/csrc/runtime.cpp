@@ -715,16 +715,13 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       ta.tcg0[l] = ta.nb;
       ta.nb += int(cdiv(ra.seg[l].count, (long long)TAIL_COLS));
     }
-    const size_t ngroups = size_t(cdiv(ta.nb, TAIL_GROUP));
     trows_.ensure(size_t(ta.nb) * ta.nc);
     tdots_.ensure(size_t(ta.nc));
-    tgrows_.ensure(ngroups * size_t(ta.nc));
     ta.rows = trows_.get();
     ta.dots = tdots_.get();
-    ta.grows = tgrows_.get();
-    if (cols_done_.size() < ngroups + 1) { // counters zero between launches (each last arrival re-zeroes its own)
-      cols_done_.resize(ngroups + 1);
-      LBF_HIP(hipMemsetAsync(cols_done_.get(), 0, (ngroups + 1) * sizeof(unsigned), s));
+    if (!cols_done_.get()) {
+      cols_done_.resize(1);
+      LBF_HIP(hipMemsetAsync(cols_done_.get(), 0, sizeof(unsigned), s));
     }
     ta.cols_done = cols_done_.get();
     {

@@ -202,8 +202,8 @@ private:
   int fold_ = -1, fold_c0_ = 0;
   bool gemm_head_on() const; // the output layer runs inside the last hidden layer's forward GEMM
   int dx_tile(long long B, int N) const;
-  DevBuf<double> loss_part_, dots_part_, sse_, colpart_, trows_, tdots_, tgrows_;
-  DevBuf<unsigned> cols_done_; // the fused tail's arrival counters (zero between launches)
+  DevBuf<double> loss_part_, dots_part_, sse_, colpart_, trows_, tdots_;
+  DevBuf<unsigned> cols_done_; // tail_cols arrival counter (zero between launches)
   // R-pass workspace (hvp): R{Z}, R{A}, R{dZ} and delta per layer, two products, one segment
   std::vector<DevBuf<float>> RZ_, RA_, RD_, DL_;
   DevBuf<float> T1_, T2_, seg_;

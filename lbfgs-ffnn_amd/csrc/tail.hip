@@ -1,14 +1,15 @@
 // Fused optimizer tail of a speculative L-BFGS iteration (see TailArgs in kernels.hpp).
 //
 // Replaces, on the fast path (first trial accepted), the sequence reduce_all -> finish -> ls_ctl ->
-// gram sweep -> history step by one launch:
-//   tail_reduce  (one launch, one block per 128-column group): the gradient column from its split-K slabs
-//                (or as written), s = x_t - x_prev and y = g_t - g_prev stored into the ring's write slot,
-//                and the Gram sweep of (s, y, g_t) against every live history vector -> one row of
-//                partial dots per block; the rows are summed in two levels by the last-arriving blocks
-//                (groups of TAIL_GROUP rows, then the group rows), and the block that finishes runs the
-//                fin: loss and status block, the line-search decision with its host record (ls_ctl's
-//                rule), and on acceptance the push + two-loop coefficients (hist_core.hpp).
+// gram sweep -> history step by two launches:
+//   tail_reduce    (one block per 128-column group): the gradient column from its split-K slabs (or as
+//                  written), s = x_t - x_prev and y = g_t - g_prev stored into the ring's write slot,
+//                  and the Gram sweep of (s, y, g_t) against every live history vector -> one row of
+//                  partial dots per block;
+//   tail_cols_fin  (one block per dot column): fixed-order reduction of the rows; the last block to
+//                  arrive then runs the one-block fin: loss and status block, the line-search decision
+//                  with its host record (ls_ctl's rule), and on acceptance the push + two-loop
+//                  coefficients (hist_core.hpp).
 // The reference's counterpart is one LBFGS::solve iteration after its line search
 // (lbfgs.hpp:77-98 / lbfgs.cuh:143-190) with the gradient of MLPObjective / CudaNetwork.
 #include "hist_core.hpp"
@@ -39,28 +40,15 @@ __device__ __forceinline__ double t_wave_sum(double v) { return wave_sum_f64(v);
 // per-vector 64-lane reductions. Rows are stored transposed, [nc][nb], so tail_cols reads each
 // column contiguously. 128-column groups halve the grid (n = 101,770: 796 blocks), which keeps every
 // block resident at once (this kernel's SGPR count admits 6 blocks per CU).
-__device__ __forceinline__ void tail_fin_body(const TailArgs &a, double *dyn);
-// LDS of tail_fin_body's dyn area for history size m (doubles)
-__host__ __device__ constexpr int tail_fin_doubles(int m) { return 3 * m * m + 2 * (m + 1) * (m + 1) + (m + 1); }
-// largest m a VPW serves (tail_vpw)
-__host__ __device__ constexpr int tail_vpw_maxm(int vpw) { return vpw <= 2 ? 2 : vpw <= 4 ? 6 : vpw <= 8 ? 14 : TAIL_MAXM; }
-constexpr int tail_max(int a, int b) { return a > b ? a : b; }
-
 template <int VPW>
-__global__ __launch_bounds__(256, 4) void tail_reduce_kernel(const TailArgs a) {
+__global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   constexpr int TC = TAIL_COLS, C = TAIL_COLS / 64;
   const RedAllArgs &ra = a.ra;
   if (ra.abort && *ra.abort) return;
-  // one LDS pool: the sweep's staging (part | xs | ops) and, in the block that finishes the launch, the
-  // history step's dyn area over it
-  constexpr int SWEEP_D = (4 * TC * 8 + 4 * VPW * TC * 4 + 5 * TC * 4) / 8;
-  constexpr int POOL_D = tail_max(SWEEP_D, tail_fin_doubles(tail_vpw_maxm(VPW)));
-  __shared__ __attribute__((aligned(16))) double pool[POOL_D];
-  double(*part)[TC] = reinterpret_cast<double(*)[TC]>(pool);
-  float(*xs)[TC] = reinterpret_cast<float(*)[TC]>(pool + 4 * TC);             // this group's live history values
-  float(*ops)[TC] = reinterpret_cast<float(*)[TC]>(pool + 4 * TC + 4 * VPW * TC / 2); // s, y, g, p, w
+  __shared__ double part[4][TC];
+  __shared__ float xs[2 * TAIL_MAXM][TC]; // this group's values of the live history vectors
+  __shared__ float ops[5][TC];            // s, y, g, p, w
   __shared__ int ist[IST_ORDER + TAIL_MAXM];
-  __shared__ int s_last;
   const HistView &h = a.h;
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6), stripe = wave; // uniform: scalar branches
@@ -217,75 +205,45 @@ __global__ __launch_bounds__(256, 4) void tail_reduce_kernel(const TailArgs a) {
     }
     d += dpp_f64<0xB1, 0xF>(d); // quad_perm [1,0,3,2]
     d += dpp_f64<0x4E, 0xF>(d); // quad_perm [2,3,0,1]: every lane of the quad holds the same sum
-    if (c >= 0 && q == 0) // write-through (sc1): read by the block that finishes this row's group
-      __hip_atomic_store(&a.rows[(long long)c * a.nb + blockIdx.x], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c >= 0 && q == 0) a.rows[(long long)c * a.nb + blockIdx.x] = d;
   }
   KT(54);
   KTB(4);
 #ifdef LBF_KTRACE
   if (t == 0 && blockIdx.x >= 1024 && blockIdx.x < 2048) lbf_kt_blk[6 * 1024 + blockIdx.x - 1024] = wall_clock64();
 #endif
-  // ---- column sums in two levels, inside this launch: the last block of each group of TAIL_GROUP rows to
-  // arrive sums the group's rows (row order), the last group to arrive sums the group rows (group order)
-  // and runs the history step. Fence-free hand-off (MI355X_MICROARCH.md visibility table, first row): sc1
-  // stores drained (vmcnt(0)) before the barrier, ONE relaxed agent-scope add per block, sc1 loads by the
-  // last arrival; each last arrival re-zeroes its counter for the next launch (stream order). ----
-  const int ngroups = (a.nb + TAIL_GROUP - 1) / TAIL_GROUP, grp = int(blockIdx.x) / TAIL_GROUP;
-  const int gsize = min(TAIL_GROUP, a.nb - grp * TAIL_GROUP);
-  // columns in use: the live pairs' 6 count0 and the 8 self columns (the rest hold nothing this launch)
-  auto used = [&](int col) { return col < 6 * count0 || (col >= 6 * h.m && col < a.nc); };
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
-  if (t == 0) {
-    unsigned *cnt = a.cols_done + grp;
-    const bool last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == unsigned(gsize - 1);
-    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = last ? 1 : 0;
-  }
-  lds_barrier();
-  if (!s_last) return;
-  for (int col = t; col < a.nc; col += 256) {
-    if (!used(col)) continue;
-    const double *src = a.rows + (long long)col * a.nb + grp * TAIL_GROUP;
-    double v[TAIL_GROUP];
+}
+
+// dots[c] = sum over rows in row order (per-thread strided rows, then a fixed tree); rows are stored
+// transposed ([nc][nb]), so each block reads one contiguous column. The sum is
+// stored write-through (agent-scope relaxed store = sc1) and waited for, so the arrival counter's add
+// publishes it without a release fence (MI355X_MICROARCH.md hand-off table, first row).
+__device__ __forceinline__ void tail_cols_body(const TailArgs &a) {
+  __shared__ double ws[4];
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int count0 = a.h.ist[IST_COUNT];
+  // only the columns in use (live pairs and the self block)
+  if (c < 6 * a.h.m && c >= 6 * count0) return;
+  const double *colp = a.rows + (long long)c * a.nb;
+  double v[8];
+  double s = 0.0;
+  for (int r0 = t; r0 < a.nb; r0 += 256 * 8) {
 #pragma unroll
-    for (int r = 0; r < TAIL_GROUP; ++r) // every load in flight at once (clamped rows, masked below)
-      v[r] = __hip_atomic_load(src + (r < gsize ? r : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    double sum = 0.0;
-#pragma unroll
-    for (int r = 0; r < TAIL_GROUP; ++r)
-      if (r < gsize) sum += v[r];
-    __hip_atomic_store(&a.grows[(long long)col * ngroups + grp], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
-  if (t == 0) {
-    unsigned *cnt = a.cols_done + ngroups;
-    const bool last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == unsigned(ngroups - 1);
-    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = last ? 1 : 0;
-  }
-  lds_barrier();
-  if (!s_last) return;
-  KT(55);
-  for (int col = t; col < a.nc; col += 256) {
-    if (!used(col)) continue;
-    const double *src = a.grows + (long long)col * ngroups;
-    double sum = 0.0;
-    for (int r0 = 0; r0 < ngroups; r0 += 8) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        v[u] = __hip_atomic_load(src + (r0 + u < ngroups ? r0 + u : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (r0 + u < ngroups) sum += v[u];
+    for (int u = 0; u < 8; ++u) { // unconditional loads from clamped rows: all eight in flight at once
+      const int r = r0 + 256 * u;
+      v[u] = colp[r < a.nb ? r : 0];
     }
-    __hip_atomic_store(&a.dots[col], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += (r0 + 256 * u < a.nb) ? v[u] : 0.0;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier(); // the staging area is free: the history step's dyn area goes over it
-  tail_fin_body(a, pool);
+  s = t_wave_sum(s);
+  if ((t & 63) == 0) ws[t >> 6] = s;
+  lds_barrier();
+  if (t == 0) {
+    const double d = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+    __hip_atomic_store(&a.dots[c], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 }
 
 constexpr int TF_THREADS = 256;
@@ -295,9 +253,9 @@ constexpr int TF_THREADS = 256;
 // Wave 0 (decision, then the recurrences) issues no global store until the coefficients: the status
 // block, the host record (system-scope stores to host-mapped memory, whose acknowledgement the
 // sequence word must wait for) and the history step's ring/Gram writes are made by waves 1..3.
-// dyn: LDS for sy [2*m*m] (SY and its transpose) | yy [m*m] | SY, YY [S*S] | rho [S] (tail_fin_doubles(m)).
-__device__ __forceinline__ void tail_fin_body(const TailArgs &a, double *dyn) {
+__device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
   const RedAllArgs &ra = a.ra;
+  extern __shared__ double dyn[]; // sy [2*m*m] (SY and its transpose) | yy [m*m] | SY, YY [S*S] | rho [S]
   __shared__ HistSmem sm;
   __shared__ double v[4];
   __shared__ double s_rec[4]; // loss, tgg, alpha0, accept_prev
@@ -418,6 +376,22 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a, double *dyn) {
   KT(44);
 }
 
+// tail_cols, then (cols_done) the last block to finish runs the one-block fin: one launch fewer on
+// the iteration's critical path. Hand-off without fences (the guide prices __threadfence at ~3.5 us):
+// each block's column sum is an sc1 (write-through) store waited for with vmcnt(0) before the same lane's
+// agent-scope add; the block whose add returns the last count reads the sums with sc1 loads.
+__global__ __launch_bounds__(TF_THREADS) void tail_cols_fin_kernel(const TailArgs a) {
+  if (a.ra.abort && *a.ra.abort) return; // uniform for the launch: nobody arrives, the counter stays 0
+  tail_cols_body(a);
+  __shared__ int s_last;
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(a.cols_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) *a.cols_done = 0u; // ready for the next launch (stream-ordered)
+  tail_fin_body(a);
+}
+
 } // namespace
 
 int tail_vpw(int m) {
@@ -426,10 +400,12 @@ int tail_vpw(int m) {
   return per_wave <= 2 ? 2 : per_wave <= 4 ? 4 : per_wave <= 8 ? 8 : 16;
 }
 
+static size_t fin_shmem(const TailArgs &a) {
+  return (size_t(3) * a.h.m * a.h.m + 2 * size_t(a.h.slots) * a.h.slots + a.h.slots) * sizeof(double);
+}
+
 void tail_reduce(hipStream_t s, const TailArgs &a) {
   if (a.nb <= 0) return;
-  if (!a.cols_done || !a.grows || a.h.slots != a.h.m + 1 || a.nc > 256)
-    throw Error(2, "tail_reduce: arrival counters, group rows, m + 1 slots and <= 256 dot columns");
   switch (tail_vpw(a.h.m)) {
   case 2: hipLaunchKernelGGL(tail_reduce_kernel<2>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
   case 4: hipLaunchKernelGGL(tail_reduce_kernel<4>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
@@ -437,6 +413,9 @@ void tail_reduce(hipStream_t s, const TailArgs &a) {
   case 16: hipLaunchKernelGGL(tail_reduce_kernel<16>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
   default: throw Error(2, "tail_reduce: history size not supported by the fused tail");
   }
+  LBF_KERNEL_CHECK();
+  if (!a.cols_done) throw Error(2, "tail_reduce: needs the arrival counter (cols_done)");
+  hipLaunchKernelGGL(tail_cols_fin_kernel, dim3(unsigned(a.nc)), dim3(TF_THREADS), fin_shmem(a), s, a);
   LBF_KERNEL_CHECK();
 }
 
