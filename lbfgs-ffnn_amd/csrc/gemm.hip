@@ -913,8 +913,6 @@ template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const G
     launch<2, 2, 1, 2, AKC, BKC, EPI, 1, 2, 3>(s, d);
   } else if (d.tile == TILE_64x64) { // 64 x 64 (16 KB per stage)
     launch<2, 2, 1, 1, AKC, BKC, EPI, 1, 2, 5>(s, d);
-  } else if (d.tile == TILE_128x128K2) { // 128 x 128, two k-groups, one workgroup per CU (4 stages, 128 KB)
-    launch<2, 2, 2, 2, AKC, BKC, EPI, 2, 1, 4>(s, d);
   } else if (d.N > 64) { // 128 x 128 (32 KB per stage)
     launch<2, 2, 2, 2, AKC, BKC, EPI, 1, 2, 2>(s, d);
   } else if (d.N > 32) launch<2, 2, 2, 1, AKC, BKC, EPI, 1, 1, 3>(s, d); // 128 x 64 (24 KB per stage)
@@ -936,11 +934,6 @@ void gemm_tile_for(int N, int tile, int *BM, int *BN) {
   }
   if (tile == TILE_64x128) {
     *BM = 64;
-    *BN = 128;
-    return;
-  }
-  if (tile == TILE_128x128K2) {
-    *BM = 128;
     *BN = 128;
     return;
   }

@@ -23,9 +23,8 @@ enum Act : int { ACT_LINEAR = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_SIGMOID = 3 };
 // ------------------------------------------------------------------------------------------------
 // Tile shapes: TILE_AUTO = 128 rows x (128 | 64 | 32 by N); TILE_32x128 (few row tiles: a rank's
 // shard); TILE_64x64 (split-K weight gradients with fewer, longer splits); TILE_64x128 (mid-size
-// shards: two workgroups per CU where 128-row tiles would leave one); TILE_128x128K2 (128 x 128 with two
-// k-groups of four waves, one workgroup per CU: a long split-K weight gradient in half the slabs).
-enum GemmTile : int { TILE_AUTO = 0, TILE_32x128 = 1, TILE_64x64 = 2, TILE_64x128 = 3, TILE_128x128K2 = 4 };
+// shards: two workgroups per CU where 128-row tiles would leave one).
+enum GemmTile : int { TILE_AUTO = 0, TILE_32x128 = 1, TILE_64x64 = 2, TILE_64x128 = 3 };
 enum GemmEpi : int { EPI_FWD = 0, EPI_DX = 1, EPI_STORE = 2, EPI_HEAD = 3 };
 
 struct GemmDesc {

@@ -96,7 +96,6 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
   }
   nparams_ = off;
   if (const char *e = std::getenv("LBF_NO_FOLD")) fold_on_ = e[0] != '1'; // tests: the unfolded route
-  dw_k2_ = env_int("LBF_DW_K2", 1) != 0; // A/B of TILE_128x128K2 (round 4 measurement; removed after)
   rowhead_on_ = env_int("LBF_ROWHEAD", 1) != 0; // A/B of the row head (round 4 measurement; removed after)
 }
 
@@ -192,11 +191,8 @@ void Mlp::plan(long long B) {
     // (S-LBFGS minibatches, K = 128 / 256 rows) take 64x64 tiles at any width: four times the tiles of
     // 128x128 at the same K, where 128x128 tiles filled a fifth of the chip (784 -> 512: 56 workgroups).
     L.dtile = ((L.out <= 128 && L.in + 1 <= 1024 && B <= 16384) || B <= DW_SMALL_BATCH) ? TILE_64x64 : TILE_AUTO;
-    // Long K over a layer at least 128 wide (cfg 2's 784 -> 128 at 60000 rows): 128 x 128 tiles with two
-    // k-groups, one workgroup per CU, so each output element is summed from half the split-K slabs that two
-    // 4-wave workgroups per CU need (cfg 2: 39 slabs instead of 82, 33 -> 16 MB for the tail to read); the
-    // MFMA work per CU is the same
-    if (L.dtile == TILE_AUTO && L.out > 64 && B > 16384 && B % 4 == 0 && dw_k2_) L.dtile = TILE_128x128K2;
+    // (128 x 128 tiles with two k-groups and one workgroup per CU, half the split-K slabs, measured slower at
+    // cfg 2: dW 128.5 against 112.2 us, profiles/r04/a/bench_400{,_nok2}.json; not kept)
   }
   // The last hidden layer's dW GEMM has in + 1 rows; when they pass a multiple of its tile height by
   // at most 16 input columns + the bias row (784 + 1 = 6 x 128 + 17 at cfg 2), those rows go to the
@@ -230,8 +226,7 @@ void Mlp::plan(long long B) {
       if (fold_ >= 0 && l == nl - 2) cols += (long long)(fold_ + 1) * L.out;
       side = cdiv(cdiv(cols, 256), tiles) * tiles; // gemm.hip SIDE_COLS per side block
     }
-    const long long lslots = L.dtile == TILE_128x128K2 ? slots / 2 : slots; // one workgroup per CU
-    long long splits = split_factor(tiles, B, min_chunk, std::max(lslots - side, lslots / 2), M * L.out);
+    long long splits = split_factor(tiles, B, min_chunk, std::max(slots - side, slots / 2), M * L.out);
     long long kc = cdiv(cdiv(B, splits), 32) * 32;
     if (kc <= 0) kc = 32;
     splits = std::max(1LL, cdiv(B, kc));
