@@ -113,7 +113,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
   const double *dots = sm.dots;
   const double *self = dots + 6 * h.m;
   const double *SYsrc = LDS ? a.SY : h.SY, *YYsrc = LDS ? a.YY : h.YY, *rhosrc = LDS ? a.rho : h.rho;
-  KT(56);
+  KTF(56);
   // Gram rows of the new pair and the g-dots -> global (consumed by later steps); u / nu: this
   // thread's index among the writers
   auto write_rows = [&](int u, int nu) {
@@ -190,7 +190,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
     }
     if (!FUSED) h.scal[SC_COUNT] = double(count);
     sm.k = count;
-    KT(57);
+    KTF(57);
   }
   lds_barrier();
   // ---- C1: stage the live quantities ----
@@ -283,7 +283,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
     sm.rho_l[i] = fresh ? sm.rhow : hc_ld<LDS>(rhosrc, j);
   }
   lds_barrier();
-  KT(59);
+  KTF(59);
   if (wave != 0) {
     if constexpr (FUSED) { // the deferred writes of step B (the live count: wave 0, below)
       const int u = t - 64, nu = nt - 64;
@@ -329,7 +329,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
     // each step is VALU + v_readlane only.
     const double rho_me = lane < k ? rho_l[lane] : 0.0;
     double r = lane < k ? gS_l[lane] : 0.0;
-    KT(63);
+    KTF(63);
     KTC(64);
     for (int i0 = k - 1; i0 >= 0; i0 -= 8) { // backward: alpha_i = rho_i (gS_i - sum_{j>i} alpha_j SY[i][j])
       double col[8];
@@ -349,7 +349,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
       }
     }
     KTC(65);
-    KT(60);
+    KTF(60);
     double acc = lane < k ? gY_l[lane] : 0.0; // gY_l - sum_j alpha_j YY[l][j]  (YY symmetric)
     for (int j0 = 0; j0 < k; j0 += 8) {
       double yv[8];
@@ -407,7 +407,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
         }
       }
     }
-    KT(60);
+    KTF(60);
     double acc0 = in0 ? gY_l[l0] : 0.0, acc1 = in1 ? gY_l[l1] : 0.0; // gY_l - sum_j alpha_j YY[l][j]
     for (int j0 = 0; j0 < k; j0 += 8) {
       double y0v[8], y1v[8];
@@ -465,7 +465,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
       if (lane < i) r0v -= ai * (sy_t ? syT[i * k + lane] : sy[lane * k + i]);
       if (lane + 64 < i) r1v -= ai * (sy_t ? syT[i * k + lane + 64] : sy[(lane + 64) * k + i]);
     }
-    KT(60);
+    KTF(60);
     double t0v = 0.0, t1v = 0.0;
     {
       double acc0 = lane < k ? gY_l[lane] : 0.0, acc1 = lane + 64 < k ? gY_l[lane + 64] : 0.0;
@@ -488,7 +488,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
       if (lane + 64 > i && lane + 64 < k) t1v += ci * sy[i * k + lane + 64];
     }
   }
-  KT(61);
+  KTF(61);
   const double ds = a.dsign;
   double part = 0.0;
   if (lane < k) part += c0 * gS_l[lane] - gamma * al0 * gY_l[lane];
@@ -519,7 +519,7 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
     h.scal[SC_GAMMA] = gamma;
     h.scal[SC_ALPHA0] = (a.iter == 0) ? fmin(1.0, 1.0 / sqrt(gg)) : 1.0;
   }
-  KT(62);
+  KTF(62);
 }
 
 } // namespace lbf

@@ -111,6 +111,11 @@ static __device__ unsigned long long lbf_kt_buf[256]; // one per translation uni
   do {                                                                                                  \
     if ((blockIdx.x | blockIdx.y | blockIdx.z | threadIdx.x) == 0) lbf_kt_buf[slot] = clock64();                              \
   } while (0)
+// KTF(slot): thread 0 of whichever block runs it (one-block phases: the tail's fin, hist_core)
+#define KTF(slot)                                                                                       \
+  do {                                                                                                  \
+    if (threadIdx.x == 0) lbf_kt_buf[slot] = wall_clock64();                                            \
+  } while (0)
 // KTB(slot): per-block stamps (thread 0 of every block with blockIdx.z == 0, first 1024 blocks) for
 // the distribution of phase times across the grid.
 static __device__ unsigned long long lbf_kt_blk[8 * 1024];
@@ -120,6 +125,9 @@ static __device__ unsigned long long lbf_kt_blk[8 * 1024];
     if (threadIdx.x == 0 && blockIdx.z == 0 && lin_ < 1024) lbf_kt_blk[(slot) * 1024 + lin_] = wall_clock64(); \
   } while (0)
 #else
+#define KTF(slot)                                                                                       \
+  do {                                                                                                  \
+  } while (0)
 #define KTB(slot)                                                                                       \
   do {                                                                                                  \
   } while (0)

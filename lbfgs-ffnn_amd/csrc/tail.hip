@@ -267,7 +267,7 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
   const int m = h.m, S_ = h.slots;
   double *SYp = dyn + 3 * m * m, *YYp = SYp + S_ * S_, *rhop = YYp + S_ * S_;
   double *sc = h.scal;
-  KT(40);
+  KTF(40);
   // ---- prefetch (one round trip) ----
   double sse = 0.0;
   if (!a.hilo)
@@ -289,9 +289,9 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
   }
   sse = t_wave_sum(sse);
   if (lane == 0) v[wave] = sse;
-  KT(45);
+  KTF(45);
   lds_barrier();
-  KT(46);
+  KTF(46);
   if (t == 0) { // decide (LDS only: wave 0 issues no global store before the recurrences)
     const double *D = sm.dots;
     const double sse_t = a.hilo ? (double(a.hilo[0]) + double(a.hilo[1])) : ((v[0] + v[1]) + v[2]) + v[3];
@@ -327,7 +327,7 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
     s_status = !ok ? SPEC_REJECT : (conv ? SPEC_CONVERGED : SPEC_ACCEPT);
   }
   lds_barrier();
-  KT(41);
+  KTF(41);
   // status block, abort flag and host record: payload, then (after its acknowledgement) the
   // sequence word. Written by wave 1 after its last barrier (see hist_core<true>).
   auto publish = [&]() {
@@ -368,12 +368,12 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
   st.SY = SYp;
   st.YY = YYp;
   hist_prologue<true>(st, sm, ist_l[IST_WSLOT]);
-  KT(42);
-  KT(43);
+  KTF(42);
+  KTF(43);
   hist_core<true>(st, sm, dyn, 2 * m * m, dyn + 2 * m * m, m * m);
   // waves 1..3 leave hist_core after its deferred stores; wave 1 then publishes
   if (t == 64) publish();
-  KT(44);
+  KTF(44);
 }
 
 // tail_cols, then (cols_done) the last block to finish runs the one-block fin: one launch fewer on
@@ -382,6 +382,7 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
 // agent-scope add; the block whose add returns the last count reads the sums with sc1 loads.
 __global__ __launch_bounds__(TF_THREADS) void tail_cols_fin_kernel(const TailArgs a) {
   if (a.ra.abort && *a.ra.abort) return; // uniform for the launch: nobody arrives, the counter stays 0
+  KT(39);
   tail_cols_body(a);
   __shared__ int s_last;
   if (threadIdx.x == 0)

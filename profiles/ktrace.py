@@ -6,7 +6,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["LBF_LIB_PATH"] = os.path.join(ROOT, "lbfgs-ffnn_amd", "build", "ktrace", "liblbfgs_amd.so")
+os.environ["LBF_LIB_PATH"] = os.path.join(ROOT, "lbfgs-ffnn_amd", "build", "ktrace", "liblbfgs_amd_abi3.so")
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402,F401
 import __graft_entry__  # noqa: E402
@@ -62,6 +62,15 @@ def main():
         e2 = [(blk[6 * 1024 + i] - t0) / 100 for i in hi]
         print(f"tail_reduce blocks >=1024 ({len(hi)}): start {min(s2):.2f}/{q(s2):.2f}/{max(s2):.2f}  "
               f"end {min(e2):.2f}/{q(e2):.2f}/{max(e2):.2f}")
+    # the tail's timeline on its last launch, from the first tail_reduce block's start
+    endr = max(x for x in S[4] if x) if any(S[4]) else 0
+    marks = [("reduce end (last block)", endr), ("cols_fin block0 start", tbuf[39]), ("fin start", tbuf[40]),
+             ("fin prefetch issued", tbuf[45]), ("fin loads landed", tbuf[46]), ("decision", tbuf[41]),
+             ("hist prologue", tbuf[42]), ("hist_core start", tbuf[56]), ("push", tbuf[57]),
+             ("staged", tbuf[59]), ("bwd loop start", tbuf[63]), ("bwd loop end", tbuf[60]), ("fwd loop end", tbuf[61]),
+             ("coef stored", tbuf[62]), ("fin end", tbuf[44])]
+    print("tail timeline (us from the first tail_reduce block's start):",
+          "  ".join(f"{n} {(v - t0) / 100:.2f}" for n, v in marks if v))
     for name, rg in GROUPS.items():
         t0 = buf[rg[0]]
         print(name, " ".join(f"{(buf[i] - t0) / 100.0:.2f}" for i in rg))

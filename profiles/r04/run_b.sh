@@ -31,4 +31,7 @@ cd /tmp && \
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/pmc_fetch.json 2> $O/pmc_fetch.err && \
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/pmc_write.json 2> $O/pmc_write.err && \
 cd $R && python3 profiles/collect_pmc.py $O/pmc_fetch $O/pmc_write --section "gemm_fwd[0]" --kernel "$K" --config 784,128,10:60000:1 --out $O/pmc_traffic.json || { echo "pmc failed"; exit 1; }
-echo "rc=0"
+echo "main steps ok"
+KT_N=7500 timeout -k 10 120 python3 profiles/ktrace.py > $O/ktrace_7500.txt 2>&1 && \
+KT_N=60000 timeout -k 10 120 python3 profiles/ktrace.py > $O/ktrace_60000.txt 2>&1 || { echo "ktrace failed"; exit 1; }
+echo "ktrace ok"

@@ -88,10 +88,14 @@ def test_dp_lbfgs_full_size(ctx, dp_ctx, pkg):
     assert np.allclose(out[0]["loss"], out[1]["loss"], rtol=1e-9, atol=0)
 
 
-def test_dp_slbfgs_equals_single(ctx, dp_ctx, pkg):
+@pytest.mark.parametrize("dp_mode", ["sliced", "replicated"])
+def test_dp_slbfgs_equals_single(ctx, dp_ctx, pkg, dp_mode):
+    """Both S-LBFGS data-parallel modes through a 1-rank communicator against the single route: sliced (every
+    inner step's gradients through the collective) and replicated (the inner steps without it, only the
+    epoch's full-batch gradient through it)."""
     dims, acts = [784, 16, 10], ["relu", "linear"]
     Xh, Yh = pkg.synth_mnist(512)
-    kw = dict(M=5, L=4, b=32, b_H=16, step=0.02, max_epochs=2, tol=0.0, lam=1e-4)
+    kw = dict(M=5, L=4, b=32, b_H=16, step=0.02, max_epochs=2, tol=0.0, lam=1e-4, dp_mode=dp_mode)
     out = []
     for c in (ctx, dp_ctx):
         net = pkg.Mlp(c, dims, acts)
@@ -104,15 +108,18 @@ def test_dp_slbfgs_equals_single(ctx, dp_ctx, pkg):
     assert np.linalg.norm(P1 - Pd) <= 1e-6 * np.linalg.norm(P1)
 
 
-def test_dp_slbfgs_cfg4_bitwise(ctx, dp_ctx, pkg):
-    """BASELINE cfg 4's shape (784-512-256-10, b = 256, b_H = 128, L = M = 10) for one epoch over 12800 rows:
-    the data-parallel route (both minibatch gradients of a step in one [g(w_t) | g(w)] all-reduce, the
-    twin's anchor gradients one step ahead, the FD pair in one [g(u+eps s) | g(u-eps s)] all-reduce) against
-    the single route: the same parameters bit for bit (s_lbfgs.hpp:218-262)."""
+@pytest.mark.parametrize("dp_mode", ["sliced", "replicated"])
+def test_dp_slbfgs_cfg4_bitwise(ctx, dp_ctx, pkg, dp_mode):
+    """BASELINE cfg 4's shape (784-512-256-10, b = 256, b_H = 128, L = M = 10) for two epochs over 12800 rows:
+    the data-parallel routes against the single route, the same parameters bit for bit (s_lbfgs.hpp:218-262).
+    Sliced: both minibatch gradients of a step in one [g(w_t) | g(w)] all-reduce, the twin's anchor gradients
+    one step ahead, the FD pair in one [g(u+eps s) | g(u-eps s)] all-reduce. Replicated: the whole inner-step
+    chain without a collective (the free-running twin included), the full-batch gradient at each anchor
+    through the collective."""
     dims, acts = [784, 512, 256, 10], ["relu", "relu", "linear"]
     Xh, Yh = pkg.synth_mnist(12800)
     X, Y = dev(Xh), dev(Yh)
-    kw = dict(M=10, L=10, b=256, b_H=128, step=0.005, max_epochs=1, tol=0.0, lam=1e-4)
+    kw = dict(M=10, L=10, b=256, b_H=128, step=0.005, max_epochs=2, tol=0.0, lam=1e-4, dp_mode=dp_mode)
     out = []
     for c in (ctx, dp_ctx):
         net = pkg.Mlp(c, dims, acts)
@@ -123,7 +130,7 @@ def test_dp_slbfgs_cfg4_bitwise(ctx, dp_ctx, pkg):
     assert torch.equal(P1, Pd)
     assert np.array_equal(h1["accepted"], hd["accepted"])
     assert i1.n_evals == idd.n_evals and i1.n_rows == idd.n_rows
-    assert abs(h1["loss"][0] - hd["loss"][0]) <= 1e-12 * abs(h1["loss"][0])
+    assert np.all(np.abs(h1["loss"] - hd["loss"]) <= 1e-12 * np.abs(h1["loss"]))
 
 
 def test_batch_grads_equal_per_minibatch_loss_grad(ctx, pkg):

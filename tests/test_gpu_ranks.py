@@ -226,6 +226,10 @@ def test_ranks_empty_share_lbfgs(ctx, pkg):
     # NaN on both routes; one-row SVRG steps with FD pairs part at the rounding level: tol 5 %)
     (2, dict(M=5, L=4, b=1, b_H=1, step=0.002, rtol=5e-2)),
     (2, dict(M=5, L=4, b=32, b_H=1, hvp_exact=1)),  # exact HVP with b_H < world
+    # replicated inner steps: identical chains on every rank, the full-batch gradient sharded
+    (2, dict(M=5, L=4, b=32, b_H=16, dp_mode="replicated")),
+    (3, dict(M=5, L=4, b=32, b_H=16, dp_mode="replicated")),
+    (4, dict(M=5, L=4, b=32, b_H=1, hvp_exact=1, dp_mode="replicated")),
 ])
 def test_ranks_slbfgs_equals_single(ctx, pkg, world, kw):
     dims, acts, N = [784, 16, 10], ["relu", "linear"], 512 if kw["b"] > 1 else 64
@@ -233,7 +237,7 @@ def test_ranks_slbfgs_equals_single(ctx, pkg, world, kw):
     X, Y = dev(Xh), dev(Yh)
     kw = dict(kw)
     rtol = kw.pop("rtol", 1e-3)
-    args = dict(step=0.02, max_epochs=2, tol=0.0, lam=1e-4)
+    args = dict(step=0.02, max_epochs=2, tol=0.0, lam=1e-4, dp_mode="sliced")
     args.update(kw)
     net1 = pkg.Mlp(ctx, dims, acts)
     P0 = net1.init_params(123, "cpu")
@@ -258,15 +262,17 @@ def test_ranks_slbfgs_equals_single(ctx, pkg, world, kw):
     assert rel(host(res[0][1]), host(P1)) <= 10 * rtol
 
 
-def test_ranks_cfg4_epoch(ctx, pkg):
+@pytest.mark.parametrize("dp_mode", ["sliced", "replicated"])
+def test_ranks_cfg4_epoch(ctx, pkg, dp_mode):
     """BASELINE cfg 4 (784-512-256-10, N = 60000, b = 256, b_H = 128, L = M = 10) for one epoch at world 2
-    against the single route: the twin's anchor gradients ahead and ONE all-reduce per [g(w_t) | g(w)]
-    block; same number of live curvature pairs, epoch loss within 5 % (234 SVRG steps with FD pairs are
-    chaotic at the rounding level: tests/test_gpu_fullsize.py), ranks bitwise identical."""
+    against the single route. Sliced: the twin's anchor gradients ahead and ONE all-reduce per [g(w_t) | g(w)]
+    block. Replicated: every rank runs the whole chain, the full-batch gradient at the anchor is sharded.
+    Same number of live curvature pairs, epoch loss within 5 % (234 SVRG steps with FD pairs are chaotic at
+    the rounding level: tests/test_gpu_fullsize.py), ranks bitwise identical."""
     dims, acts, N, world = [784, 512, 256, 10], ["relu", "relu", "linear"], 60000, 2
     Xh, Yh = pkg.synth_mnist(N)
     X, Y = dev(Xh), dev(Yh)
-    args = dict(M=10, L=10, b=256, b_H=128, step=0.005, max_epochs=1, tol=0.0, lam=1e-4)
+    args = dict(M=10, L=10, b=256, b_H=128, step=0.005, max_epochs=1, tol=0.0, lam=1e-4, dp_mode=dp_mode)
     net1 = pkg.Mlp(ctx, dims, acts)
     P0 = net1.init_params(123, "cpu")
     P1 = P0.clone()
@@ -284,4 +290,8 @@ def test_ranks_cfg4_epoch(ctx, pkg):
     assert np.isfinite(h["loss"][0])
     assert h["accepted"][0] == h1["accepted"][0]
     assert abs(h["loss"][0] - h1["loss"][0]) <= 0.05 * abs(h1["loss"][0])
-    assert res[0][2] + res[1][2] == i1.n_rows  # the ranks' slices partition the single route's rows
+    if dp_mode == "sliced":
+        assert res[0][2] + res[1][2] == i1.n_rows  # the ranks' slices partition the single route's rows
+    else:  # every rank evaluates every minibatch row; the two full-batch evaluations are split
+        full = 2 * N
+        assert res[0][2] + res[1][2] == 2 * (i1.n_rows - full) + full
