@@ -74,40 +74,96 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
       zero_mask |= 1u << j;
     }
   }
-  if (wave == 0) { // the new vectors of the group (null operands read ga / sa and are masked)
-    const float *dflt = g.has_g ? g.ga : g.sa;
-    const float ysc = float(g.yscale);
-    // g.ga from its split-K slabs (gred_on): this lane's 4Q columns, every slab value loaded before the sums
-    f32x4 gfin[Q];
-    if (a.gred_on) {
-      const RedAllArgs &R = a.gred;
+  // g.ga from its split-K slabs (gred_on): wave w sums the splits k = w (mod 4) of this lane's quads in split
+  // order (reduce_all_kernel's stripes) into LDS; wave 0 adds the four stripes after the barrier,
+  // ((0 + 1) + 2) + 3 as reduce_all does: bitwise its gradient. History::update defers only segment tables
+  // whose offsets, counts and strides are multiples of 4 floats (16-B aligned slabs), so a lane's quad lies
+  // in one segment and is one 16-B load per split. The segment is found by a loop over the (kernel-argument)
+  // table with a wave-uniform index: no lane waits on a load of the table.
+  __shared__ double gpart[4][TC];
+  auto seg_of = [&](long long e, const float *&base, long long &col, long long &strd, int &nsp) {
+    const RedAllArgs &R = a.gred;
+    base = R.G;
+    col = e;
+    strd = 0;
+    nsp = 0;
+    for (int si = 0; si < R.nseg; ++si) {
+      const RedSeg &S = R.seg[si];
+      if (e >= S.goff) {
+        const bool sp = S.splits > 0;
+        base = sp ? S.slab : R.G;
+        col = sp ? e - S.goff : e;
+        strd = sp ? S.stride : 0;
+        nsp = S.splits;
+      }
+    }
+  };
+  if (a.gred_on) { // (History::update: has_g, no pair)
+    const RedAllArgs &R = a.gred;
+    int kmax = 0;
+    for (int si = 0; si < R.nseg; ++si) kmax = max(kmax, R.seg[si].splits);
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) gpart[wave][256 * q + 4 * lane + c] = 0.0;
+    for (int k0 = wave; k0 < kmax; k0 += 4) { // one round trip per four splits
+      f32x4 x[Q];
+      int nsp[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) { // unconditional, clamped into the quad's slabs (or G itself)
+        const float *base;
+        long long col, strd;
+        seg_of(e4[q], base, col, strd, nsp[q]);
+        const int kc = min(k0, max(nsp[q] - 1, 0));
+        x[q] = *reinterpret_cast<const f32x4 *>(base + col + (long long)kc * strd);
+      }
 #pragma unroll
       for (int q = 0; q < Q; ++q)
+        if (k0 < nsp[q])
+#pragma unroll
+          for (int c = 0; c < 4; ++c) gpart[wave][256 * q + 4 * lane + c] += double(x[q][c]);
+    }
+    lds_barrier();
+    if (wave == 0) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const float *base;
+        long long col, strd;
+        int nsp;
+        seg_of(e4[q], base, col, strd, nsp);
+        const f32x4 gw = *reinterpret_cast<const f32x4 *>(R.G + e4[q]); // unsplit segments: G as written
+        // the other operands of v = g - gb + gc (null operands read G, masked)
+        const f32x4 gb4 = *reinterpret_cast<const f32x4 *>((g.gb ? g.gb : R.G) + e4[q]);
+        const f32x4 gc4 = *reinterpret_cast<const f32x4 *>((g.gc ? g.gc : R.G) + e4[q]);
+        float ww[4] = {0.f, 0.f, 0.f, 0.f};
+        if (R.l2 && R.lambda != 0.0) // uniform; w is exactly n long
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ww[c] = R.w[min(e4[q] + c, h.n - 1)];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const long long e = e4[q] + c;
-          int si = 0;
-          while (si + 1 < R.nseg && R.seg[si + 1].goff <= e) ++si;
-          const RedSeg &S = R.seg[si];
-          const long long col = min(e - S.goff, S.count - 1); // padding columns (masked later) stay in bounds
-          float gv;
-          if (S.splits > 0) {
-            double st[4] = {0.0, 0.0, 0.0, 0.0};
-            const float *src = S.slab + col;
-            for (int k = 0; k < S.splits; ++k) st[k & 3] += double(src[(long long)k * S.stride]);
-            gv = float(((st[0] + st[1]) + st[2]) + st[3]);
-          } else {
-            gv = R.G[e];
+          const int qq = 256 * q + 4 * lane + c;
+          float gv = 0.f;
+          if (live[q][c]) {
+            gv = nsp > 0 ? float(((gpart[0][qq] + gpart[1][qq]) + gpart[2][qq]) + gpart[3][qq]) : gw[c];
+            if (R.l2 && R.lambda != 0.0) gv = gv + float(R.lambda) * ww[c]; // finalize_kernel's update
+            if (g.gb) gv = gv - gb4[c];
+            if (g.gc) gv = gv + gc4[c];
+            if (g.g_out) g.g_out[col0[q] + c] = gv;
           }
-          if (R.l2 && R.lambda != 0.0) gv = gv + float(R.lambda) * R.w[e]; // finalize_kernel's update
-          gfin[q][c] = gv;
+          ops[0][qq] = 0.f;
+          ops[1][qq] = 0.f;
+          ops[2][qq] = gv;
         }
+      }
     }
+  } else if (wave == 0) { // the new vectors of the group (null operands read ga / sa and are masked)
+    const float *dflt = g.has_g ? g.ga : g.sa;
+    const float ysc = float(g.yscale);
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       auto ld4 = [&](const float *p) { return *reinterpret_cast<const f32x4 *>((p ? p : dflt) + e4[q]); };
       const f32x4 sa = ld4(g.sa), sb = ld4(g.sb), ya = ld4(g.ya), yb = ld4(g.yb);
-      const f32x4 ga = a.gred_on ? gfin[q] : ld4(g.ga), gb = ld4(g.gb), gc = ld4(g.gc);
+      const f32x4 ga = ld4(g.ga), gb = ld4(g.gb), gc = ld4(g.gc);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int qq = 256 * q + 4 * lane + c;

@@ -177,20 +177,27 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
 }
 
 // Row head (RowHeadArgs): wave w of the block takes rows (4 blockIdx + w) rpw + r; lane l owns hidden
-// columns l + 64 j, j < NJ. Per row: the activations from the split-K slabs (every slab value of the row
-// loaded before the sums), Z = a W + b reduced across the wave in fp64 (DPP), the loss and dZ (every
-// lane holds the row's dZ), delta = (dZ W^T) .* act_prev'(a) stored, [dW ; db] accumulated per lane in
-// fp32; at the end the four waves' partials are summed in wave order into the block's slab.
-template <int NJ>
+// columns l + 64 j, j < NJ; OP = Out rounded up to 4 (register arrays sized by it). Per row: the target row
+// (through idx) and every slab value of the row's activations are requested before the first use (one
+// round trip; rounds of 8 splits beyond that), then the activations in fwd_reduce_act's arithmetic (slabs
+// summed in split order, fp32), Z = a W + b reduced across the wave in fp64 (DPP), the loss and dZ (every
+// lane holds the row's dZ), delta = (dZ W^T) .* act_prev'(a) stored, and the row's [a | 1]^T dZ added into
+// the wave's LDS partial (fp32, row order: what a register accumulator would hold); at the end the four
+// waves' partials are summed in wave order into the block's slab.
+template <int NJ, int OP>
 __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
   if (a.abort && *a.abort) return;
   extern __shared__ __attribute__((aligned(16))) float red[]; // [4][(H + 1) * Out]
   __shared__ double ssew[4];
+  constexpr int SU = 8; // splits per column in flight per round
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int H = a.H, Out = a.Out, per = (H + 1) * Out;
   const long long rbase = ((long long)blockIdx.x * 4 + wave) * a.rpw;
-  // the output layer's weights of this lane's columns, both biases (clamped loads, masked values)
-  float w2[NJ][HMAX_OUT], hb[NJ];
+  // the output layer's weights of this lane's columns, both biases: unconditional loads from clamped
+  // addresses, NOT masked (a masked load compiles to a branch around it and a wait inside, one round trip
+  // per value). The clamped entries only ever meet zeros: av = 0 on columns past H, dZ = 0 on outputs past
+  // Out, and those products are never stored.
+  float w2[NJ][OP], hb[NJ];
   bool cv[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -199,53 +206,58 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
     const int cc = cv[j] ? c : H - 1;
     hb[j] = a.hbias[cc];
 #pragma unroll
-    for (int o = 0; o < HMAX_OUT; ++o) {
-      const float v = a.P[(long long)cc * Out + (o < Out ? o : Out - 1)];
-      w2[j][o] = (cv[j] && o < Out) ? v : 0.0f;
-    }
+    for (int o = 0; o < OP; ++o) w2[j][o] = a.P[(long long)cc * Out + (o < Out ? o : Out - 1)];
   }
-  float b2[HMAX_OUT];
+  float b2[OP], dbacc[OP];
 #pragma unroll
-  for (int o = 0; o < HMAX_OUT; ++o) b2[o] = a.P[(long long)H * Out + (o < Out ? o : Out - 1)];
-  float acc[NJ][HMAX_OUT], dbacc[HMAX_OUT];
-#pragma unroll
-  for (int o = 0; o < HMAX_OUT; ++o) {
+  for (int o = 0; o < OP; ++o) {
+    b2[o] = a.P[(long long)H * Out + (o < Out ? o : Out - 1)];
     dbacc[o] = 0.0f;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j][o] = 0.0f;
   }
+  float *mine = red + wave * per;
   double sse = 0.0;
-  for (int r = 0; r < a.rpw; ++r) {
+  int r = 0;
+  for (; r < a.rpw; ++r) {
     const long long b = rbase + r;
     if (b >= a.B) break; // wave-uniform
-    // ---- activations: fwd_reduce_act's arithmetic (slabs summed in split order, fp32) ----
+    // ---- loads: the target row first (two deep through idx), then the slabs ----
+    const long long yrow = a.idx ? (long long)a.idx[b] : b;
+    float yv[OP];
+#pragma unroll
+    for (int o = 0; o < OP; ++o) yv[o] = a.Y[yrow * Out + (o < Out ? o : Out - 1)];
+    float sum[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) sum[j] = 0.0f;
+    for (int k0 = 0; k0 < a.splits; k0 += SU) {
+      float v[NJ][SU];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float *src = a.fslab + b * H + (cv[j] ? lane + 64 * j : H - 1);
+#pragma unroll
+        for (int u = 0; u < SU; ++u) v[j][u] = src[(long long)min(k0 + u, a.splits - 1) * a.stride];
+      }
+      // every load of the round (and the targets) issued before the first use: the compiler may not sink
+      // a load into the uniform branches below
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int u = 0; u < SU; ++u)
+          if (k0 + u < a.splits) sum[j] += v[j][u];
+    }
+    // ---- activations (fwd_reduce_act's arithmetic) ----
     float av[NJ];
     with_act(a.act_prev, [&](auto AC) __attribute__((always_inline)) {
       constexpr int A = decltype(AC)::value;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int cc = cv[j] ? lane + 64 * j : H - 1;
-        const float *src = a.fslab + b * H + cc;
-        float sum = 0.0f;
-        int k = 0;
-        for (; k + 8 <= a.splits; k += 8) { // eight loads in flight, summed in split order
-          float v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = src[(long long)(k + u) * a.stride];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) sum += v[u];
-        }
-        for (; k < a.splits; ++k) sum += src[(long long)k * a.stride];
-        av[j] = cv[j] ? act_c<A>(sum + hb[j]) : 0.0f;
-      }
+      for (int j = 0; j < NJ; ++j) av[j] = cv[j] ? act_c<A>(sum[j] + hb[j]) : 0.0f;
     });
     // ---- Z = a W + b (fp64 partials, fixed DPP tree), loss, dZ: identical on every lane ----
-    const long long yrow = a.idx ? (long long)a.idx[b] : b;
-    float dz[HMAX_OUT];
+    float dz[OP];
     with_act(a.act_out, [&](auto AC) __attribute__((always_inline)) {
       constexpr int A = decltype(AC)::value;
 #pragma unroll
-      for (int o = 0; o < HMAX_OUT; ++o) {
+      for (int o = 0; o < OP; ++o) {
         dz[o] = 0.0f;
         if (o < Out) { // uniform
           double zp = 0.0;
@@ -253,7 +265,7 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
           for (int j = 0; j < NJ; ++j) zp += double(av[j]) * double(w2[j][o]);
           const float z = float(wave_sum_f64(zp));
           const float outv = act_c<A>(z + b2[o]);
-          const float d = outv - a.Y[yrow * Out + o];
+          const float d = outv - yv[o];
           sse += double(d) * double(d);
           dz[o] = d * dact_c<A>(outv) * float(a.inv_scale);
         }
@@ -266,26 +278,32 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
       for (int j = 0; j < NJ; ++j) {
         float dd = 0.0f;
 #pragma unroll
-        for (int o = 0; o < HMAX_OUT; ++o) dd += dz[o] * w2[j][o];
+        for (int o = 0; o < OP; ++o) dd += dz[o] * w2[j][o];
         if (cv[j]) a.delta[b * H + lane + 64 * j] = dd * dact_c<A>(av[j]);
-#pragma unroll
-        for (int o = 0; o < HMAX_OUT; ++o) acc[j][o] += av[j] * dz[o];
       }
     });
 #pragma unroll
-    for (int o = 0; o < HMAX_OUT; ++o) dbacc[o] += dz[o];
+    for (int j = 0; j < NJ; ++j)
+      if (cv[j]) {
+        float *row = mine + (lane + 64 * j) * Out;
+#pragma unroll
+        for (int o = 0; o < OP; ++o)
+          if (o < Out) row[o] = r == 0 ? av[j] * dz[o] : row[o] + av[j] * dz[o];
+      }
+#pragma unroll
+    for (int o = 0; o < OP; ++o) dbacc[o] += dz[o];
   }
+  if (r == 0) // a wave past the last row: zero partials
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      if (cv[j])
+#pragma unroll
+        for (int o = 0; o < OP; ++o)
+          if (o < Out) mine[(lane + 64 * j) * Out + o] = 0.0f;
   // ---- the block's slab: the four waves' partials summed in wave order ----
-  float *mine = red + wave * per;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j)
-    if (cv[j])
-#pragma unroll
-      for (int o = 0; o < HMAX_OUT; ++o)
-        if (o < Out) mine[(lane + 64 * j) * Out + o] = acc[j][o];
   if (lane == 0) {
 #pragma unroll
-    for (int o = 0; o < HMAX_OUT; ++o)
+    for (int o = 0; o < OP; ++o)
       if (o < Out) mine[H * Out + o] = dbacc[o];
     ssew[wave] = sse; // every lane holds the same sum
   }
@@ -305,23 +323,29 @@ int rowhead_nwg(long long B) { return int(cdiv(std::max(1LL, B), 4LL * rowhead_r
 void rowhead(hipStream_t s, const RowHeadArgs &a) {
   LBF_REQUIRE(rowhead_supported(a.H, a.Out) && a.splits >= 1 && a.rpw == rowhead_rpw(a.B), "rowhead: shape");
   const size_t shmem = size_t(4) * (a.H + 1) * a.Out * sizeof(float);
-  static const bool attr_set = [] { // once per process, thread-safe
-    const void *fns[] = {reinterpret_cast<const void *>(rowhead_kernel<1>),
-                         reinterpret_cast<const void *>(rowhead_kernel<2>),
-                         reinterpret_cast<const void *>(rowhead_kernel<3>),
-                         reinterpret_cast<const void *>(rowhead_kernel<4>)};
-    for (const void *f : fns) LBF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
-    return true;
-  }();
-  (void)attr_set;
+  const int nj = (a.H + 63) / 64, op = (a.Out + 3) / 4 * 4;
   const dim3 grid(unsigned(rowhead_nwg(a.B))), block(256);
-  switch ((a.H + 63) / 64) {
-  case 1: hipLaunchKernelGGL(rowhead_kernel<1>, grid, block, shmem, s, a); break;
-  case 2: hipLaunchKernelGGL(rowhead_kernel<2>, grid, block, shmem, s, a); break;
-  case 3: hipLaunchKernelGGL(rowhead_kernel<3>, grid, block, shmem, s, a); break;
-  default: hipLaunchKernelGGL(rowhead_kernel<4>, grid, block, shmem, s, a); break;
+  // <NJ, OP> for hidden widths up to 256 and outputs up to 16; the attribute once per instance (thread-safe)
+#define LBF_ROWHEAD_CASE(NJ, OP)                                                                              \
+  if (nj == NJ && op == OP) {                                                                                \
+    static const bool attr_set = [] {                                                                        \
+      LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(rowhead_kernel<NJ, OP>),                    \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));                   \
+      return true;                                                                                           \
+    }();                                                                                                     \
+    (void)attr_set;                                                                                          \
+    hipLaunchKernelGGL((rowhead_kernel<NJ, OP>), grid, block, shmem, s, a);                                  \
+    LBF_KERNEL_CHECK();                                                                                      \
+    return;                                                                                                  \
   }
-  LBF_KERNEL_CHECK();
+#define LBF_ROWHEAD_NJ(NJ) LBF_ROWHEAD_CASE(NJ, 4) LBF_ROWHEAD_CASE(NJ, 8) LBF_ROWHEAD_CASE(NJ, 12) LBF_ROWHEAD_CASE(NJ, 16)
+  LBF_ROWHEAD_NJ(1)
+  LBF_ROWHEAD_NJ(2)
+  LBF_ROWHEAD_NJ(3)
+  LBF_ROWHEAD_NJ(4)
+#undef LBF_ROWHEAD_NJ
+#undef LBF_ROWHEAD_CASE
+  throw Error(2, "rowhead: no instance for this shape");
 }
 
 bool head_supported(int H, int Out) { return Out >= 1 && Out <= HMAX_OUT && H >= 1 && H <= HMAX; }

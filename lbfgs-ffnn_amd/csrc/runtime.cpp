@@ -1068,7 +1068,15 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign, c
                        al16(g.gc) && al16(g.g_out); // 16-B lanes in dir_sweep (null pointers pass)
   const bool defer = gred && gred->nseg > 0;
   const bool dir = dir_on_ && aligned && g.policy == POL_SLBFGS && (want_dir == 0 || want_dir == 1);
-  if (defer && !(dir && g.has_g && gred->G == g.ga)) { // only the fused sweep finishes deferred slabs
+  // the sweep reads a lane's four columns of a segment's slabs as one 16-B load per split
+  bool quads = true;
+  for (int i = 0; defer && i < gred->nseg; ++i) {
+    const RedSeg &S = gred->seg[i];
+    quads = quads && S.goff % 4 == 0 && S.parts == 1 &&
+            (S.splits == 0 || (S.count % 4 == 0 && S.stride % 4 == 0 && al16(S.slab)));
+  }
+  const bool in_sweep = defer && dir && quads && g.has_g && !g.has_pair && gred->G == g.ga;
+  if (defer && !in_sweep) { // only the fused sweep finishes deferred slabs
     ProfScope ps(ctx_, PK_SLAB, 0);
     reduce_all(s, *gred);
   }
@@ -1077,7 +1085,7 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign, c
     // gram -> fold -> hist_step
     DirArgs d;
     d.g = g;
-    if (defer && g.has_g && gred->G == g.ga) { // g.ga finished inside the sweep from its split-K slabs
+    if (in_sweep) { // g.ga finished inside the sweep from its split-K slabs
       d.gred = *gred;
       d.gred_on = 1;
     }

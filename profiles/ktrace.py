@@ -44,7 +44,10 @@ def main():
     L.lbf_dbg_ktrace_tail_blk.argtypes = [C.c_void_p]
     assert L.lbf_dbg_ktrace_tail_blk(blk) == 0
     nb = 1024
-    S = [[blk[k * 1024 + i] for i in range(nb)] for k in range(5)]
+    # blocks that ran (a launch of fewer than 1024 blocks leaves the rest of the table zero)
+    ran = [i for i in range(nb) if blk[i] and blk[4 * 1024 + i]]
+    S = [[blk[k * 1024 + i] for i in ran] for k in range(5)]
+    nb = len(ran)
     t0 = min(S[0])
     q = lambda v: sorted(v)[len(v) // 2]
     names = ["header", "loads", "wave0 dots", "gram sweep"]
@@ -56,7 +59,7 @@ def main():
     en = [(x - t0) / 100 for x in S[4]]
     line.append(f"end {min(en):.2f}/{q(en):.2f}/{max(en):.2f}")
     print("tail_reduce blocks 0..1023 (min/med/max us):", "  ".join(line))
-    hi = [i for i in range(1024) if S[0][i] and blk[5 * 1024 + i] > t0 and blk[6 * 1024 + i] > blk[5 * 1024 + i]]
+    hi = [i for i in range(1024) if blk[5 * 1024 + i] > t0 and blk[6 * 1024 + i] > blk[5 * 1024 + i]]
     if hi:
         s2 = [(blk[5 * 1024 + i] - t0) / 100 for i in hi]
         e2 = [(blk[6 * 1024 + i] - t0) / 100 for i in hi]
