@@ -328,6 +328,162 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs 
   }
 }
 
+// Column sums only (the S-LBFGS direction step, followed by dir_combine_kernel): plain stores, read by the
+// next launch.
+__global__ __launch_bounds__(DF_THREADS) void dir_cols_kernel(const DirArgs a) {
+  const HistView &h = a.g.h;
+  if (h.abort && *h.abort) return;
+  __shared__ double ws[4];
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int count0 = h.ist[IST_COUNT];
+  if (c < 6 * h.m && c >= 6 * count0) return; // only the columns in use (live pairs and the self block)
+  const double *colp = a.rows + (long long)c * a.nb;
+  double v[8];
+  double s = 0.0;
+  for (int r0 = t; r0 < a.nb; r0 += DF_THREADS * 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { // unconditional loads from clamped rows: all eight in flight at once
+      const int r = r0 + DF_THREADS * u;
+      v[u] = colp[r < a.nb ? r : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += (r0 + DF_THREADS * u < a.nb) ? v[u] : 0.0;
+  }
+  s = wave_sum_f64(s);
+  if ((t & 63) == 0) ws[t >> 6] = s;
+  lds_barrier();
+  if (t == 0) a.dots[c] = ((ws[0] + ws[1]) + ws[2]) + ws[3]; // dir_cols_fin's order
+}
+
+// The S-LBFGS direction step's coefficients and its combine in one launch (direction-only steps: has_g, no
+// pair, no reset; k <= KQ live pairs). Every block stages the ring header, the dots, SY, YY and rho (one
+// round trip, with its g and x quads), issues its quads of the live history vectors, and while they are in
+// flight wave 0 runs the two-loop recurrences (recur_fast, hist_core's fast path: bitwise the same
+// coefficients); then p = sum c_i basis_i and x_out = x_in + alpha p as combine_small computes them.
+// Block 0 also makes the step's global writes (g-dots rows, coefficients, scalars: hist_core's for this
+// step), so the state after the launch is what dir_cols_fin + combine leave. Replaces dir_cols_fin's serial
+// step and the combine's header round trip on the critical path.
+template <int KQ>
+__global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const CombineArgs cb) {
+  const HistView &h = a.g.h;
+  if (h.abort && *h.abort) return;
+  constexpr int MM = DIR_MAXM, SS = DIR_MAXM + 1;
+  __shared__ double sSY[SS * SS], sYY[SS * SS], srho[SS];
+  __shared__ double sy[2 * MM * MM], yyl[MM * MM];
+  __shared__ double dl[6 * MM + 6], gS_l[MM], gY_l[MM], rho_l[MM], cf[2 * MM + 1];
+  __shared__ int Ls[MM];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int m = h.m, S_ = h.slots;
+  // ---- round trip 1: header, dots, Gram blocks, rho; this lane's g and x ----
+  const int k = __builtin_amdgcn_readfirstlane(h.ist[IST_COUNT]);
+  if (t < m) Ls[t] = h.ist[IST_ORDER + t];
+  for (int i = t; i < S_ * S_; i += 256) {
+    sSY[i] = h.SY[i];
+    sYY[i] = h.YY[i];
+  }
+  if (t < S_) srho[t] = h.rho[t];
+  if (t < 6 * m + 6) dl[t] = a.dots[t];
+  const long long n = h.n;
+  const long long e = ((long long)blockIdx.x * 256 + t) * 4;
+  const bool full = e + 3 < n;
+  const long long eq = full ? e : 0; // the vector path's quad (clamped; the tail quad goes element-wise)
+  const f32x4 g4 = *reinterpret_cast<const f32x4 *>(cb.g + eq);
+  const f32x4 x4 = *reinterpret_cast<const f32x4 *>((cb.x_out ? cb.x_in : cb.g) + eq);
+  lds_barrier();
+  // ---- round trip 2: this lane's quads of the live history vectors, in flight through the recurrences ----
+  f32x4 sv[KQ], yv[KQ];
+  if (k > 0)
+#pragma unroll
+    for (int i = 0; i < KQ; ++i) {
+      const long long off = (long long)Ls[i < k ? i : k - 1] * h.ld + eq;
+      sv[i] = *reinterpret_cast<const f32x4 *>(h.S + off);
+      yv[i] = *reinterpret_cast<const f32x4 *>(h.Y + off);
+    }
+  if (wave == 0) {
+    // stage the live pairs' Gram entries in order (hist_core C1 with no pair: L = L0, the fresh dots' rows)
+    for (int q = lane; q < k * k; q += 64) {
+      const int i = q / k, j = q - i * k;
+      const double v = sSY[Ls[i] * S_ + Ls[j]];
+      sy[q] = v;
+      sy[k * k + j * k + i] = v; // transposed copy
+      yyl[q] = sYY[Ls[i] * S_ + Ls[j]];
+    }
+    if (lane < k) {
+      gS_l[lane] = dl[6 * lane + 4];
+      gY_l[lane] = dl[6 * lane + 5];
+      rho_l[lane] = srho[Ls[lane]];
+    }
+    const double gg = dl[6 * m + 5];
+    const double gamma = k > 0 ? slbfgs_gamma(sy[(k - 1) * k + (k - 1)], yyl[(k - 1) * k + (k - 1)]) : 1.0;
+    double al0 = 0.0, c0 = 0.0;
+    recur_fast(k, lane, rho_l, gS_l, gY_l, sy, sy + k * k, yyl, gamma, al0, c0);
+    const double ds = a.dsign;
+    if (lane < k) {
+      cf[lane] = ds * c0;
+      cf[MM + lane] = ds * (-gamma * al0);
+    }
+    if (lane == 0) cf[2 * MM] = ds * gamma;
+    if (blockIdx.x == 0) { // hist_core's global writes for this step (FUSED, has_g, no pair, want_dir 1)
+      double part = 0.0;
+      if (lane < k) part += c0 * gS_l[lane] - gamma * al0 * gY_l[lane];
+      const double gTz = wave_sum_f64(part) + gamma * gg;
+      if (lane < k) {
+        const int j = Ls[lane];
+        h.gS[j] = gS_l[lane];
+        h.gY[j] = gY_l[lane];
+        h.coef[lane] = ds * c0;
+        h.coef[S_ + lane] = ds * (-gamma * al0);
+      }
+      if (lane == 0) {
+        h.coef[2 * S_] = ds * gamma;
+        h.scal[SC_RESET] = 0.0;
+        h.scal[SC_GTP] = ds * gTz;
+        h.ist[IST_COUNT] = k;
+        h.scal[SC_COUNT] = double(k);
+        h.scal[SC_GG] = gg;
+        h.scal[SC_GAMMA] = gamma;
+        h.scal[SC_ALPHA0] = (a.iter == 0) ? fmin(1.0, 1.0 / sqrt(gg)) : 1.0;
+      }
+    }
+  }
+  lds_barrier();
+  // ---- combine (combine_small's arithmetic per element) ----
+  const double cg = cf[2 * MM];
+  const double alpha = cb.alpha;
+  if (full) {
+    f32x4 d4, o4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double acc = cg * double(g4[c]);
+#pragma unroll
+      for (int i = 0; i < KQ; ++i)
+        if (i < k) acc += cf[i] * double(sv[i][c]) + cf[MM + i] * double(yv[i][c]);
+      d4[c] = float(acc);
+      o4[c] = x4[c] + float(alpha) * d4[c];
+    }
+    if (cb.dir) *reinterpret_cast<f32x4 *>(cb.dir + e) = d4;
+    if (cb.x_out) {
+      *reinterpret_cast<f32x4 *>(cb.x_out + e) = o4;
+      if (cb.x_out2) *reinterpret_cast<f32x4 *>(cb.x_out2 + e) = o4;
+    }
+  } else {
+    for (long long q = e; q < n; ++q) { // the tail quad, element-wise (no read past n)
+      double acc = cg * double(cb.g[q]);
+      for (int i = 0; i < k; ++i) {
+        const long long off = (long long)Ls[i] * h.ld + q;
+        acc += cf[i] * double(h.S[off]) + cf[MM + i] * double(h.Y[off]);
+      }
+      const float d = float(acc);
+      if (cb.dir) cb.dir[q] = d;
+      if (cb.x_out) {
+        const float o = cb.x_in[q] + float(alpha) * d;
+        cb.x_out[q] = o;
+        if (cb.x_out2) cb.x_out2[q] = o;
+      }
+    }
+  }
+}
+
 template <int C>
 void launch_sweep(hipStream_t s, const DirArgs &a, int vpw) {
   switch (vpw) {
@@ -381,6 +537,25 @@ static void cols_fin_launch(hipStream_t s, const DirArgs &a) {
 }
 
 void dir_fin(hipStream_t s, const DirArgs &a) { cols_fin_launch(s, a); }
+
+bool dir_combine_supported(const DirArgs &a, const CombineArgs &c) {
+  const GramArgs &g = a.g;
+  return a.want_dir == 1 && g.has_g && !g.has_pair && !g.reset && g.policy == POL_SLBFGS && g.h.m <= DIR_MAXM &&
+         !c.alpha_from_state && g.h.ld % 4 == 0;
+}
+
+void dir_cols_combine(hipStream_t s, const DirArgs &a, const CombineArgs &c) {
+  LBF_REQUIRE(dir_combine_supported(a, c), "dir_cols_combine: direction-only S-LBFGS step, m <= DIR_MAXM");
+  hipLaunchKernelGGL(dir_cols_kernel, dim3(unsigned(dir_ncols(a.g.h.m))), dim3(DF_THREADS), 0, s, a);
+  LBF_KERNEL_CHECK();
+  const dim3 grid(unsigned(cdiv(a.g.h.n, 1024)));
+  const int m = a.g.h.m; // live pairs k <= m
+  if (m <= 4) hipLaunchKernelGGL(dir_combine_kernel<4>, grid, dim3(256), 0, s, a, c);
+  else if (m <= 8) hipLaunchKernelGGL(dir_combine_kernel<8>, grid, dim3(256), 0, s, a, c);
+  else if (m <= 12) hipLaunchKernelGGL(dir_combine_kernel<12>, grid, dim3(256), 0, s, a, c);
+  else hipLaunchKernelGGL(dir_combine_kernel<16>, grid, dim3(256), 0, s, a, c);
+  LBF_KERNEL_CHECK();
+}
 
 bool gram_fin_supported(int m) { return m >= 0 && m <= GRAM_FIN_MAXM; }
 

@@ -35,29 +35,32 @@ using namespace headc;
 constexpr int MAX_WG = 512; // 2 workgroups per CU
 
 // One tile's activations, A[b0 .. b0+TB)[0 .. H), in registers: every load issued before the first use
-// (clamped addresses, masked values), so staging a tile is one memory round trip instead of one per
-// 16-B chunk of the thread's share. H % 4 == 0 and 16-B aligned rows (vec); else the scalar path.
+// from a clamped address and masked only when staged (a value masked at the load compiles to a branch
+// around the load and a wait inside it: one round trip per 16-B chunk), so staging a tile is one memory
+// round trip. H % 4 == 0 and 16-B aligned rows (vec); else the scalar path.
 struct TileRegs {
   static constexpr int QPT = TB * (HMAX / 4) / 256; // 16-B chunks per thread (16 at H = 256)
   f32x4 v[QPT];
-  __device__ inline void load(const float *A, int H, int Hp, long long b0, int rows) {
+  int rows = 0;
+  __device__ inline void load(const float *A, int H, int Hp, long long b0, int rows_) {
     const int t = threadIdx.x, Hq = H >> 2, hq = Hp >> 2;
+    rows = rows_;
 #pragma unroll
     for (int j = 0; j < QPT; ++j) {
       const int e = t + j * 256;
       const int r = e / hq, c4 = e - r * hq;
-      const bool ok = e < TB * hq && r < rows && c4 < Hq;
-      const f32x4 x = *reinterpret_cast<const f32x4 *>(A + (ok ? (b0 + r) * H + 4 * c4 : 0LL));
-      v[j] = ok ? x : (f32x4){0.f, 0.f, 0.f, 0.f};
+      const bool ok = e < TB * hq && r < rows_ && c4 < Hq;
+      v[j] = *reinterpret_cast<const f32x4 *>(A + (ok ? (b0 + r) * H + 4 * c4 : 0LL));
     }
   }
   __device__ inline void store(const Smem &sm) const {
-    const int t = threadIdx.x, hq = sm.Hp >> 2;
+    const int t = threadIdx.x, hq = sm.Hp >> 2, Hq = sm.H >> 2;
 #pragma unroll
     for (int j = 0; j < QPT; ++j) {
       const int e = t + j * 256;
       const int r = e / hq, c4 = e - r * hq;
-      if (e < TB * hq) *reinterpret_cast<f32x4 *>(sm.As + r * sm.LDA + 4 * c4) = v[j];
+      const bool ok = r < rows && c4 < Hq;
+      if (e < TB * hq) *reinterpret_cast<f32x4 *>(sm.As + r * sm.LDA + 4 * c4) = ok ? v[j] : (f32x4){0.f, 0.f, 0.f, 0.f};
     }
   }
 };

@@ -71,6 +71,71 @@ template <bool LDS> __device__ __forceinline__ int hc_ldi(const int *p, int i) {
   else return p[i];
 }
 
+// The two-loop recurrences for k <= 64 (wave 0; lane l owns index l), from LDS: sy = SY of the live
+// pairs in order (k x k, row stride k), syT its transpose, yyl = YY; rho_l, gS_l, gY_l per live index.
+// Returns this lane's alpha (al0) and alpha - beta (c0). The LDS operands of 8 steps are loaded ahead
+// of them (unit stride across lanes), so each step is VALU + v_readlane only. Shared by hist_core and the
+// S-LBFGS direction's combine (dir.hip), which rely on it for bitwise the same coefficients.
+__device__ __forceinline__ void recur_fast(int k, int lane, const double *rho_l, const double *gS_l,
+                                           const double *gY_l, const double *sy, const double *syT,
+                                           const double *yyl, double gamma, double &al0, double &c0) {
+  const double rho_me = lane < k ? rho_l[lane] : 0.0;
+  double r = lane < k ? gS_l[lane] : 0.0;
+  for (int i0 = k - 1; i0 >= 0; i0 -= 8) { // backward: alpha_i = rho_i (gS_i - sum_{j>i} alpha_j SY[i][j])
+    double col[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 - u;
+      col[u] = (i >= 0 && lane < i) ? syT[i * k + lane] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 - u;
+      if (i >= 0) {
+        const double ai = lane_f64(rho_me * r, i);
+        if (lane == i) al0 = ai;
+        r = lane < i ? r - ai * col[u] : r;
+      }
+    }
+  }
+  KTC(65);
+  KTF(60);
+  double acc = lane < k ? gY_l[lane] : 0.0; // gY_l - sum_j alpha_j YY[l][j]  (YY symmetric)
+  for (int j0 = 0; j0 < k; j0 += 8) {
+    double yv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) yv[u] = (j0 + u < k && lane < k) ? yyl[(j0 + u) * k + lane] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (j0 + u < k) acc -= lane_f64(al0, j0 + u) * yv[u];
+  }
+  double tv = gamma * acc;
+  for (int i0 = 0; i0 < k; i0 += 8) { // forward: beta_i = rho_i t_i ; t_l += (alpha_i - beta_i) SY[i][l]
+    double row[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u;
+      row[u] = (i < k && lane > i && lane < k) ? sy[i * k + lane] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u;
+      if (i < k) {
+        const double cand = rho_me * tv;
+        const double ci = lane_f64(al0, i) - lane_f64(cand, i);
+        if (lane == i) c0 = ci;
+        tv = (lane > i && lane < k) ? tv + ci * row[u] : tv;
+      }
+    }
+  }
+}
+
+// The slbfgs gamma (s_lbfgs.hpp:119-126) from the newest pair's ys and yy.
+__device__ __forceinline__ double slbfgs_gamma(double ys, double yy) {
+  const double g = fabs(yy) < 1e-12 ? 1.0 : ys / yy;
+  return fmin(fmax(g, 1e-6), 1e6);
+}
+
 // Barriers here are LDS-only (wave.hpp lds_barrier): within a history step no thread reads global
 // memory another thread of the block wrote in the same step (fresh entries come from the dots in LDS).
 //
@@ -317,67 +382,16 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
     } else if (a.policy == POL_CUDA) {
       gamma = yy > 0.0 ? ys / yy : 1.0; // lbfgs.cuh:247
     } else {
-      gamma = fabs(yy) < 1e-12 ? 1.0 : ys / yy; // s_lbfgs.hpp:119-126
-      gamma = fmin(fmax(gamma, 1e-6), 1e6);
+      gamma = slbfgs_gamma(ys, yy); // s_lbfgs.hpp:119-126
     }
   }
   const double *syT = sy + k * k; // syT[i*k + l] = SY[l][i] (when sy_t)
   double al0 = 0.0, al1 = 0.0;     // alpha of indices lane, lane + 64
   double c0 = 0.0, c1 = 0.0;       // alpha - beta of indices lane, lane + 64
   if (k <= 64 && sy_t && yy_lds) {
-    // Fast path: the LDS operands of 8 steps are loaded ahead of them (unit stride across lanes), so
-    // each step is VALU + v_readlane only.
-    const double rho_me = lane < k ? rho_l[lane] : 0.0;
-    double r = lane < k ? gS_l[lane] : 0.0;
     KTF(63);
     KTC(64);
-    for (int i0 = k - 1; i0 >= 0; i0 -= 8) { // backward: alpha_i = rho_i (gS_i - sum_{j>i} alpha_j SY[i][j])
-      double col[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 - u;
-        col[u] = (i >= 0 && lane < i) ? syT[i * k + lane] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 - u;
-        if (i >= 0) {
-          const double ai = lane_f64(rho_me * r, i);
-          if (lane == i) al0 = ai;
-          r = lane < i ? r - ai * col[u] : r;
-        }
-      }
-    }
-    KTC(65);
-    KTF(60);
-    double acc = lane < k ? gY_l[lane] : 0.0; // gY_l - sum_j alpha_j YY[l][j]  (YY symmetric)
-    for (int j0 = 0; j0 < k; j0 += 8) {
-      double yv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) yv[u] = (j0 + u < k && lane < k) ? yyl[(j0 + u) * k + lane] : 0.0;
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (j0 + u < k) acc -= lane_f64(al0, j0 + u) * yv[u];
-    }
-    double tv = gamma * acc;
-    for (int i0 = 0; i0 < k; i0 += 8) { // forward: beta_i = rho_i t_i ; t_l += (alpha_i - beta_i) SY[i][l]
-      double row[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 + u;
-        row[u] = (i < k && lane > i && lane < k) ? sy[i * k + lane] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 + u;
-        if (i < k) {
-          const double cand = rho_me * tv;
-          const double ci = lane_f64(al0, i) - lane_f64(cand, i);
-          if (lane == i) c0 = ci;
-          tv = (lane > i && lane < k) ? tv + ci * row[u] : tv;
-        }
-      }
-    }
+    recur_fast(k, lane, rho_l, gS_l, gY_l, sy, syT, yyl, gamma, al0, c0);
   } else if (big) {
     // Two indices per lane (l0 = lane, l1 = lane + 64); the LDS operands of 8 steps are loaded ahead
     // of them, so each step is VALU + v_readlane only (the k <= 64 fast path, widened).

@@ -410,6 +410,11 @@ int dir_cols_per_block(int m, long long n);
 int dir_ncols(int m);
 void dir_sweep(hipStream_t s, const DirArgs &a);
 void dir_fin(hipStream_t s, const DirArgs &a);
+// The direction-only S-LBFGS step (has_g, no pair, want_dir 1) as column sums + one launch that runs the
+// coefficient recurrences in every block and combines (x_out = x_in + alpha p): replaces dir_fin + the
+// combine. c.h = a.g.h; alpha not from state.
+bool dir_combine_supported(const DirArgs &a, const CombineArgs &c);
+void dir_cols_combine(hipStream_t s, const DirArgs &a, const CombineArgs &c);
 // The same column sums + last-block history step for gram_update's transposed partials (the unfused
 // L-BFGS path: n > 2M or m > TAIL_MAXM), replacing fold_rows + hist_step: a.rows = the partials,
 // a.nb = gram_nwg(n). m <= GRAM_FIN_MAXM (LDS of the fused step).

@@ -1058,7 +1058,8 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
 
 void History::reset() { hist_reset(ctx_->stream, v_); }
 
-void History::update(const GramArgs &g0, int want_dir, int iter, double dsign, const RedAllArgs *gred) {
+bool History::update_impl(const GramArgs &g0, int want_dir, int iter, double dsign, const RedAllArgs *gred,
+                          const CombineArgs *cmb) {
   GramArgs g = g0;
   g.h = v_;
   g.h.abort = ctx_->abort;
@@ -1100,9 +1101,15 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign, c
       ProfScope ps(ctx_, PK_GRAM);
       dir_sweep(s, d);
     }
+    if (cmb && dir_combine_supported(d, *cmb)) {
+      // direction-only step: column sums, then the coefficients computed in every block of the combine
+      ProfScope ps(ctx_, PK_COMBINE);
+      dir_cols_combine(s, d, *cmb);
+      return true;
+    }
     ProfScope ps(ctx_, PK_COEF);
     dir_fin(s, d);
-    return;
+    return false;
   }
   if (gfin_on_ && (want_dir == 0 || want_dir == 1)) {
     // Gram sweep with transposed partials, then one block per column whose last arrival runs the step:
@@ -1122,7 +1129,7 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign, c
     }
     ProfScope ps(ctx_, PK_COEF);
     gram_fin(s, d);
-    return;
+    return false;
   }
   {
     ProfScope ps(ctx_, PK_GRAM);
@@ -1150,13 +1157,23 @@ void History::update(const GramArgs &g0, int want_dir, int iter, double dsign, c
   c.dsign = dsign;
   ProfScope ps(ctx_, PK_COEF);
   hist_coef(s, c);
+  return false;
 }
 
 void History::update_combine(const GramArgs &g0, int iter, double dsign, const float *x_in, float *x_out,
                              float *x_out2, double alpha, const RedAllArgs *gred) {
   // (the combine inside the column-sum launch measured slower: its waiting blocks slowed the column sums
   // and the one-block step, profiles/r03b/README.md)
-  update(g0, 1, iter, dsign, gred);
+  CombineArgs c;
+  c.h = v_;
+  c.h.abort = ctx_->abort;
+  c.g = g0.g_out;
+  c.x_in = x_in;
+  c.x_out = x_out;
+  c.x_out2 = x_out2;
+  c.alpha_from_state = 0;
+  c.alpha = alpha;
+  if (update_impl(g0, 1, iter, dsign, gred, &c)) return;
   combine(g0.g_out, nullptr, x_in, x_out, x_out2, false, alpha);
 }
 

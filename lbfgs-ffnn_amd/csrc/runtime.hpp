@@ -223,7 +223,9 @@ public:
   // Gram sweep + bookkeeping (+ direction coefficients when want_dir > 0).
   // gred (nullable, nseg > 0): g.ga's values are still split-K slabs (Mlp::loss_grad_deferred); the fused
   // S-LBFGS sweep finishes them in place of reduce_all, other routes launch reduce_all first.
-  void update(const GramArgs &g, int want_dir, int iter, double dsign, const RedAllArgs *gred = nullptr);
+  void update(const GramArgs &g, int want_dir, int iter, double dsign, const RedAllArgs *gred = nullptr) {
+    (void)update_impl(g, want_dir, iter, dsign, gred, nullptr);
+  }
   void combine(const float *g, float *dir, const float *x_in, float *x_out, float *x_out2, bool alpha_from_state,
                double alpha);
   // update(g, 1, iter, dsign) then combine(g.g_out, nullptr, x_in, x_out, x_out2, false, alpha)
@@ -233,6 +235,11 @@ public:
   int m() const { return v_.m; }
 
 private:
+  // cmb: the combine to fuse into the update when the S-LBFGS direction path can (dir_cols_combine);
+  // returns whether it did
+  bool update_impl(const GramArgs &g, int want_dir, int iter, double dsign, const RedAllArgs *gred,
+                   const CombineArgs *cmb);
+
   Ctx *ctx_;
   HistView v_;
   DevBuf<float> S_, Y_;
