@@ -377,10 +377,6 @@ struct TailArgs {
   float *nx_dir = nullptr, *nx_x = nullptr;
   int nx_alpha_state = 1;
   double nx_alpha = 1.0;
-  // ... with a snapshot of the ring header and the status block taken by tail_cols: every block of the
-  // combine reads the step's inputs there, since block 0 rewrites h.ist / h.scal during the launch
-  int *snap_ist = nullptr;      // IST_ORDER + TAIL_MAXM ints
-  double *snap_scal = nullptr;  // SC_N doubles
 };
 // tail_reduce + tail_cols_fin launches; with nx_dir: tail_reduce + tail_cols + tail_combine
 void tail_reduce(hipStream_t s, const TailArgs &a);

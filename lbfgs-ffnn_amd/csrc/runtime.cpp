@@ -708,12 +708,6 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     ta.nx_x = tf->nx_x;
     ta.nx_alpha_state = tf->nx_alpha_state;
     ta.nx_alpha = tf->nx_alpha;
-    if (ta.nx_dir) {
-      tsnap_i_.ensure(size_t(IST_ORDER + TAIL_MAXM));
-      tsnap_d_.ensure(size_t(SC_N));
-      ta.snap_ist = tsnap_i_.get();
-      ta.snap_scal = tsnap_d_.get();
-    }
     ta.nc = 6 * tf->h.m + 8;
     ta.nb = 0; // one TAIL_COLS column group per block: latency-bound work wants every CU busy
     for (int l = 0; l < nl; ++l) {

@@ -207,8 +207,6 @@ private:
   int dx_tile(long long B, int N) const;
   DevBuf<double> loss_part_, dots_part_, sse_, colpart_, trows_, tdots_;
   DevBuf<unsigned> cols_done_; // tail_cols arrival counter (zero between launches)
-  DevBuf<int> tsnap_i_;        // tail_combine's snapshot of the ring header ...
-  DevBuf<double> tsnap_d_;     // ... and of the status block (TailArgs::snap_*)
   // R-pass workspace (hvp): R{Z}, R{A}, R{dZ} and delta per layer, two products, one segment
   std::vector<DevBuf<float>> RZ_, RA_, RD_, DL_;
   DevBuf<float> T1_, T2_, seg_;

@@ -284,22 +284,18 @@ __device__ __forceinline__ bool tail_fin_body(const TailArgs &a, double *coef_l,
     for (int r = t; r < ra.nsse; r += TF_THREADS) sse += ra.sse_part[r];
   for (int q = t; q < a.nc; q += TF_THREADS) // sc1 loads: written this launch by other blocks (hand-off)
     sm.dots[q] = __hip_atomic_load(&a.dots[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // SY, YY, rho: block 0 of a REPL launch rewrites only slot w's entries, which the step takes from the
-  // fresh dots; the ring header and the status words it rewrites are read from tail_cols' snapshot
   for (int i = t; i < S_ * S_; i += TF_THREADS) {
     SYp[i] = h.SY[i];
     YYp[i] = h.YY[i];
   }
   if (t < S_) rhop[t] = h.rho[t];
-  const int *ist_src = REPL ? a.snap_ist : h.ist;
-  const double *sc_src = REPL ? a.snap_scal : sc;
-  if (t < IST_ORDER + m) ist_l[t] = ist_src[t];
+  if (t < IST_ORDER + m) ist_l[t] = h.ist[t];
   double gfo = 0.0, fold = 0.0, alpha0 = 0.0, accept_prev = 0.0;
   if (t == 0) {
-    gfo = sc_src[SC_GTP];
-    fold = a.ls.armijo ? sc_src[SC_FOLDF] : sc_src[SC_FOLD];
-    alpha0 = sc_src[SC_ALPHA0];
-    accept_prev = sc_src[SC_ACCEPT];
+    gfo = sc[SC_GTP];
+    fold = a.ls.armijo ? sc[SC_FOLDF] : sc[SC_FOLD];
+    alpha0 = sc[SC_ALPHA0];
+    accept_prev = sc[SC_ACCEPT];
   }
   sse = t_wave_sum(sse);
   if (lane == 0) v[wave] = sse;
@@ -393,8 +389,7 @@ __device__ __forceinline__ bool tail_fin_body(const TailArgs &a, double *coef_l,
   if (t == 64 && writer) publish();
   if (REPL && t == 0) { // wave 0, after the recurrences (hist_core's last phase)
     rep->k = sm.k;
-    const int l0 = ist_l[IST_COUNT] > 0 ? ist_l[IST_ORDER + 0] : ist_l[IST_WSLOT]; // the issue list's head
-    rep->off = (sm.k > 0 && sm.L[0] != l0) ? 1 : 0; // evicted the oldest: the live run starts at 1
+    rep->off = (sm.k > 0 && sm.L[0] != ist_l[IST_ORDER + 0]) ? 1 : 0; // evicted the oldest: list from 1
     const double gg = sm.dots[6 * m + 5];
     rep->alpha0 = (a.iter_next == 0) ? fmin(1.0, 1.0 / sqrt(gg)) : 1.0; // hist_core's SC_ALPHA0
   }
@@ -419,15 +414,9 @@ __global__ __launch_bounds__(TF_THREADS) void tail_cols_fin_kernel(const TailArg
   (void)tail_fin_body<false>(a, nullptr, nullptr, [](const int *) {});
 }
 
-// Column sums only; tail_combine_kernel reads them after the launch boundary, and the snapshot of the
-// ring header and status block its blocks read (block 0 of tail_combine rewrites the originals).
+// Column sums only; tail_combine_kernel reads them after the launch boundary.
 __global__ __launch_bounds__(TF_THREADS) void tail_cols_kernel(const TailArgs a) {
   if (a.ra.abort && *a.ra.abort) return;
-  if (blockIdx.x == 0) {
-    const int t = threadIdx.x;
-    if (t < IST_ORDER + a.h.m) a.snap_ist[t] = a.h.ist[t];
-    if (t < SC_N) a.snap_scal[t] = a.h.scal[t];
-  }
   tail_cols_body(a);
 }
 
@@ -521,8 +510,7 @@ void tail_reduce(hipStream_t s, const TailArgs &a) {
   }
   LBF_KERNEL_CHECK();
   if (a.nx_dir) { // the next iteration's combine fused behind the step (tail_combine_supported)
-    LBF_REQUIRE(tail_combine_supported(a.h.n, a.h.m) && a.snap_ist && a.snap_scal,
-                "tail_reduce: fused combine unsupported here");
+    LBF_REQUIRE(tail_combine_supported(a.h.n, a.h.m), "tail_reduce: fused combine unsupported here");
     hipLaunchKernelGGL(tail_cols_kernel, dim3(unsigned(a.nc)), dim3(TF_THREADS), 0, s, a);
     LBF_KERNEL_CHECK();
     const dim3 grid(unsigned(cdiv(a.h.n, TF_THREADS)));
