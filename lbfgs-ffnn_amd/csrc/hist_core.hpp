@@ -45,11 +45,6 @@ struct HistStep {
   // in LDS by the caller (the fused tail prefetches them with its first loads). Unused otherwise.
   const int *ist = nullptr;
   const double *rho = nullptr, *SY = nullptr, *YY = nullptr;
-  // FUSED only. write_global = 0: the step runs in every block of a launch (the tail's combine) and only
-  // one of them makes its global writes; coef_lds (LDS, 2 * slots + 1 doubles): the coefficients as
-  // they are written to h.coef, for that block's own combine.
-  int write_global = 1;
-  double *coef_lds = nullptr;
 };
 
 // Ring slot the next pair is written to.
@@ -356,7 +351,6 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
   KTF(59);
   if (wave != 0) {
     if constexpr (FUSED) { // the deferred writes of step B (the live count: wave 0, below)
-      if (!a.write_global) return;
       const int u = t - 64, nu = nt - 64;
       write_rows(u, nu);
       if (u == 0) {
@@ -516,19 +510,6 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
   const double gTz = hc_wave_sum(part) + gamma * gg;
   // lbfgs.cuh:97-104 (CUDA semantics only): not a descent direction -> steepest descent + reset
   const bool fallback = a.policy == POL_CUDA && a.want_dir == 1 && ds * gTz >= 0.0;
-  if (FUSED && a.coef_lds) {
-    double *cl = a.coef_lds;
-    if (lane < k) {
-      cl[lane] = fallback ? 0.0 : ds * c0;
-      cl[S_ + lane] = fallback ? 0.0 : ds * (-gamma * al0);
-    }
-    if (lane + 64 < k) {
-      cl[lane + 64] = fallback ? 0.0 : ds * c1;
-      cl[S_ + lane + 64] = fallback ? 0.0 : ds * (-gamma * al1);
-    }
-    if (lane == 0) cl[2 * S_] = fallback ? -1.0 : ds * gamma;
-  }
-  if (FUSED && !a.write_global) return;
   if (lane < k) {
     h.coef[lane] = fallback ? 0.0 : ds * c0;
     h.coef[S_ + lane] = fallback ? 0.0 : ds * (-gamma * al0);

@@ -372,15 +372,8 @@ struct TailArgs {
   int nb = 0, nc = 0;       // nb: TAIL_COLS column groups over all segments (one block each)
   // Arrival counter (zero between launches): the last tail_cols block to finish runs the one-block fin.
   unsigned *cols_done = nullptr;
-  // The next iteration's combine fused behind the step (nx_dir non-null; tail_combine_supported): p into
-  // nx_dir, x_next = ra.w + alpha p into nx_x, alpha = alpha0 of the step (nx_alpha_state) or nx_alpha.
-  float *nx_dir = nullptr, *nx_x = nullptr;
-  int nx_alpha_state = 1;
-  double nx_alpha = 1.0;
 };
-// tail_reduce + tail_cols_fin launches; with nx_dir: tail_reduce + tail_cols + tail_combine
-void tail_reduce(hipStream_t s, const TailArgs &a);
-bool tail_combine_supported(long long n, int m);
+void tail_reduce(hipStream_t s, const TailArgs &a); // tail_reduce + tail_cols_fin launches
 int tail_vpw(int m);                                // vectors per wave of the Gram sweep (0: unsupported)
 
 // S-LBFGS history update in two launches (dir.hip): a one-round-trip Gram sweep of the new s / y / g

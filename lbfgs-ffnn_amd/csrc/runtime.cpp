@@ -704,10 +704,6 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     ta.policy = tf->policy;
     ta.iter_next = tf->iter_next;
     ta.ls = tf->ls;
-    ta.nx_dir = tf->nx_dir;
-    ta.nx_x = tf->nx_x;
-    ta.nx_alpha_state = tf->nx_alpha_state;
-    ta.nx_alpha = tf->nx_alpha;
     ta.nc = 6 * tf->h.m + 8;
     ta.nb = 0; // one TAIL_COLS column group per block: latency-bound work wants every CU busy
     for (int l = 0; l < nl; ++l) {

@@ -79,10 +79,6 @@ struct TailFuse {
   int policy = POL_CPU;
   int iter_next = 1;
   LsCtlArgs ls;
-  // the next iteration's combine behind the step (TailArgs::nx_*; null: the solver launches it)
-  float *nx_dir = nullptr, *nx_x = nullptr;
-  int nx_alpha_state = 1;
-  double nx_alpha = 1.0;
 };
 
 struct Layer {

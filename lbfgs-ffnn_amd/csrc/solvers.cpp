@@ -58,8 +58,6 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
   // folded history step moves fewer bytes.
   fuse_ = depth_ > 0 && obj_->fused_tail() && prm_.m > 0 && prm_.m <= TAIL_MAXM && n_ <= kFusedTailMaxN;
   if (const char *e = std::getenv("LBF_FUSED_TAIL")) fuse_ = fuse_ && e[0] != '0';
-  // ... and the next iteration's combine inside it (every block runs the step: n within one resident grid)
-  fuse_combine_ = fuse_ && tail_combine_supported(n_, prm_.m);
   if (depth_ > 0) {
     abort_.resize(1);
     LBF_HIP(hipMemsetAsync(abort_.get(), 0, sizeof(int), ctx_->stream));
@@ -157,18 +155,9 @@ void LbfgsSolver::restore(const Roles &r) {
 
 float LbfgsSolver::begin_iteration(const LsCtlArgs *ls) {
   const bool armijo = prm_.line_search == LBF_LS_ARMIJO;
-  // the fused tail also combines the next iteration's direction and trial point: p_ and the buffer that
-  // accept_roles() makes the next trial (xp_ now)
-  auto next_combine = [&](TailFuse &tf) {
-    if (!fuse_combine_) return;
-    tf.nx_dir = p_.get();
-    tf.nx_x = xp_;
-    tf.nx_alpha_state = armijo ? 0 : 1;
-    tf.nx_alpha = 1.0;
-  };
   if (ls && dir_ready_) { // the previous fused tail computed this direction's coefficients
     float alpha = 1.0f;
-    if (!fuse_combine_) hist_.combine(g_, p_.get(), x_, xt_, nullptr, !armijo, armijo ? double(alpha) : 0.0);
+    hist_.combine(g_, p_.get(), x_, xt_, nullptr, !armijo, armijo ? double(alpha) : 0.0);
     TailFuse tf;
     tf.h = hist_.view();
     tf.has_pair = prm_.m > 0;
@@ -178,7 +167,6 @@ float LbfgsSolver::begin_iteration(const LsCtlArgs *ls) {
     tf.iter_next = iter_ + 1;
     tf.ls = *ls;
     tf.ls.alphaf = alpha;
-    next_combine(tf);
     obj_->eval_fused(xt_, gt_, p_.get(), hist_.scal(), tf);
     return alpha;
   }
@@ -212,7 +200,6 @@ float LbfgsSolver::begin_iteration(const LsCtlArgs *ls) {
     tf.iter_next = iter_ + 1;
     tf.ls = *ls;
     tf.ls.alphaf = alpha;
-    next_combine(tf);
     obj_->eval_fused(xt_, gt_, p_.get(), hist_.scal(), tf);
   } else {
     eval(xt_, gt_, p_.get());

@@ -147,7 +147,6 @@ private:
   int depth_ = 0;
   int seq_ = 0;
   bool fuse_ = false;      // fused optimizer tail on the speculative path
-  bool fuse_combine_ = false; // ... which also combines the next direction (tail_combine_kernel)
   bool dir_ready_ = false; // the last fused tail left the next direction's coefficients on the device
   DevBuf<int> abort_;
   SpecRecord *spec_rec_ = nullptr;

@@ -253,17 +253,7 @@ constexpr int TF_THREADS = 256;
 // Wave 0 (decision, then the recurrences) issues no global store until the coefficients: the status
 // block, the host record (system-scope stores to host-mapped memory, whose acknowledgement the
 // sequence word must wait for) and the history step's ring/Gram writes are made by waves 1..3.
-// REPL (tail_combine_kernel): the body runs in every block of a launch; block 0 alone makes the global
-// writes and the host record, every block gets the coefficients in coef_l (LDS) and, through rep, the live
-// count, the offset of the final ring order in the issue list and alpha0. issue(ist) runs on every thread
-// once the ring header is in LDS (the caller's history loads, in flight through the decision and the step).
-// Returns whether the trial was accepted (the step ran).
-struct TailRep {
-  int k, off;
-  double alpha0;
-};
-template <bool REPL, class Issue>
-__device__ __forceinline__ bool tail_fin_body(const TailArgs &a, double *coef_l, TailRep *rep, Issue &&issue) {
+__device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
   const RedAllArgs &ra = a.ra;
   extern __shared__ double dyn[]; // sy [2*m*m] (SY and its transpose) | yy [m*m] | SY, YY [S*S] | rho [S]
   __shared__ HistSmem sm;
@@ -302,8 +292,6 @@ __device__ __forceinline__ bool tail_fin_body(const TailArgs &a, double *coef_l,
   KTF(45);
   lds_barrier();
   KTF(46);
-  issue(ist_l);
-  const bool writer = !REPL || blockIdx.x == 0;
   if (t == 0) { // decide (LDS only: wave 0 issues no global store before the recurrences)
     const double *D = sm.dots;
     const double sse_t = a.hilo ? (double(a.hilo[0]) + double(a.hilo[1])) : ((v[0] + v[1]) + v[2]) + v[3];
@@ -362,8 +350,8 @@ __device__ __forceinline__ bool tail_fin_body(const TailArgs &a, double *coef_l,
   // Rejected: history untouched (the host finishes the line search). Converged: the solver stops
   // before the next history update, exactly like the host-driven loop.
   if (s_status != SPEC_ACCEPT) {
-    if (t == 64 && writer) publish();
-    return false;
+    if (t == 64) publish();
+    return;
   }
   // ---- accepted: push the pair, coefficients of the next direction ----
   HistStep st;
@@ -379,22 +367,13 @@ __device__ __forceinline__ bool tail_fin_body(const TailArgs &a, double *coef_l,
   st.rho = rhop;
   st.SY = SYp;
   st.YY = YYp;
-  st.write_global = writer ? 1 : 0;
-  st.coef_lds = REPL ? coef_l : nullptr;
   hist_prologue<true>(st, sm, ist_l[IST_WSLOT]);
   KTF(42);
   KTF(43);
   hist_core<true>(st, sm, dyn, 2 * m * m, dyn + 2 * m * m, m * m);
   // waves 1..3 leave hist_core after its deferred stores; wave 1 then publishes
-  if (t == 64 && writer) publish();
-  if (REPL && t == 0) { // wave 0, after the recurrences (hist_core's last phase)
-    rep->k = sm.k;
-    rep->off = (sm.k > 0 && sm.L[0] != ist_l[IST_ORDER + 0]) ? 1 : 0; // evicted the oldest: list from 1
-    const double gg = sm.dots[6 * m + 5];
-    rep->alpha0 = (a.iter_next == 0) ? fmin(1.0, 1.0 / sqrt(gg)) : 1.0; // hist_core's SC_ALPHA0
-  }
+  if (t == 64) publish();
   KTF(44);
-  return true;
 }
 
 // tail_cols, then (cols_done) the last block to finish runs the one-block fin: one launch fewer on
@@ -411,60 +390,7 @@ __global__ __launch_bounds__(TF_THREADS) void tail_cols_fin_kernel(const TailArg
   __syncthreads();
   if (!s_last) return;
   if (threadIdx.x == 0) *a.cols_done = 0u; // ready for the next launch (stream-ordered)
-  (void)tail_fin_body<false>(a, nullptr, nullptr, [](const int *) {});
-}
-
-// Column sums only; tail_combine_kernel reads them after the launch boundary.
-__global__ __launch_bounds__(TF_THREADS) void tail_cols_kernel(const TailArgs a) {
-  if (a.ra.abort && *a.ra.abort) return;
-  tail_cols_body(a);
-}
-
-// The fin in every block, then the next iteration's combine (History::combine's arithmetic, combine_small's
-// order: bitwise its direction and trial point): p = sum_i c_i basis_i over the final live order, written
-// to nx.dir, and x_next = x_t + alpha p to nx.x, where x_t = ra.w is the accepted trial and g = ra.G its
-// gradient. The lane's values of the ring slots that can be live after the push (the old live order, then
-// the write slot) are loaded as soon as the ring header is in LDS, so they arrive during the decision and
-// the recurrences; the final live order is a contiguous run of that list (rep.off). Rejected or converged:
-// no combine (block 0 publishes the record, as tail_cols_fin does). KS >= m + 1.
-template <int KS>
-__global__ __launch_bounds__(TF_THREADS) void tail_combine_kernel(const TailArgs a) {
-  if (a.ra.abort && *a.ra.abort) return;
-  __shared__ double coef_l[2 * KS + 1];
-  __shared__ TailRep rep;
-  const HistView &h = a.h;
-  const long long n = h.n;
-  const long long e0 = (long long)blockIdx.x * TF_THREADS + threadIdx.x;
-  const bool in = e0 < n;
-  const long long e = in ? e0 : n - 1; // loads unconditional (clamped), stores masked
-  const float gv = a.ra.G[e], xv = a.ra.w[e];
-  float sv[KS + 1], yv[KS + 1];
-  auto issue = [&](const int *ist) {
-    const int c0 = __builtin_amdgcn_readfirstlane(ist[IST_COUNT]);
-    const int wsl = __builtin_amdgcn_readfirstlane(ist[IST_WSLOT]);
-#pragma unroll
-    for (int i = 0; i <= KS; ++i) {
-      const int slot = __builtin_amdgcn_readfirstlane(i < c0 ? ist[IST_ORDER + i] : wsl);
-      const long long off = (long long)slot * h.ld + e;
-      sv[i] = h.S[off];
-      yv[i] = h.Y[off];
-    }
-  };
-  if (!tail_fin_body<true>(a, coef_l, &rep, issue)) return;
-  lds_barrier(); // coefficients and rep from wave 0
-  const int k = rep.k, off = rep.off, S_ = h.slots;
-  double acc = coef_l[2 * S_] * double(gv);
-#pragma unroll
-  for (int i = 0; i < KS; ++i)
-    if (i < k) {
-      const float s_ = off ? sv[i + 1] : sv[i], y_ = off ? yv[i + 1] : yv[i];
-      acc += coef_l[i] * double(s_) + coef_l[S_ + i] * double(y_);
-    }
-  if (!in) return;
-  const float d = float(acc);
-  const double alpha = a.nx_alpha_state ? rep.alpha0 : a.nx_alpha;
-  a.nx_dir[e] = d;
-  a.nx_x[e] = xv + float(alpha) * d;
+  tail_fin_body(a);
 }
 
 } // namespace
@@ -479,26 +405,6 @@ static size_t fin_shmem(const TailArgs &a) {
   return (size_t(3) * a.h.m * a.h.m + 2 * size_t(a.h.slots) * a.h.slots + a.h.slots) * sizeof(double);
 }
 
-template <int KS> static void tail_combine_launch(hipStream_t s, const TailArgs &a, dim3 grid) {
-  hipLaunchKernelGGL(tail_combine_kernel<KS>, grid, dim3(TF_THREADS), fin_shmem(a), s, a);
-  LBF_KERNEL_CHECK();
-}
-
-// The fused combine runs the fin in every block, so its grid (one element per lane) must be resident at
-// once: n up to the resident blocks' lanes; m + 1 <= 16 ring slots.
-bool tail_combine_supported(long long n, int m) {
-  if (m < 1 || m + 1 > 16 || n <= 0) return false;
-  static const long long resident = [] { // blocks of the widest instance the chip holds at once
-    int dev = 0, cus = 0, per = 0;
-    LBF_HIP(hipGetDevice(&dev));
-    LBF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const size_t shmem = (size_t(3) * 15 * 15 + 2 * size_t(16) * 16 + 16) * sizeof(double);
-    LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tail_combine_kernel<16>, TF_THREADS, shmem));
-    return (long long)std::max(1, cus) * std::max(1, per);
-  }();
-  return cdiv(n, TF_THREADS) <= resident;
-}
-
 void tail_reduce(hipStream_t s, const TailArgs &a) {
   if (a.nb <= 0) return;
   switch (tail_vpw(a.h.m)) {
@@ -509,16 +415,6 @@ void tail_reduce(hipStream_t s, const TailArgs &a) {
   default: throw Error(2, "tail_reduce: history size not supported by the fused tail");
   }
   LBF_KERNEL_CHECK();
-  if (a.nx_dir) { // the next iteration's combine fused behind the step (tail_combine_supported)
-    LBF_REQUIRE(tail_combine_supported(a.h.n, a.h.m), "tail_reduce: fused combine unsupported here");
-    hipLaunchKernelGGL(tail_cols_kernel, dim3(unsigned(a.nc)), dim3(TF_THREADS), 0, s, a);
-    LBF_KERNEL_CHECK();
-    const dim3 grid(unsigned(cdiv(a.h.n, TF_THREADS)));
-    if (a.h.slots <= 8) tail_combine_launch<8>(s, a, grid);
-    else if (a.h.slots <= 12) tail_combine_launch<12>(s, a, grid);
-    else tail_combine_launch<16>(s, a, grid);
-    return;
-  }
   if (!a.cols_done) throw Error(2, "tail_reduce: needs the arrival counter (cols_done)");
   hipLaunchKernelGGL(tail_cols_fin_kernel, dim3(unsigned(a.nc)), dim3(TF_THREADS), fin_shmem(a), s, a);
   LBF_KERNEL_CHECK();
