@@ -96,7 +96,6 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
   }
   nparams_ = off;
   if (const char *e = std::getenv("LBF_NO_FOLD")) fold_on_ = e[0] != '1'; // tests: the unfolded route
-  rowhead_on_ = env_int("LBF_ROWHEAD", 1) != 0; // A/B of the row head (round 4 measurement; removed after)
 }
 
 // Split-K factor for `tiles` output tiles over a K of `K` rows: the GEMM tiles run two workgroups per
@@ -261,7 +260,7 @@ bool Mlp::rowhead_on(long long B) const {
   const int nl = int(layers_.size());
   if (nl < 2 || B <= 0) return false;
   const Layer &Lo = layers_[size_t(nl - 1)], &Lh = layers_[size_t(nl - 2)];
-  return Lh.fsplits > 1 && rowhead_supported(Lo.in, Lo.out) && head_supported(Lo.in, Lo.out) && rowhead_on_;
+  return Lh.fsplits > 1 && rowhead_supported(Lo.in, Lo.out) && head_supported(Lo.in, Lo.out);
 }
 
 bool Mlp::gemm_head_on() const {

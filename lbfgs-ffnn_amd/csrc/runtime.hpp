@@ -193,7 +193,6 @@ private:
   std::vector<DevBuf<float>> A_, D_;
   DevBuf<float> slab_, head_slab_, fslab_;
   bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1: the unfolded route, tests)
-  bool rowhead_on_ = true;
   bool rowhead_on(long long B) const; // the standalone head fed by the last hidden layer's slabs
   // Planned fold: the last hidden layer's [dW ; db] rows fold_c0_ .. in (fold_ input columns and the
   // bias row) are computed in the forward GEMM's EPI_HEAD epilogue instead of a mostly empty last

@@ -838,15 +838,11 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
       if (t + 1 < m_inner) anchor_ahead(t + 1);
       tock(0, h0);
       h0 = tick();
-      static const int defer_on = env_int("LBF_SLBFGS_DEFER", 1); // round-4 A/B (removed after)
       if (dp)
         net_->loss_grad_local(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b);
-      else if (defer_on) // the gradient's last reduction runs inside the direction sweep (one launch fewer per step)
+      else // the gradient's last reduction runs inside the direction sweep (one launch fewer per step)
         net_->loss_grad_deferred(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda,
                                  &gred);
-      else
-        net_->loss_grad(wt_.get(), g1(t), rows_x(sl), rows_y(sl), nullptr, sl.cnt, inv_b, prm_.lambda, nullptr,
-                        nullptr);
       tock(1, h0);
       h0 = tick();
       twin_wait(tk[size_t(t)]); // task t recorded ev_g2_[t & 1] / ev_anc_[t]

@@ -1,6 +1,7 @@
 #!/bin/bash
-# round 4, run C: the sweep-side gradient reduction as 16-B quads over four stripe waves, and the row head
-# with every load of a row in flight at once (no masked loads); suite, cfg-4 A/B and its kernel trace.
+# round 4, run C: the sweep-side gradient reduction as 16-B quads over four stripe waves, the row head with
+# every load of a row in flight at once, the S-LBFGS direction's recurrences inside its combine, the L-BFGS
+# tail's next combine inside the fin (every block); suite, cfg 2 / 7500 / cfg 4 and their kernel traces.
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
@@ -10,12 +11,19 @@ cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
 B() { n=$1; shift; timeout -k 10 200 python -u bench.py "$@" > $O/$n.json 2> $O/$n.err || { echo "bench $n failed"; tail -3 $O/$n.err; exit 1; }; }
+B bench_driver --steps 20 --warmup 5
+B bench_400 --steps 400 --no-cpu-baseline
+B bench_7500 --steps 400 --samples 7500 --no-cpu-baseline
 B bench_cfg4 --solver slbfgs --steps 6 --no-cpu-baseline
 LBF_SLBFGS_DEFER=0 B bench_cfg4_nodefer --solver slbfgs --steps 6 --no-cpu-baseline
 LBF_ROWHEAD=0 B bench_cfg4_norowhead --solver slbfgs --steps 6 --no-cpu-baseline
 B bench_cfg4_b --solver slbfgs --steps 6 --no-cpu-baseline
 cd /tmp
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt4 -o run -- python3 $R/bench.py --solver slbfgs --no-cpu-baseline --steps 3 --warmup 1 > $O/kt4.json 2> $O/kt4.err || { echo "prof failed"; exit 1; }
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt4 -o run -- python3 $R/bench.py --solver slbfgs --no-cpu-baseline --steps 3 --warmup 1 > $O/kt4.json 2> $O/kt4.err && \
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt60000 -o run -- python3 $R/bench.py --no-cpu-baseline --steps 50 > $O/kt60000.json 2> $O/kt60000.err && \
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt7500 -o run -- python3 $R/bench.py --samples 7500 --no-cpu-baseline --steps 50 > $O/kt7500.json 2> $O/kt7500.err || { echo "prof failed"; exit 1; }
 cd $R
-python3 profiles/kstats_live.py $O/kt4/run_kernel_trace.csv --out $O/kt4_live.csv || { echo "kstats failed"; exit 1; }
+python3 profiles/kstats_live.py $O/kt4/run_kernel_trace.csv --out $O/kt4_live.csv && \
+python3 profiles/kstats_live.py --spec $O/kt60000/run_kernel_trace.csv --out $O/kt60000_live.csv && \
+python3 profiles/kstats_live.py --spec $O/kt7500/run_kernel_trace.csv --out $O/kt7500_live.csv || { echo "kstats failed"; exit 1; }
 echo "run c ok"
