@@ -71,7 +71,13 @@ int lbf_ctx_create(int device, void *stream, lbf_ctx **out) {
       if (stream) {
         c->c.stream = static_cast<hipStream_t>(stream);
       } else {
-        LBF_HIP(hipStreamCreateWithFlags(&c->c.stream, hipStreamDefault)); // blocking: ordered with the legacy stream torch uses
+        // blocking: ordered with the legacy stream torch uses; the highest priority, so that a solver's
+        // critical chain is dispatched ahead of its own off-path work (the S-LBFGS twin, lowest priority)
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest < least)
+          LBF_HIP(hipStreamCreateWithPriority(&c->c.stream, hipStreamDefault, greatest));
+        else
+          LBF_HIP(hipStreamCreateWithFlags(&c->c.stream, hipStreamDefault));
         c->c.own_stream = true;
       }
       c->scal.resize(SC_N);

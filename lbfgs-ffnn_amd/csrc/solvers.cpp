@@ -572,7 +572,12 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
     tctx_.reset(new Ctx());
     tctx_->device = ctx_->device;
     tctx_->cus = ctx_->cus;
-    LBF_HIP(hipStreamCreateWithFlags(&tctx_->stream, hipStreamNonBlocking));
+    // the lowest priority: the anchor gradients are off the critical path, the context stream's chain is on it
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest < least)
+      LBF_HIP(hipStreamCreateWithPriority(&tctx_->stream, hipStreamNonBlocking, least));
+    else
+      LBF_HIP(hipStreamCreateWithFlags(&tctx_->stream, hipStreamNonBlocking));
     tctx_->own_stream = true;
     tctx_->prof.on = ctx_->prof.on; // the benchmark's section timing covers the twin's launches too
     tctx_->prof.only = ctx_->prof.only;
