@@ -552,6 +552,7 @@ void dir_cols_combine(hipStream_t s, const DirArgs &a, const CombineArgs &c) {
   const int m = a.g.h.m; // live pairs k <= m
   if (m <= 4) hipLaunchKernelGGL(dir_combine_kernel<4>, grid, dim3(256), 0, s, a, c);
   else if (m <= 8) hipLaunchKernelGGL(dir_combine_kernel<8>, grid, dim3(256), 0, s, a, c);
+  else if (m <= 10) hipLaunchKernelGGL(dir_combine_kernel<10>, grid, dim3(256), 0, s, a, c); // cfg 4
   else if (m <= 12) hipLaunchKernelGGL(dir_combine_kernel<12>, grid, dim3(256), 0, s, a, c);
   else hipLaunchKernelGGL(dir_combine_kernel<16>, grid, dim3(256), 0, s, a, c);
   LBF_KERNEL_CHECK();

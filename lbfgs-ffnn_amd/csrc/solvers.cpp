@@ -573,18 +573,12 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
     tctx_->device = ctx_->device;
     tctx_->cus = ctx_->cus;
     // the lowest priority: the anchor gradients are off the critical path, the context stream's chain is on it
+    // (the twin confined to 32-128 of the CUs measured the same, profiles/r04/e/)
     int least = 0, greatest = 0;
-    static const int twin_cus = env_int("LBF_TWIN_CUS", 0); // round-4 A/B: the twin on a subset of the CUs
-    if (twin_cus > 0 && twin_cus < ctx_->cus) {
-      std::vector<uint32_t> mask(size_t((ctx_->cus + 31) / 32), 0u);
-      const int stride = std::max(1, ctx_->cus / twin_cus);
-      for (int i = 0, k = 0; i < ctx_->cus && k < twin_cus; i += stride, ++k) mask[size_t(i / 32)] |= 1u << (i % 32);
-      LBF_HIP(hipExtStreamCreateWithCUMask(&tctx_->stream, uint32_t(mask.size()), mask.data()));
-    } else if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest < least) {
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest < least)
       LBF_HIP(hipStreamCreateWithPriority(&tctx_->stream, hipStreamNonBlocking, least));
-    } else {
+    else
       LBF_HIP(hipStreamCreateWithFlags(&tctx_->stream, hipStreamNonBlocking));
-    }
     tctx_->own_stream = true;
     tctx_->prof.on = ctx_->prof.on; // the benchmark's section timing covers the twin's launches too
     tctx_->prof.only = ctx_->prof.only;
