@@ -57,6 +57,12 @@ struct GemmK {
   float *head_delta, *head_slab;
   double *head_sse;
   int head_fold, head_fold_c0;
+  const float *a_slab;
+  int a_splits;
+  long long a_slab_stride;
+  const float *a_bias;
+  int a_act;
+  float *a_out;
 };
 
 // Side job (see GemmDesc): one 256-column group (four per lane) x 4 split stripes per block, fp64 in
@@ -629,7 +635,7 @@ struct GldsPiece {
 // KW = 2 (small tiles that run one workgroup per CU, e.g. 32 x 128 for a rank's shard): eight waves, two
 // per SIMD; k-group q computes steps [8q, 8q+8) of every 32-deep tile from the same LDS stage, group 0
 // alone issues the LDS-DMA pieces, and the groups' accumulators are summed through LDS in group order.
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1>
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1, bool ASUM = false>
 __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(const GemmK g) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32;
   constexpr int ASZ = BM * BK, STG = (BM + BN) * BK;
@@ -637,6 +643,8 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
   static_assert((BM + BN) % 32 == 0, "pieces per wave");
   static_assert(AKC || BM >= 64, "mn-contiguous swizzle needs >= 64 columns");
   static_assert(BKC || BN >= 64, "mn-contiguous swizzle needs >= 64 columns");
+  static_assert(!ASUM || (AKC && !GATHER && PA == 4), "A from slabs: the 32-row k-contiguous tile, one A piece per wave");
+  constexpr int PD = ASUM ? P - 1 : P; // LDS-DMA pieces per wave per k-tile
   constexpr int HEAD_F = headc::smem_floats_epi(BN, BM > headc::TB ? BM : headc::TB);
   constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > NS * STG) ? HEAD_F : NS * STG;
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
@@ -708,6 +716,7 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
 #pragma unroll
     for (int i = 0; i < P; ++i) {
       const int j = wave + 4 * i;
+      if (ASUM && j < PA) continue; // formed by the prologue
       const unsigned long long a = pc[i].p0 + (unsigned long long)t * pc[i].step;
       glds16(reinterpret_cast<const float *>(kt + pc[i].kq < ke ? a : zero_u),
              stage + (j < PA ? j * 256 : ASZ + (j - PA) * 256));
@@ -783,12 +792,46 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
     if (g.head_fold > 0) hpre.load_fold(g.A, g.lda, g.a_idx, g.head_fold_c0, g.head_fold, m0, g.M);
   }
   const int nk = kb < ke ? (ke - kb + BK - 1) / BK : 0;
+  if constexpr (ASUM) {
+    // This wave's A piece (rows 8 wave .. +7, the DMA's chunk swizzle) of every k-tile of the chunk (nk <= NS,
+    // gemm_asum_ok), k-tile t by k-group t % KW: all splits' 16-B quads loaded, summed in split order (fp32,
+    // fwd_reduce_act's order), + bias, activation, into the tile's stage; rows / k past the ends are zeros,
+    // as the DMA's zero chunk. Column tile 0 also stores the activations.
+    const int r = 8 * wave + (lane >> 3);
+    const int gc = (lane & 7) ^ ((r >> 1) & 7);
+    const int row = m0 + r;
+    const bool rok = row < g.M;
+    const long long rbase = (long long)(rok ? row : 0) * g.lda;
+    for (int t = kgrp; t < nk; t += KW) {
+      const int kq = kb + t * BK + 4 * gc;
+      const bool ok = rok && kq < ke;
+      const long long off = rbase + (ok ? kq : 0);
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+      for (int s0 = 0; s0 < g.a_splits; s0 += 8) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { // unconditional (clamped split), masked in the sum
+          const int sp = min(s0 + u, g.a_splits - 1);
+          v[u] = *reinterpret_cast<const f32x4 *>(g.a_slab + (long long)sp * g.a_slab_stride + off);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (s0 + u < g.a_splits) sum += v[u];
+      }
+      const f32x4 b4 = *reinterpret_cast<const f32x4 *>(g.a_bias + (ok ? kq : 0));
+      f32x4 a4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a4[e] = ok ? act_rt(g.a_act, sum[e] + b4[e]) : 0.0f;
+      *reinterpret_cast<f32x4 *>(lds + (t % NS) * STG + wave * 256 + lane * 4) = a4;
+      if (ok && blockIdx.x == 0) *reinterpret_cast<f32x4 *>(g.a_out + rbase + kq) = a4;
+    }
+  }
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
     if (t < nk) issue(t);
   {
     for (int i = 0; i < nk; ++i) {
-      vm_wait_tiles<P, NS>(min(NS - 2, nk - 1 - i)); // this wave's pieces of k-tile i landed
+      vm_wait_tiles<PD, NS>(min(NS - 2, nk - 1 - i)); // this wave's pieces of k-tile i landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier(); // everyone's pieces landed; buffer (i - 1) % NS no longer read
       if (EPI == EPI_HEAD && i < 24) KT(1 + i);
@@ -880,10 +923,23 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.head_sse = d.head_sse;
   k.head_fold = d.head_fold;
   k.head_fold_c0 = d.head_fold_c0;
+  k.a_slab = d.a_slab;
+  k.a_splits = d.a_splits;
+  k.a_slab_stride = d.a_slab_stride;
+  k.a_bias = d.a_bias;
+  k.a_act = d.a_act;
+  k.a_out = d.a_out;
   dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
   if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
     if (fast && (AKC || !d.a_idx)) {
       const dim3 gb(256 * KW);
+      if constexpr (AKC && BM == 32 && WN * TN == 4 && NS >= 2) {
+        if (d.a_slab) { // gemm_asum_ok
+          hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, KW, true>), grid, gb, 0, s, k);
+          return;
+        }
+      }
+      if (d.a_slab) throw std::runtime_error("gemm: A from slabs not supported for this tile");
       if (d.a_idx)
         hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, NS, KW>), grid, gb, 0, s, k);
       else
@@ -953,8 +1009,17 @@ long long gemm_tiles(const GemmDesc &d) {
   return cdiv((long long)d.M, (long long)BM) * cdiv((long long)d.N, (long long)BN);
 }
 
+bool gemm_asum_ok(const GemmDesc &d) {
+  const int kc = d.splits > 1 ? d.k_chunk : d.K;
+  return d.tile == TILE_32x128 && d.a_kc && !d.b_kc && !d.a_idx && (d.epi == EPI_STORE || d.epi == EPI_FWD) &&
+         d.K % 4 == 0 && d.lda % 4 == 0 && d.ldb % 4 == 0 && d.a_slab_stride % 4 == 0 && kc > 0 && kc <= 4 * 32 &&
+         d.a_splits >= 1 && aligned16(d.A) && aligned16(d.B) && aligned16(d.a_slab) && aligned16(d.a_bias) &&
+         aligned16(d.a_out);
+}
+
 void gemm(hipStream_t s, const GemmDesc &d) {
   if (d.M <= 0 || d.N <= 0) return;
+  if (d.a_slab && !gemm_asum_ok(d)) throw std::runtime_error("gemm: A from slabs not supported for this shape");
   if (d.epi == EPI_HEAD) {
     int BM, BN;
     gemm_tile_for(d.N, d.tile, &BM, &BN);

@@ -48,6 +48,16 @@ struct GemmDesc {
   long long ldaux = 0;
   int aux_act = ACT_LINEAR;
   const int *abort = nullptr; // speculative execution: the kernel is a no-op when *abort != 0
+  // A from the previous layer's forward split-K slabs (a_slab non-null; only where gemm_asum_ok): each
+  // workgroup forms its A tiles as act(sum_s a_slab[s * a_slab_stride + .] + a_bias) (fwd_reduce_act's
+  // arithmetic, splits in order) in its prologue, and the workgroups of column tile 0 also write them to
+  // a_out (row stride lda), which replaces the fwd_reduce_act launch of the previous layer.
+  const float *a_slab = nullptr;
+  int a_splits = 0;
+  long long a_slab_stride = 0;
+  const float *a_bias = nullptr;
+  int a_act = ACT_LINEAR;
+  float *a_out = nullptr;
   // Side job riding in an extra z-plane of the launch: side_dst[c] = sum_s side_slab[s*stride + c]
   // (fixed split order, fp64) for c < side_count. Used to finish the fused head's [dW ; db] slabs
   // while the next layer's dW GEMM runs.
@@ -73,6 +83,9 @@ struct GemmDesc {
 // Row tiles of the forward GEMM for M rows and N columns (== EPI_HEAD partial slabs).
 int gemm_row_tiles(int M, int tile);
 
+// Whether gemm() can take d's A from the previous layer's slabs (a_slab): the 32 x 128 k-contiguous
+// forward split-K tile, no row gather, a k-chunk of at most four k-tiles, 16-B aligned operands.
+bool gemm_asum_ok(const GemmDesc &d);
 void gemm(hipStream_t s, const GemmDesc &d);
 // Tile (BM, BN) the dispatcher picks for a given N (used by the split-K planner).
 void gemm_tile_for(int N, int tile, int *BM, int *BN);

@@ -245,6 +245,7 @@ void Mlp::plan(long long B) {
   }
   slab_.ensure(slab);
   fslab_.ensure(std::max<size_t>(fslab, 1));
+  fslab2_.ensure(std::max<size_t>(fslab, 1)); // odd layers' slabs: the next layer may read the previous one's
   planned_ = B;
 }
 
@@ -330,29 +331,58 @@ GemmDesc Mlp::fwd_desc(size_t l, const float *P, const float *in, const int *idx
   return d;
 }
 
+// Layer l's forward GEMM as forward() launches it (split-K slabs into fslab_buf(l) when split).
+GemmDesc Mlp::fwd_launch_desc(size_t l, const float *P, const float *in, const int *idx, long long B) {
+  const Layer &L = layers_[l];
+  GemmDesc d = fwd_desc(l, P, in, idx, B);
+  if (L.fsplits > 1) {
+    d.epi = EPI_STORE;
+    d.C = fslab_buf(l);
+    d.splits = L.fsplits;
+    d.k_chunk = L.fk_chunk;
+    d.slab_stride = B * L.out;
+  }
+  return d;
+}
+
+// d (layer l + 1's GEMM) takes its A, layer l's activations, from layer l's split-K slabs
+void Mlp::set_asum(GemmDesc &d, size_t l, const float *P, long long B) {
+  const Layer &L = layers_[l];
+  d.a_slab = fslab_buf(l);
+  d.a_splits = L.fsplits;
+  d.a_slab_stride = B * L.out;
+  d.a_bias = P + L.off + size_t(L.in) * L.out;
+  d.a_act = L.act;
+  d.a_out = A_[l].get();
+}
+
 const float *Mlp::forward(const float *P, const float *X, const int *idx, long long B, int nrun, bool raw_last) {
   ensure(B);
   hipStream_t s = ctx_->stream;
   const float *in = X;
   const size_t nr = nrun < 0 ? layers_.size() : size_t(nrun);
+  bool pending = false; // layer l - 1's slabs are reduced by layer l's GEMM (its A prologue)
   for (size_t l = 0; l < nr; ++l) {
     const Layer &L = layers_[l];
-    GemmDesc d = fwd_desc(l, P, in, idx, B);
-    if (L.fsplits > 1) {
-      d.epi = EPI_STORE;
-      d.C = fslab_.get();
-      d.splits = L.fsplits;
-      d.k_chunk = L.fk_chunk;
-      d.slab_stride = B * L.out;
-      // (an in-launch reduction by each tile's last split measured slower: the reducer's serial slab read
-      // lengthened the GEMM more than the launch it saved, profiles/r03/bench_cfg4_*_fin.json)
+    GemmDesc d = fwd_launch_desc(l, P, in, idx, B);
+    if (pending) set_asum(d, l - 1, P, B);
+    {
       ProfScope ps(ctx_, PK_FWD, int(l), double(B));
       gemm(s, d);
-      if (!(raw_last && l + 1 == nr))
-        fwd_reduce_act(s, fslab_.get(), L.fsplits, B * L.out, int(B), L.out, d.bias, L.act, A_[l].get(), ctx_->abort);
-    } else {
-      ProfScope ps(ctx_, PK_FWD, int(l), double(B));
-      gemm(s, d);
+    }
+    pending = false;
+    if (L.fsplits > 1 && !(raw_last && l + 1 == nr)) {
+      // The split-K slabs summed in split order with the bias and activation: by the next layer's GEMM while
+      // it loads its A (one launch fewer; the 32 x 128 split tile of S-LBFGS minibatches), else by
+      // fwd_reduce_act. (An in-launch reduction by each tile's last split measured slower: the reducer's
+      // serial slab read lengthened the GEMM more than the launch it saved, profiles/r03/bench_cfg4_*_fin.json.)
+      if (l + 1 < nr) {
+        GemmDesc dn = fwd_launch_desc(l + 1, P, A_[l].get(), nullptr, B);
+        set_asum(dn, l, P, B);
+        pending = gemm_asum_ok(dn);
+      }
+      if (!pending)
+        fwd_reduce_act(s, fslab_buf(l), L.fsplits, B * L.out, int(B), L.out, d.bias, L.act, A_[l].get(), ctx_->abort);
     }
     in = A_[l].get();
   }
@@ -384,7 +414,7 @@ void Mlp::forward_phase(const float *P, const float *X, const float *Y, const in
     // in one launch (head.hip rowhead)
     const Layer &Lh = layers_[nl - 2];
     RowHeadArgs r;
-    r.fslab = fslab_.get();
+    r.fslab = fslab_buf(size_t(nl - 2));
     r.splits = Lh.fsplits;
     r.stride = B * Lh.out;
     r.hbias = P + Lh.off + size_t(Lh.in) * Lh.out;

@@ -118,7 +118,7 @@ public:
   Ctx *ctx() const { return ctx_; }
 
   // Forward only: activations of every layer into the workspace; returns the output buffer.
-  // raw_last: the last layer run stays as its split-K slabs in fslab_ (no fwd_reduce_act; rowhead reads them)
+  // raw_last: the last layer run stays as its split-K slabs in fslab_buf(l) (no fwd_reduce_act; rowhead reads them)
   const float *forward(const float *P, const float *X, const int *idx, long long B, int nrun = -1,
                        bool raw_last = false);
   // Fused loss + gradient (+ all-reduce over the communicator) + line-search dots.
@@ -186,12 +186,15 @@ private:
   void ensure(long long B);
   bool side_reduced(int l, bool fused, int nloss) const;
   GemmDesc fwd_desc(size_t l, const float *P, const float *in, const int *idx, long long B) const;
+  GemmDesc fwd_launch_desc(size_t l, const float *P, const float *in, const int *idx, long long B);
+  void set_asum(GemmDesc &d, size_t l, const float *P, long long B);
   Ctx *ctx_;
   std::vector<Layer> layers_;
   size_t nparams_ = 0;
   long long cap_ = -1, planned_ = -1;
   std::vector<DevBuf<float>> A_, D_;
-  DevBuf<float> slab_, head_slab_, fslab_;
+  DevBuf<float> slab_, head_slab_, fslab_, fslab2_;
+  float *fslab_buf(size_t l) const { return (l & 1) ? fslab2_.get() : fslab_.get(); } // forward slabs of layer l
   bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1: the unfolded route, tests)
   bool rowhead_on(long long B) const; // the standalone head fed by the last hidden layer's slabs
   // Planned fold: the last hidden layer's [dW ; db] rows fold_c0_ .. in (fold_ input columns and the

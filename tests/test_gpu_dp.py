@@ -155,6 +155,10 @@ def test_batch_grads_equal_per_minibatch_loss_grad(ctx, pkg):
                                          ([784, 128, 10], ["relu", "linear"], 1000),
                                          ([784, 512, 256, 10], ["relu", "tanh", "linear"], 256),  # split-K
                                          ([784, 512, 256, 10], ["relu", "relu", "linear"], 96),
+                                         # the next split GEMM forms its A from the previous layer's slabs
+                                         # (activation inside the prologue; 13 slabs = two rounds at B = 96)
+                                         ([784, 512, 256, 10], ["tanh", "relu", "linear"], 256),
+                                         ([784, 512, 256, 128, 10], ["relu", "sigmoid", "relu", "linear"], 256),
                                          ([784, 128, 64, 10], ["sigmoid", "relu", "linear"], 333),
                                          # N = 16 < the tile width, EPI_HEAD with the 16-column fold, M < 32: the
                                          # epilogue consumes the whole tile's accumulators (rows >= M, columns
