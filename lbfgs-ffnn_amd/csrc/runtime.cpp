@@ -594,16 +594,30 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
   };
   // dX of layer l as split-K slabs whose sum dW of layer l-1 forms in its B prologue (with act'), when that
   // GEMM can: the S-LBFGS minibatch's 256-row dX runs on 32 x 128 tiles, a quarter of the chip unsplit
-  auto dx_split = [&](int l) -> int {
-    if (l <= 0 || B <= 0) return 0;
+  auto dx_chunk = [&](int l) -> int { // the split dX's k-chunk (0: unsplit)
+    // only into layer 0: a deeper layer's delta also feeds the next dX GEMM, which needs it materialized
+    if (l != 1 || B <= 0) return 0;
     const Layer &L = layers_[l];
     const long long tiles = cdiv(B, 32) * cdiv((long long)L.in, 128);
     if (dx_tile(B, L.in) != TILE_32x128 || L.out % 32) return 0;
-    int sp = int(std::max(2LL, std::min(8LL, (long long)ctx_->cus / (2 * tiles))));
+    const int sp = int(std::max(2LL, std::min(8LL, (long long)ctx_->cus / (2 * tiles))));
     const int kc = int(cdiv(cdiv(L.out, sp), 32) * 32);
-    sp = int(cdiv(L.out, kc));
-    if (sp < 2) return 0;
-    dxslab_.ensure(size_t(sp) * size_t(B) * L.in);
+    return cdiv(L.out, kc) >= 2 ? kc : 0;
+  };
+  { // one slab buffer for every layer's split dX, sized before any launch reads it (no reallocation under
+    // a queued GEMM)
+    size_t need = 0;
+    for (int l = lstart; l >= 1; --l) {
+      const int kc = dx_chunk(l);
+      if (kc > 0) need = std::max(need, size_t(cdiv(layers_[l].out, kc)) * size_t(B) * layers_[l].in);
+    }
+    if (need) dxslab_.ensure(need);
+  }
+  auto dx_split = [&](int l) -> int {
+    const int kc = dx_chunk(l);
+    if (kc <= 0) return 0;
+    const Layer &L = layers_[l];
+    const int sp = int(cdiv(L.out, kc));
     GemmDesc dn = dw_desc(l - 1);
     dn.b_slab = dxslab_.get();
     dn.b_splits = sp;
