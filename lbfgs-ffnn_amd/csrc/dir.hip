@@ -361,8 +361,9 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_kernel(const DirArgs a) {
 // flight wave 0 runs the two-loop recurrences (recur_fast, hist_core's fast path: bitwise the same
 // coefficients); then p = sum c_i basis_i and x_out = x_in + alpha p as combine_small computes them.
 // Block 0 also makes the step's global writes (g-dots rows, coefficients, scalars: hist_core's for this
-// step), so the state after the launch is what dir_cols_fin + combine leave. Replaces dir_cols_fin's serial
-// step and the combine's header round trip on the critical path.
+// step; no block of the launch reads any of them, and the ring header every block reads is not written),
+// so the state after the launch is what dir_cols_fin + combine leave. Replaces dir_cols_fin's serial step
+// and the combine's header round trip on the critical path.
 template <int KQ>
 __global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const CombineArgs cb) {
   const HistView &h = a.g.h;
@@ -438,7 +439,8 @@ __global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const
         h.coef[2 * S_] = ds * gamma;
         h.scal[SC_RESET] = 0.0;
         h.scal[SC_GTP] = ds * gTz;
-        h.ist[IST_COUNT] = k;
+        // (the live count is unchanged by a direction-only step: the ring header, which every block reads
+        // at its start, is not written here)
         h.scal[SC_COUNT] = double(k);
         h.scal[SC_GG] = gg;
         h.scal[SC_GAMMA] = gamma;
