@@ -267,8 +267,9 @@ def test_ranks_cfg4_epoch(ctx, pkg, dp_mode):
     """BASELINE cfg 4 (784-512-256-10, N = 60000, b = 256, b_H = 128, L = M = 10) for one epoch at world 2
     against the single route. Sliced: the twin's anchor gradients ahead and ONE all-reduce per [g(w_t) | g(w)]
     block. Replicated: every rank runs the whole chain, the full-batch gradient at the anchor is sharded.
-    Same number of live curvature pairs, epoch loss within 5 % (234 SVRG steps with FD pairs are chaotic at
-    the rounding level: tests/test_gpu_fullsize.py), ranks bitwise identical."""
+    Same number of live curvature pairs, epoch loss within 5 % or 3x the single route's own spread from
+    2-ulp-moved parameters (234 SVRG steps with FD pairs are chaotic at the rounding level:
+    tests/test_gpu_fullsize.py), ranks bitwise identical."""
     dims, acts, N, world = [784, 512, 256, 10], ["relu", "relu", "linear"], 60000, 2
     Xh, Yh = pkg.synth_mnist(N)
     X, Y = dev(Xh), dev(Yh)
@@ -289,7 +290,12 @@ def test_ranks_cfg4_epoch(ctx, pkg, dp_mode):
     h = res[0][0]
     assert np.isfinite(h["loss"][0])
     assert h["accepted"][0] == h1["accepted"][0]
-    assert abs(h["loss"][0] - h1["loss"][0]) <= 0.05 * abs(h1["loss"][0])
+    # the epoch loss is chaotic at the rounding level (tests/test_gpu_fullsize.py): the single route from
+    # parameters moved by ~2 ulp measures how far a re-rounding alone takes it
+    P3 = P0.clone().mul_(1.0 + 2.0 ** -22)
+    h3, _ = pkg.slbfgs_solve(net1, P3, X, Y, **args)
+    spread = abs(h3["loss"][0] - h1["loss"][0]) / abs(h1["loss"][0])
+    assert abs(h["loss"][0] - h1["loss"][0]) <= max(0.05, 3.0 * spread) * abs(h1["loss"][0]), spread
     if dp_mode == "sliced":
         assert res[0][2] + res[1][2] == i1.n_rows  # the ranks' slices partition the single route's rows
     else:  # every rank evaluates every minibatch row; the two full-batch evaluations are split
