@@ -63,11 +63,6 @@ struct GemmK {
   const float *a_bias;
   int a_act;
   float *a_out;
-  const float *b_slab;
-  int b_splits;
-  long long b_slab_stride;
-  const float *b_aux;
-  int b_act;
 };
 
 // Side job (see GemmDesc): one 256-column group (four per lane) x 4 split stripes per block, fp64 in
@@ -640,8 +635,7 @@ struct GldsPiece {
 // KW = 2 (small tiles that run one workgroup per CU, e.g. 32 x 128 for a rank's shard): eight waves, two
 // per SIMD; k-group q computes steps [8q, 8q+8) of every 32-deep tile from the same LDS stage, group 0
 // alone issues the LDS-DMA pieces, and the groups' accumulators are summed through LDS in group order.
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1, bool ASUM = false,
-          bool BSUM = false>
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1, bool ASUM = false>
 __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(const GemmK g) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32;
   constexpr int ASZ = BM * BK, STG = (BM + BN) * BK;
@@ -650,8 +644,7 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
   static_assert(AKC || BM >= 64, "mn-contiguous swizzle needs >= 64 columns");
   static_assert(BKC || BN >= 64, "mn-contiguous swizzle needs >= 64 columns");
   static_assert(!ASUM || (AKC && !GATHER && PA == 4), "A from slabs: the 32-row k-contiguous tile, one A piece per wave");
-  static_assert(!BSUM || (!BKC && BN == 64 && KW == 1 && P == 4 && PA == 8), "B from slabs: the 64 x 64 dW tile");
-  constexpr int PD = ASUM ? P - 1 : (BSUM ? P - 2 : P); // LDS-DMA pieces per wave per k-tile
+  constexpr int PD = ASUM ? P - 1 : P; // LDS-DMA pieces per wave per k-tile
   constexpr int HEAD_F = headc::smem_floats_epi(BN, BM > headc::TB ? BM : headc::TB);
   constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > NS * STG) ? HEAD_F : NS * STG;
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
@@ -723,7 +716,7 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
 #pragma unroll
     for (int i = 0; i < P; ++i) {
       const int j = wave + 4 * i;
-      if ((ASUM && j < PA) || (BSUM && j >= PA)) continue; // formed by the prologue
+      if (ASUM && j < PA) continue; // formed by the prologue
       const unsigned long long a = pc[i].p0 + (unsigned long long)t * pc[i].step;
       glds16(reinterpret_cast<const float *>(kt + pc[i].kq < ke ? a : zero_u),
              stage + (j < PA ? j * 256 : ASZ + (j - PA) * 256));
@@ -833,42 +826,6 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
       if (ok && blockIdx.x == 0) *reinterpret_cast<f32x4 *>(g.a_out + rbase + kq) = a4;
     }
   }
-  if constexpr (BSUM) {
-    // This wave's two B pieces (pieces wave + 8 and wave + 12: k-rows jj * 4 + lane / 16 of each k-tile, the
-    // DMA's chunk swizzle) of every k-tile of the chunk (nk <= NS, gemm_bsum_ok): the dX slabs' 16-B quads
-    // summed in split order, times act' of the aux quad (EPI_DX's arithmetic), into the tile's stage;
-    // columns / k-rows past the ends are zeros, as the DMA's zero chunk.
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int jj = wave + 4 * h;
-      const int kl = jj * 4 + (lane >> 4);
-      const int gc = (lane & 15) ^ (((kl >> 4) & 1) * 8);
-      const int col = n0 + 4 * gc;
-      const bool cok = col < g.N;
-      for (int t = 0; t < nk; ++t) {
-        const int kr = kb + t * BK + kl;
-        const bool ok = cok && kr < ke;
-        const long long off = ok ? (long long)kr * g.ldb + col : 0;
-        f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-        for (int s0 = 0; s0 < g.b_splits; s0 += 8) {
-          f32x4 v[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) { // unconditional (clamped split), masked in the sum
-            const int sp = min(s0 + u, g.b_splits - 1);
-            v[u] = *reinterpret_cast<const f32x4 *>(g.b_slab + (long long)sp * g.b_slab_stride + off);
-          }
-#pragma unroll
-          for (int u = 0; u < 8; ++u)
-            if (s0 + u < g.b_splits) sum += v[u];
-        }
-        const f32x4 ax = *reinterpret_cast<const f32x4 *>(g.b_aux + off);
-        f32x4 b4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) b4[e] = ok ? sum[e] * dact_rt(g.b_act, ax[e]) : 0.0f;
-        *reinterpret_cast<f32x4 *>(lds + (t % NS) * STG + ASZ + jj * 256 + lane * 4) = b4;
-      }
-    }
-  }
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
     if (t < nk) issue(t);
@@ -972,11 +929,6 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.a_bias = d.a_bias;
   k.a_act = d.a_act;
   k.a_out = d.a_out;
-  k.b_slab = d.b_slab;
-  k.b_splits = d.b_splits;
-  k.b_slab_stride = d.b_slab_stride;
-  k.b_aux = d.b_aux;
-  k.b_act = d.b_act;
   dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
   if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
     if (fast && (AKC || !d.a_idx)) {
@@ -987,15 +939,7 @@ void launch(hipStream_t s, const GemmDesc &d) {
           return;
         }
       }
-      if constexpr (!AKC && !BKC && BN == 64 && KW == 1 && (BM + BN) / 32 == 4 && BM / 8 == 8) {
-        if (d.b_slab) { // gemm_bsum_ok
-          hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, KW, false, true>), grid, gb, 0,
-                             s, k);
-          return;
-        }
-      }
       if (d.a_slab) throw std::runtime_error("gemm: A from slabs not supported for this tile");
-      if (d.b_slab) throw std::runtime_error("gemm: B from slabs not supported for this tile");
       if (d.a_idx)
         hipLaunchKernelGGL((gemm_glds_kernel<WM, WN, TM, TN, AKC, BKC, EPI, true, NS, KW>), grid, gb, 0, s, k);
       else
@@ -1073,18 +1017,9 @@ bool gemm_asum_ok(const GemmDesc &d) {
          aligned16(d.a_out);
 }
 
-bool gemm_bsum_ok(const GemmDesc &d) {
-  const int kc = d.splits > 1 ? d.k_chunk : d.K;
-  return d.tile == TILE_64x64 && !d.a_kc && !d.b_kc && !d.a_idx && d.epi == EPI_STORE && d.K % 4 == 0 &&
-         d.lda % 4 == 0 && d.ldb % 4 == 0 && d.N % 4 == 0 && (d.a_mvalid > 0 ? d.a_mvalid : d.M) % 4 == 0 &&
-         d.b_slab_stride % 4 == 0 && kc > 0 && kc <= 5 * 32 && d.b_splits >= 1 && aligned16(d.A) && aligned16(d.B) &&
-         aligned16(d.b_slab) && aligned16(d.b_aux);
-}
-
 void gemm(hipStream_t s, const GemmDesc &d) {
   if (d.M <= 0 || d.N <= 0) return;
   if (d.a_slab && !gemm_asum_ok(d)) throw std::runtime_error("gemm: A from slabs not supported for this shape");
-  if (d.b_slab && !gemm_bsum_ok(d)) throw std::runtime_error("gemm: B from slabs not supported for this shape");
   if (d.epi == EPI_HEAD) {
     int BM, BN;
     gemm_tile_for(d.N, d.tile, &BM, &BN);
@@ -1099,7 +1034,6 @@ void gemm(hipStream_t s, const GemmDesc &d) {
   else if (d.epi == EPI_DX && d.a_kc && d.b_kc) dispatch_tile<true, true, EPI_DX>(s, d);
   else if (d.epi == EPI_STORE && !d.a_kc && !d.b_kc) dispatch_tile<false, false, EPI_STORE>(s, d);
   else if (d.epi == EPI_STORE && d.a_kc && !d.b_kc) dispatch_tile<true, false, EPI_STORE>(s, d);
-  else if (d.epi == EPI_STORE && d.a_kc && d.b_kc) dispatch_tile<true, true, EPI_STORE>(s, d); // split dX
   else throw std::runtime_error("gemm: unsupported operand/epilogue combination");
   LBF_KERNEL_CHECK();
 }

@@ -58,15 +58,6 @@ struct GemmDesc {
   const float *a_bias = nullptr;
   int a_act = ACT_LINEAR;
   float *a_out = nullptr;
-  // B from the next layer's dX split-K slabs (b_slab non-null; only where gemm_bsum_ok): the dW GEMM forms
-  // its B tiles (delta of this layer) as (sum_s b_slab[s * b_slab_stride + .]) * act'(b_aux) (EPI_DX's
-  // arithmetic, splits in order; b_aux has B's row stride ldb), which replaces the dX launch's epilogue and
-  // the delta round trip.
-  const float *b_slab = nullptr;
-  int b_splits = 0;
-  long long b_slab_stride = 0;
-  const float *b_aux = nullptr;
-  int b_act = ACT_LINEAR;
   // Side job riding in an extra z-plane of the launch: side_dst[c] = sum_s side_slab[s*stride + c]
   // (fixed split order, fp64) for c < side_count. Used to finish the fused head's [dW ; db] slabs
   // while the next layer's dW GEMM runs.
@@ -95,9 +86,6 @@ int gemm_row_tiles(int M, int tile);
 // Whether gemm() can take d's A from the previous layer's slabs (a_slab): the 32 x 128 k-contiguous
 // forward split-K tile, no row gather, a k-chunk of at most four k-tiles, 16-B aligned operands.
 bool gemm_asum_ok(const GemmDesc &d);
-// Whether gemm() can take d's B from dX slabs (b_slab): the 64 x 64 mn-contiguous dW tile, ungathered A,
-// a k-chunk of at most five k-tiles, 16-B aligned operands.
-bool gemm_bsum_ok(const GemmDesc &d);
 void gemm(hipStream_t s, const GemmDesc &d);
 // Tile (BM, BN) the dispatcher picks for a given N (used by the split-K planner).
 void gemm_tile_for(int N, int tile, int *BM, int *BN);

@@ -562,14 +562,15 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     Gl = words_.get();
   }
   if (empty) zero_fill(s, (long long)nparams_ + 2, Gl, ctx_->abort);
-  // [dW ; db] = [A_in | 1]^T dZ  (layer.cuh:81-84 + sum_rows_kernel kernels.cuh:144-153)
-  auto dw_desc = [&](int l) {
+  for (int l = lstart; l >= 0; --l) {
     const Layer &L = layers_[l];
+    const float *Ain = (l == 0) ? X : A_[l - 1].get();
+    // [dW ; db] = [A_in | 1]^T dZ  (layer.cuh:81-84 + sum_rows_kernel kernels.cuh:144-153)
     GemmDesc d;
     d.M = L.in + 1;
     d.N = L.out;
     d.K = int(B);
-    d.A = (l == 0) ? X : A_[l - 1].get();
+    d.A = Ain;
     d.lda = L.in;
     d.a_kc = false;
     d.a_idx = (l == 0) ? idx : nullptr;
@@ -589,54 +590,6 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       d.M = fold_c0_;
       d.a_mvalid = fold_c0_;
       d.a_ones = -1;
-    }
-    return d;
-  };
-  // dX of layer l as split-K slabs whose sum dW of layer l-1 forms in its B prologue (with act'), when that
-  // GEMM can: the S-LBFGS minibatch's 256-row dX runs on 32 x 128 tiles, a quarter of the chip unsplit
-  auto dx_chunk = [&](int l) -> int { // the split dX's k-chunk (0: unsplit)
-    // only into layer 0: a deeper layer's delta also feeds the next dX GEMM, which needs it materialized
-    if (l != 1 || B <= 0) return 0;
-    const Layer &L = layers_[l];
-    const long long tiles = cdiv(B, 32) * cdiv((long long)L.in, 128);
-    if (dx_tile(B, L.in) != TILE_32x128 || L.out % 32) return 0;
-    const int sp = int(std::max(2LL, std::min(8LL, (long long)ctx_->cus / (2 * tiles))));
-    const int kc = int(cdiv(cdiv(L.out, sp), 32) * 32);
-    return cdiv(L.out, kc) >= 2 ? kc : 0;
-  };
-  { // one slab buffer for every layer's split dX, sized before any launch reads it (no reallocation under
-    // a queued GEMM)
-    size_t need = 0;
-    for (int l = lstart; l >= 1; --l) {
-      const int kc = dx_chunk(l);
-      if (kc > 0) need = std::max(need, size_t(cdiv(layers_[l].out, kc)) * size_t(B) * layers_[l].in);
-    }
-    if (need) dxslab_.ensure(need);
-  }
-  auto dx_split = [&](int l) -> int {
-    const int kc = dx_chunk(l);
-    if (kc <= 0) return 0;
-    const Layer &L = layers_[l];
-    const int sp = int(cdiv(L.out, kc));
-    GemmDesc dn = dw_desc(l - 1);
-    dn.b_slab = dxslab_.get();
-    dn.b_splits = sp;
-    dn.b_slab_stride = B * L.in;
-    dn.b_aux = A_[l - 1].get();
-    dn.b_act = layers_[l - 1].act;
-    return gemm_bsum_ok(dn) ? kc : 0;
-  };
-  int dx_kc = 0; // > 0: layer l's delta is in dxslab_ as split-K slabs of this k-chunk
-  for (int l = lstart; l >= 0; --l) {
-    const Layer &L = layers_[l];
-    GemmDesc d = dw_desc(l);
-    if (dx_kc > 0) {
-      const Layer &N1 = layers_[l + 1];
-      d.b_slab = dxslab_.get();
-      d.b_splits = int(cdiv(N1.out, dx_kc));
-      d.b_slab_stride = B * N1.in;
-      d.b_aux = A_[l].get();
-      d.b_act = L.act;
     }
     if (l + 1 < nl && side_reduced(l + 1, fused, nloss)) {
       // finish layer l+1's [dW ; db] slabs (the fused head's, or many split-K slabs) in side blocks
@@ -664,11 +617,9 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       ProfScope ps(ctx_, PK_DW, l, double(B));
       gemm(s, d);
     }
-    dx_kc = 0;
     if (l > 0) {
       // dX = dZ W^T .* act'(A_prev)   (layer.cuh:89-103 fused with activation_deriv of layer l-1)
       const Layer &P0 = layers_[l - 1];
-      dx_kc = dx_split(l);
       GemmDesc x;
       x.M = int(B);
       x.N = L.in;
@@ -687,15 +638,6 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       x.aux_act = P0.act;
       x.abort = ctx_->abort;
       x.tile = dx_tile(B, L.in);
-      if (dx_kc > 0) { // split-K slabs (dxslab_ sized by dx_split), act' applied by the next dW GEMM's B prologue
-        const long long sp = cdiv(L.out, dx_kc);
-        x.epi = EPI_STORE;
-        x.C = dxslab_.get();
-        x.splits = int(sp);
-        x.k_chunk = dx_kc;
-        x.slab_stride = B * L.in;
-        x.aux = nullptr;
-      }
       ProfScope ps(ctx_, PK_DX, l, double(B));
       gemm(s, x);
     }

@@ -193,7 +193,7 @@ private:
   size_t nparams_ = 0;
   long long cap_ = -1, planned_ = -1;
   std::vector<DevBuf<float>> A_, D_;
-  DevBuf<float> slab_, head_slab_, fslab_, fslab2_, dxslab_;
+  DevBuf<float> slab_, head_slab_, fslab_, fslab2_;
   float *fslab_buf(size_t l) const { return (l & 1) ? fslab2_.get() : fslab_.get(); } // forward slabs of layer l
   bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1: the unfolded route, tests)
   bool rowhead_on(long long B) const; // the standalone head fed by the last hidden layer's slabs
