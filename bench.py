@@ -261,7 +261,8 @@ def main_slbfgs(a, pkg, ctx, world, rank):
             roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
         roof.update(kernel=name, avg_launch_us=round(ms * 1e3 / launches, 2), timed_launches=launches,
                     sampled_every=PROF_EVERY, avg_rows_per_timed_launch=round(work.get(dominant, 0.0) / launches, 1),
-                    traffic=None)
+                    traffic=pmc_traffic(a.pmc_json, name, f"{','.join(str(d) for d in dims)}:{a.samples}:{world}"))
+        # (traffic: the median over the section's minibatch launches, the PMC pass's most frequent size)
         out = {
             "metric": "S-LBFGS epochs/s + grad-evals/s, 784-512-256-10 MLP",
             "value": round(epochs / elapsed, 4),
@@ -391,6 +392,21 @@ def main(argv=None):
     return 0
 
 
+def pmc_traffic(path, section, config):
+    """HBM bytes per launch of `section` for `config` from the committed PMC summary (profiles/
+    pmc_traffic.json: one entry or a list of them, written by profiles/collect_pmc.py), or None."""
+    if not os.path.exists(path):
+        return None
+    try:
+        pm = json.load(open(path))
+    except Exception:
+        return None
+    for e in pm if isinstance(pm, list) else [pm]:
+        if e.get("section") == section and e.get("config") == config:
+            return e.get("hbm_bytes_per_launch")
+    return None
+
+
 def run_rank(a, world, rank, local, pkg):
     """One rank of the benchmark (world = 1: the whole job)."""
     dims = [int(x) for x in a.dims.split(",")]
@@ -504,14 +520,7 @@ def run_rank(a, world, rank, local, pkg):
         roof["avg_launch_us"] = round(avg_s * 1e6, 2)
         roof["timed_launches"] = cnt
         roof["sampled_every"] = every
-        roof["traffic"] = None
-        if os.path.exists(a.pmc_json):
-            try:
-                pm = json.load(open(a.pmc_json))
-                if pm.get("section") == name and pm.get("config") == f"{a.dims}:{N}:{world}":
-                    roof["traffic"] = pm.get("hbm_bytes_per_launch")
-            except Exception:
-                pass
+        roof["traffic"] = pmc_traffic(a.pmc_json, name, f"{a.dims}:{N}:{world}")
         ms_step = elapsed / max(iters_done, 1) * 1e3
         value = iters_done / elapsed
         out = {

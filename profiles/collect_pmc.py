@@ -47,7 +47,17 @@ def main():
                fetch_kib_median=f_kib, write_kib_median=w_kib,
                hbm_bytes_per_launch=2 * f_kib * 1024 + w_kib * 1024,
                correction="bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE under-reads wide streams 2x)")
-    json.dump(out, open(a.out, "w"), indent=1)
+    # the file holds one entry per (section, config): replace this one's, keep the others
+    entries = []
+    if os.path.exists(a.out):
+        try:
+            old = json.load(open(a.out))
+            entries = [e for e in (old if isinstance(old, list) else [old])
+                       if (e.get("section"), e.get("config")) != (a.section, a.config)]
+        except Exception:
+            entries = []
+    entries.append(out)
+    json.dump(entries if len(entries) > 1 else out, open(a.out, "w"), indent=1)
     print(json.dumps(out))
 
 
