@@ -63,6 +63,8 @@ struct GemmK {
   const float *a_bias;
   int a_act;
   float *a_out;
+  int gx, gy;   // this problem's tile grid (the grouped launch's grid is the larger of two)
+  int group_z;  // grouped launch: GEMM planes of the first problem (the second's follow)
 };
 
 // Side job (see GemmDesc): one 256-column group (four per lane) x 4 split stripes per block, fp64 in
@@ -635,8 +637,16 @@ struct GldsPiece {
 // KW = 2 (small tiles that run one workgroup per CU, e.g. 32 x 128 for a rank's shard): eight waves, two
 // per SIMD; k-group q computes steps [8q, 8q+8) of every 32-deep tile from the same LDS stage, group 0
 // alone issues the LDS-DMA pieces, and the groups' accumulators are summed through LDS in group order.
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1, bool ASUM = false>
-__global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(const GemmK g) {
+template <int WM, int WN, int TM, int TN, int EPI, int NS> struct GldsShape {
+  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32;
+  static constexpr int STG = (BM + BN) * BK;
+  static constexpr int HEAD_F = headc::smem_floats_epi(BN, BM > headc::TB ? BM : headc::TB);
+  static constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > NS * STG) ? HEAD_F : NS * STG;
+};
+
+// One GEMM tile (bx, by) of split zsplit (the kernels below choose the problem and the tile).
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW, bool ASUM>
+__device__ __forceinline__ void glds_body(const GemmK &g, float *lds, int zsplit, int bx, int by) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32;
   constexpr int ASZ = BM * BK, STG = (BM + BN) * BK;
   constexpr int PA = BM / 8, P = (BM + BN) / 32; // A pieces per k-tile, pieces per wave per k-tile
@@ -645,20 +655,12 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
   static_assert(BKC || BN >= 64, "mn-contiguous swizzle needs >= 64 columns");
   static_assert(!ASUM || (AKC && !GATHER && PA == 4), "A from slabs: the 32-row k-contiguous tile, one A piece per wave");
   constexpr int PD = ASUM ? P - 1 : P; // LDS-DMA pieces per wave per k-tile
-  constexpr int HEAD_F = headc::smem_floats_epi(BN, BM > headc::TB ? BM : headc::TB);
-  constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > NS * STG) ? HEAD_F : NS * STG;
-  __shared__ __attribute__((aligned(16))) float lds[LDS_F];
-  if (g.abort && *g.abort) return;
-  if (int(blockIdx.z) < g.side_planes) {
-    gemm_side_job(g, reinterpret_cast<double *>(lds));
-    return;
-  }
-  const int zsplit = int(blockIdx.z) - g.side_planes;
+  constexpr int LDS_F = GldsShape<WM, WN, TM, TN, EPI, NS>::LDS_F;
   const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
   const int kgrp = KW > 1 ? __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 8)) : 0;
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 31, lh = lane >> 5;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int n0 = bx * BN, m0 = by * BM;
   const int kb = zsplit * g.k_chunk;
   const int ke = min(g.K, kb + g.k_chunk);
 
@@ -823,7 +825,7 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
 #pragma unroll
       for (int e = 0; e < 4; ++e) a4[e] = ok ? act_rt(g.a_act, sum[e] + b4[e]) : 0.0f;
       *reinterpret_cast<f32x4 *>(lds + (t % NS) * STG + wave * 256 + lane * 4) = a4;
-      if (ok && blockIdx.x == 0) *reinterpret_cast<f32x4 *>(g.a_out + rbase + kq) = a4;
+      if (ok && bx == 0) *reinterpret_cast<f32x4 *>(g.a_out + rbase + kq) = a4;
     }
   }
 #pragma unroll
@@ -869,19 +871,44 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
   gemm_epilogue<WM, WN, TM, TN, EPI, KW>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, kgrp);
 }
 
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1, bool ASUM = false>
+__global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(const GemmK g) {
+  __shared__ __attribute__((aligned(16))) float lds[GldsShape<WM, WN, TM, TN, EPI, NS>::LDS_F];
+  if (g.abort && *g.abort) return;
+  if (int(blockIdx.z) < g.side_planes) {
+    gemm_side_job(g, reinterpret_cast<double *>(lds));
+    return;
+  }
+  glds_body<WM, WN, TM, TN, AKC, BKC, EPI, GATHER, NS, KW, ASUM>(g, lds, int(blockIdx.z) - g.side_planes,
+                                                               int(blockIdx.x), int(blockIdx.y));
+}
+
+// Two GEMMs of one shape in one launch (the S-LBFGS minibatch's dW GEMMs of adjacent layers): planes
+// [0, side_planes) run g's side job, the next g.group_z planes g's splits, the rest g2's; a block past its
+// problem's tile grid exits.
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int NS, int KW = 1>
+__global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_group_kernel(const GemmK g, const GemmK g2) {
+  __shared__ __attribute__((aligned(16))) float lds[GldsShape<WM, WN, TM, TN, EPI, NS>::LDS_F];
+  if (g.abort && *g.abort) return;
+  if (int(blockIdx.z) < g.side_planes) {
+    gemm_side_job(g, reinterpret_cast<double *>(lds));
+    return;
+  }
+  const int z = int(blockIdx.z) - g.side_planes, bx = int(blockIdx.x), by = int(blockIdx.y);
+  if (z >= g.group_z) {
+    if (bx >= g2.gx || by >= g2.gy) return;
+    glds_body<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, KW, false>(g2, lds, z - g.group_z, bx, by);
+  } else {
+    if (bx >= g.gx || by >= g.gy) return;
+    glds_body<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, KW, false>(g, lds, z, bx, by);
+  }
+}
+
 namespace {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// NS > 0: the LDS-DMA kernel with NS tile buffers where the shape allows it (FAST shapes, no gathered
-// mn-contiguous operand); otherwise the register-staged kernel (KW k-groups, PF register sets).
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int KW = 1, int PF = 1, int NS = 0>
-void launch(hipStream_t s, const GemmDesc &d) {
-  // FAST loads: K % 4 == 0, vector-aligned operands, column counts % 4 == 0
-  const bool fast = d.K % 4 == 0 && (d.lda % 4 == 0) && (d.ldb % 4 == 0) &&
-                    ((reinterpret_cast<uintptr_t>(d.A) | reinterpret_cast<uintptr_t>(d.B)) & 15) == 0 &&
-                    (AKC || (d.a_mvalid > 0 ? d.a_mvalid : d.M) % 4 == 0) && (BKC || d.N % 4 == 0);
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+template <int BM, int BN> GemmK make_gemmk(const GemmDesc &d) {
   GemmK k;
   k.M = d.M;
   k.N = d.N;
@@ -906,6 +933,9 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.aux_act = d.aux_act;
   k.abort = d.abort;
   const long long gx = (d.N + BN - 1) / BN, gy = (d.M + BM - 1) / BM;
+  k.gx = int(gx);
+  k.gy = int(gy);
+  k.group_z = 0;
   k.side_planes = (d.side_slab && d.side_count > 0) ? int(cdiv(cdiv(d.side_count, SIDE_COLS), gx * gy)) : 0;
   k.side_slab = d.side_slab;
   k.side_splits = d.side_splits;
@@ -929,7 +959,37 @@ void launch(hipStream_t s, const GemmDesc &d) {
   k.a_bias = d.a_bias;
   k.a_act = d.a_act;
   k.a_out = d.a_out;
+  return k;
+}
+
+// NS > 0: the LDS-DMA kernel with NS tile buffers where the shape allows it (FAST shapes, no gathered
+// mn-contiguous operand); otherwise the register-staged kernel (KW k-groups, PF register sets).
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int KW = 1, int PF = 1, int NS = 0>
+void launch(hipStream_t s, const GemmDesc &d, const GemmDesc *d2 = nullptr) {
+  // FAST loads: K % 4 == 0, vector-aligned operands, column counts % 4 == 0
+  const bool fast = d.K % 4 == 0 && (d.lda % 4 == 0) && (d.ldb % 4 == 0) &&
+                    ((reinterpret_cast<uintptr_t>(d.A) | reinterpret_cast<uintptr_t>(d.B)) & 15) == 0 &&
+                    (AKC || (d.a_mvalid > 0 ? d.a_mvalid : d.M) % 4 == 0) && (BKC || d.N % 4 == 0);
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  GemmK k = make_gemmk<BM, BN>(d);
+  const long long gx = k.gx, gy = k.gy;
   dim3 grid(unsigned(gx), unsigned(gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
+  if (d2) { // grouped with a second problem of this shape (gemm_group_ok): its splits follow d's
+    if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) {
+      GemmDesc e = *d2;
+      e.side_slab = nullptr;
+      e.side_count = 0;
+      GemmK k2 = make_gemmk<BM, BN>(e);
+      k.group_z = d.splits > 1 ? d.splits : 1;
+      const long long gx2 = std::max<long long>(gx, k2.gx), gy2 = std::max<long long>(gy, k2.gy);
+      k.side_planes = (d.side_slab && d.side_count > 0) ? int(cdiv(cdiv(d.side_count, SIDE_COLS), gx2 * gy2)) : 0;
+      const dim3 g3(unsigned(gx2), unsigned(gy2), unsigned(k.group_z + (e.splits > 1 ? e.splits : 1) + k.side_planes));
+      hipLaunchKernelGGL((gemm_glds_group_kernel<WM, WN, TM, TN, AKC, BKC, EPI, NS, KW>), g3, dim3(256 * KW), 0, s, k,
+                         k2);
+      return;
+    }
+    throw std::runtime_error("gemm: grouped launch not supported for this tile");
+  }
   if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
     if (fast && (AKC || !d.a_idx)) {
       const dim3 gb(256 * KW);
@@ -1015,6 +1075,25 @@ bool gemm_asum_ok(const GemmDesc &d) {
          d.K % 4 == 0 && d.lda % 4 == 0 && d.ldb % 4 == 0 && d.a_slab_stride % 4 == 0 && kc > 0 && kc <= 4 * 32 &&
          d.a_splits >= 1 && aligned16(d.A) && aligned16(d.B) && aligned16(d.a_slab) && aligned16(d.a_bias) &&
          aligned16(d.a_out);
+}
+
+static bool glds_fast(const GemmDesc &d) { // launch()'s FAST conditions for mn-contiguous A and B
+  return d.K % 4 == 0 && d.lda % 4 == 0 && d.ldb % 4 == 0 && aligned16(d.A) && aligned16(d.B) &&
+         (d.a_mvalid > 0 ? d.a_mvalid : d.M) % 4 == 0 && d.N % 4 == 0;
+}
+
+bool gemm_group_ok(const GemmDesc &d1, const GemmDesc &d2) {
+  auto one = [](const GemmDesc &d) {
+    return d.M > 0 && d.N > 0 && d.epi == EPI_STORE && !d.a_kc && !d.b_kc && d.tile == TILE_64x64 && !d.a_idx &&
+           !d.a_slab && glds_fast(d);
+  };
+  return one(d1) && one(d2) && !(d2.side_slab && d2.side_count > 0);
+}
+
+void gemm_group(hipStream_t s, const GemmDesc &d1, const GemmDesc &d2) {
+  if (!gemm_group_ok(d1, d2)) throw std::runtime_error("gemm_group: two 64 x 64 mn-contiguous split-K GEMMs");
+  launch<2, 2, 1, 1, false, false, EPI_STORE, 1, 2, 5>(s, d1, &d2); // dispatch_tile's TILE_64x64 instance
+  LBF_KERNEL_CHECK();
 }
 
 void gemm(hipStream_t s, const GemmDesc &d) {

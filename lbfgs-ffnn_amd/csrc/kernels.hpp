@@ -86,6 +86,10 @@ int gemm_row_tiles(int M, int tile);
 // Whether gemm() can take d's A from the previous layer's slabs (a_slab): the 32 x 128 k-contiguous
 // forward split-K tile, no row gather, a k-chunk of at most four k-tiles, 16-B aligned operands.
 bool gemm_asum_ok(const GemmDesc &d);
+// Two GEMMs of the 64 x 64 mn-contiguous split-K dW shape in ONE launch (d1 may carry a side job): the
+// S-LBFGS minibatch's dW GEMMs of adjacent layers once both deltas exist.
+bool gemm_group_ok(const GemmDesc &d1, const GemmDesc &d2);
+void gemm_group(hipStream_t s, const GemmDesc &d1, const GemmDesc &d2);
 void gemm(hipStream_t s, const GemmDesc &d);
 // Tile (BM, BN) the dispatcher picks for a given N (used by the split-K planner).
 void gemm_tile_for(int N, int tile, int *BM, int *BN);

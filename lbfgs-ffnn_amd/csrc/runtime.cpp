@@ -96,6 +96,7 @@ Mlp::Mlp(Ctx *ctx, int nl, const int *dims, const int *acts) : ctx_(ctx) {
   }
   nparams_ = off;
   if (const char *e = std::getenv("LBF_NO_FOLD")) fold_on_ = e[0] != '1'; // tests: the unfolded route
+  if (const char *e = std::getenv("LBF_NO_GROUP")) group_dw_ = e[0] != '1';
 }
 
 // Split-K factor for `tiles` output tiles over a K of `K` rows: the GEMM tiles run two workgroups per
@@ -562,15 +563,14 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     Gl = words_.get();
   }
   if (empty) zero_fill(s, (long long)nparams_ + 2, Gl, ctx_->abort);
-  for (int l = lstart; l >= 0; --l) {
+  // [dW ; db] = [A_in | 1]^T dZ  (layer.cuh:81-84 + sum_rows_kernel kernels.cuh:144-153)
+  auto dw_desc = [&](int l) {
     const Layer &L = layers_[l];
-    const float *Ain = (l == 0) ? X : A_[l - 1].get();
-    // [dW ; db] = [A_in | 1]^T dZ  (layer.cuh:81-84 + sum_rows_kernel kernels.cuh:144-153)
     GemmDesc d;
     d.M = L.in + 1;
     d.N = L.out;
     d.K = int(B);
-    d.A = Ain;
+    d.A = (l == 0) ? X : A_[l - 1].get();
     d.lda = L.in;
     d.a_kc = false;
     d.a_idx = (l == 0) ? idx : nullptr;
@@ -606,40 +606,60 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       d.side_count = nseg;
       d.side_dst = Gl + N1.off - (head ? nfold : 0);
     }
-    const long long seg = (long long)d.M * L.out;
     if (L.splits > 1) {
       d.C = slab_.get() + L.slab_off;
-      d.slab_stride = seg;
-      ProfScope ps(ctx_, PK_DW, l, double(B));
-      gemm(s, d);
+      d.slab_stride = (long long)d.M * L.out;
     } else {
       d.C = Gl + L.off;
+    }
+    return d;
+  };
+  // dX = dZ W^T .* act'(A_prev)   (layer.cuh:89-103 fused with activation_deriv of layer l-1)
+  auto dx_desc = [&](int l) {
+    const Layer &L = layers_[l];
+    const Layer &P0 = layers_[l - 1];
+    GemmDesc x;
+    x.M = int(B);
+    x.N = L.in;
+    x.K = L.out;
+    x.A = D_[l].get();
+    x.lda = L.out;
+    x.a_kc = true;
+    x.B = P + L.off; // B[n=i][k=o] = W[i][o]
+    x.ldb = L.out;
+    x.b_kc = true;
+    x.C = D_[l - 1].get();
+    x.ldc = L.in;
+    x.epi = EPI_DX;
+    x.aux = A_[l - 1].get();
+    x.ldaux = L.in;
+    x.aux_act = P0.act;
+    x.abort = ctx_->abort;
+    x.tile = dx_tile(B, L.in);
+    return x;
+  };
+  for (int l = lstart; l >= 0; --l) {
+    if (l == 1 && group_dw_ && !side_reduced(1, fused, nloss)) {
+      // the last two dW GEMMs in one launch (S-LBFGS minibatches: two small split-K grids that each
+      // leave most of the chip idle at its tail): dX of layer 1 first, since dW of layer 0 reads it
+      const GemmDesc d1 = dw_desc(1), d0 = dw_desc(0);
+      if (gemm_group_ok(d1, d0)) {
+        {
+          ProfScope ps(ctx_, PK_DX, 1, double(B));
+          gemm(s, dx_desc(1));
+        }
+        ProfScope ps(ctx_, PK_DW, 1, double(B));
+        gemm_group(s, d1, d0);
+        break;
+      }
+    }
+    {
       ProfScope ps(ctx_, PK_DW, l, double(B));
-      gemm(s, d);
+      gemm(s, dw_desc(l));
     }
     if (l > 0) {
-      // dX = dZ W^T .* act'(A_prev)   (layer.cuh:89-103 fused with activation_deriv of layer l-1)
-      const Layer &P0 = layers_[l - 1];
-      GemmDesc x;
-      x.M = int(B);
-      x.N = L.in;
-      x.K = L.out;
-      x.A = D_[l].get();
-      x.lda = L.out;
-      x.a_kc = true;
-      x.B = P + L.off; // B[n=i][k=o] = W[i][o]
-      x.ldb = L.out;
-      x.b_kc = true;
-      x.C = D_[l - 1].get();
-      x.ldc = L.in;
-      x.epi = EPI_DX;
-      x.aux = A_[l - 1].get();
-      x.ldaux = L.in;
-      x.aux_act = P0.act;
-      x.abort = ctx_->abort;
-      x.tile = dx_tile(B, L.in);
       ProfScope ps(ctx_, PK_DX, l, double(B));
-      gemm(s, x);
+      gemm(s, dx_desc(l));
     }
   }
   // every layer's partial slabs -> gradient (+ dots and the status block on a single rank)

@@ -195,6 +195,7 @@ private:
   std::vector<DevBuf<float>> A_, D_;
   DevBuf<float> slab_, head_slab_, fslab_, fslab2_;
   float *fslab_buf(size_t l) const { return (l & 1) ? fslab2_.get() : fslab_.get(); } // forward slabs of layer l
+  bool group_dw_ = true;      // dW of layers 1 and 0 in one launch (LBF_NO_GROUP=1: separate launches)
   bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1: the unfolded route, tests)
   bool rowhead_on(long long B) const; // the standalone head fed by the last hidden layer's slabs
   // Planned fold: the last hidden layer's [dW ; db] rows fold_c0_ .. in (fold_ input columns and the
