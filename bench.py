@@ -58,6 +58,9 @@ def parse(argv=None):
                     help="parameter-init stream: cpu = network.hpp:45-71 (all params N(0, s)), cuda = "
                          "network.cuh:36-59 (weights N(0, s), zero biases; the reference's GPU drivers)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--device-warmup", type=int, default=0,
+                    help="L-BFGS: loss/gradient evaluations at the initial point before the run starts (untimed, the "
+                         "same count on every rank; they leave the run's trajectory unchanged)")
     ap.add_argument("--breakdown-last", action="store_true",
                     help="L-BFGS: run the per-section breakdown pass after the warmup iterations (the round-2/3 "
                          "order) instead of before them")
@@ -433,6 +436,11 @@ def run_rank(a, world, rank, local, pkg):
         X, Y = pkg.synth_regression(ctx, hi - lo, dims[0], row0=lo)
     net = pkg.Mlp(ctx, dims, acts)
     P = net.init_params(123, a.init)
+    if a.device_warmup > 0:
+        g = net.new_params()
+        for _ in range(a.device_warmup):
+            net.loss_grad(P, X, Y, inv_scale=1.0 / N, grad=g)
+        del g
     DEV.synchronize()
 
     run = pkg.LbfgsRun(net, P, X, Y, n_global=N, line_search=a.line_search, m=a.m, max_iters=1 << 30, tol=0.0,
