@@ -58,9 +58,10 @@ def parse(argv=None):
                     help="parameter-init stream: cpu = network.hpp:45-71 (all params N(0, s)), cuda = "
                          "network.cuh:36-59 (weights N(0, s), zero biases; the reference's GPU drivers)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--device-warmup", type=int, default=0,
+    ap.add_argument("--device-warmup", type=int, default=300,
                     help="L-BFGS: loss/gradient evaluations at the initial point before the run starts (untimed, the "
-                         "same count on every rank; they leave the run's trajectory unchanged)")
+                         "same count on every rank; they leave the run's trajectory unchanged): the chip reaches its "
+                         "steady clock before the breakdown pass and the timed iterations (profiles/r04/l/drv_*.json)")
     ap.add_argument("--breakdown-last", action="store_true",
                     help="L-BFGS: run the per-section breakdown pass after the warmup iterations (the round-2/3 "
                          "order) instead of before them")

@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
 // lane holds the row's dZ), delta = (dZ W^T) .* act_prev'(a) stored, and the row's [a | 1]^T dZ added into
 // the wave's LDS partial (fp32, row order: what a register accumulator would hold); at the end the four
 // waves' partials are summed in wave order into the block's slab.
-template <int NJ, int OP, bool AHEAD>
+template <int NJ, int OP>
 __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
   if (a.abort && *a.abort) return;
   extern __shared__ __attribute__((aligned(16))) float red[]; // [4][(H + 1) * Out]
@@ -220,66 +220,33 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
   float *mine = red + wave * per;
   double sse = 0.0;
   int r = 0;
-  // one row ahead when the slabs fit one round (rpw > 1: large batches): row r + 1's target and slab
-  // values are requested before row r's arithmetic, from a clamped row (unconditional loads)
-  constexpr bool ahead = AHEAD; // the host's choice: a.splits <= SU && a.rpw > 1
-  float yn[OP], vn[NJ][SU];
-  auto load_row = [&](long long b, float(&yv)[OP], float(&v)[NJ][SU]) __attribute__((always_inline)) {
-    const long long yrow = a.idx ? (long long)a.idx[b] : b;
-#pragma unroll
-    for (int o = 0; o < OP; ++o) yv[o] = a.Y[yrow * Out + (o < Out ? o : Out - 1)];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const float *src = a.fslab + b * H + (cv[j] ? lane + 64 * j : H - 1);
-#pragma unroll
-      for (int u = 0; u < SU; ++u) v[j][u] = src[(long long)min(u, a.splits - 1) * a.stride];
-    }
-  };
-  if constexpr (ahead) load_row(min(rbase, a.B - 1), yn, vn);
   for (; r < a.rpw; ++r) {
     const long long b = rbase + r;
     if (b >= a.B) break; // wave-uniform
+    // ---- loads: the target row first (two deep through idx), then the slabs ----
+    const long long yrow = a.idx ? (long long)a.idx[b] : b;
     float yv[OP];
+#pragma unroll
+    for (int o = 0; o < OP; ++o) yv[o] = a.Y[yrow * Out + (o < Out ? o : Out - 1)];
     float sum[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) sum[j] = 0.0f;
-    if constexpr (ahead) {
+    for (int k0 = 0; k0 < a.splits; k0 += SU) {
       float v[NJ][SU];
 #pragma unroll
-      for (int o = 0; o < OP; ++o) yv[o] = yn[o];
+      for (int j = 0; j < NJ; ++j) {
+        const float *src = a.fslab + b * H + (cv[j] ? lane + 64 * j : H - 1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int u = 0; u < SU; ++u) v[j][u] = vn[j][u];
-      load_row(min(b + 1, a.B - 1), yn, vn);
+        for (int u = 0; u < SU; ++u) v[j][u] = src[(long long)min(k0 + u, a.splits - 1) * a.stride];
+      }
+      // every load of the round (and the targets) issued before the first use: the compiler may not sink
+      // a load into the uniform branches below
       asm volatile("" ::: "memory");
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int u = 0; u < SU; ++u)
-          if (u < a.splits) sum[j] += v[j][u];
-    } else {
-      // ---- loads: the target row first (two deep through idx), then the slabs ----
-      const long long yrow = a.idx ? (long long)a.idx[b] : b;
-#pragma unroll
-      for (int o = 0; o < OP; ++o) yv[o] = a.Y[yrow * Out + (o < Out ? o : Out - 1)];
-      for (int k0 = 0; k0 < a.splits; k0 += SU) {
-        float v[NJ][SU];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const float *src = a.fslab + b * H + (cv[j] ? lane + 64 * j : H - 1);
-#pragma unroll
-          for (int u = 0; u < SU; ++u) v[j][u] = src[(long long)min(k0 + u, a.splits - 1) * a.stride];
-        }
-        // every load of the round (and the targets) issued before the first use: the compiler may not sink
-        // a load into the uniform branches below
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int u = 0; u < SU; ++u)
-            if (k0 + u < a.splits) sum[j] += v[j][u];
-      }
+          if (k0 + u < a.splits) sum[j] += v[j][u];
     }
     // ---- activations (fwd_reduce_act's arithmetic) ----
     float av[NJ];
@@ -360,30 +327,26 @@ void rowhead(hipStream_t s, const RowHeadArgs &a) {
   LBF_REQUIRE(rowhead_supported(a.H, a.Out) && a.splits >= 1 && a.rpw == rowhead_rpw(a.B), "rowhead: shape");
   const size_t shmem = size_t(4) * (a.H + 1) * a.Out * sizeof(float);
   const int nj = (a.H + 63) / 64, op = (a.Out + 3) / 4 * 4;
-  const bool ahead = a.splits <= 8 && a.rpw > 1; // rowhead_kernel's SU
   const dim3 grid(unsigned(rowhead_nwg(a.B))), block(256);
   // <NJ, OP> for hidden widths up to 256 and outputs up to 16; the attribute once per instance (thread-safe)
-#define LBF_ROWHEAD_CASE(NJ, OP, AH)                                                                          \
-  if (nj == NJ && op == OP && ahead == AH) {                                                                 \
+#define LBF_ROWHEAD_CASE(NJ, OP)                                                                              \
+  if (nj == NJ && op == OP) {                                                                                \
     static const bool attr_set = [] {                                                                        \
-      LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(rowhead_kernel<NJ, OP, AH>),                \
+      LBF_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(rowhead_kernel<NJ, OP>),                    \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));                   \
       return true;                                                                                           \
     }();                                                                                                     \
     (void)attr_set;                                                                                          \
-    hipLaunchKernelGGL((rowhead_kernel<NJ, OP, AH>), grid, block, shmem, s, a);                              \
+    hipLaunchKernelGGL((rowhead_kernel<NJ, OP>), grid, block, shmem, s, a);                                  \
     LBF_KERNEL_CHECK();                                                                                      \
     return;                                                                                                  \
   }
-#define LBF_ROWHEAD_OP(NJ, AH)                                                                                \
-  LBF_ROWHEAD_CASE(NJ, 4, AH) LBF_ROWHEAD_CASE(NJ, 8, AH) LBF_ROWHEAD_CASE(NJ, 12, AH) LBF_ROWHEAD_CASE(NJ, 16, AH)
-#define LBF_ROWHEAD_NJ(NJ) LBF_ROWHEAD_OP(NJ, false) LBF_ROWHEAD_OP(NJ, true)
+#define LBF_ROWHEAD_NJ(NJ) LBF_ROWHEAD_CASE(NJ, 4) LBF_ROWHEAD_CASE(NJ, 8) LBF_ROWHEAD_CASE(NJ, 12) LBF_ROWHEAD_CASE(NJ, 16)
   LBF_ROWHEAD_NJ(1)
   LBF_ROWHEAD_NJ(2)
   LBF_ROWHEAD_NJ(3)
   LBF_ROWHEAD_NJ(4)
 #undef LBF_ROWHEAD_NJ
-#undef LBF_ROWHEAD_OP
 #undef LBF_ROWHEAD_CASE
   throw Error(2, "rowhead: no instance for this shape");
 }

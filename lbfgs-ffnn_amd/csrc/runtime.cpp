@@ -164,17 +164,7 @@ void Mlp::plan(long long B) {
     } else if (L.out <= 64 && cdiv(B, 128) < 256) {
       L.ftile = TILE_32x128;
     }
-    static const int fsplit_bm = env_int("LBF_FWD_SPLIT_BM", 0), fsplit_n = env_int("LBF_FWD_SPLIT", 0);
-    if (fsplit_n > 1 && L.out > 64 && L.out <= 128 && L.in >= 256) {
-      // A/B: split-K forward of a 65..128-wide layer (the row head then takes the output layer)
-      L.ftile = fsplit_bm == 32 ? TILE_32x128 : fsplit_bm == 64 ? TILE_64x128 : TILE_AUTO;
-      const long long fkc = cdiv(cdiv(L.in, fsplit_n), 32) * 32, fs = cdiv(L.in, fkc);
-      if (fs > 1) {
-        L.fsplits = int(fs);
-        L.fk_chunk = int(fkc);
-        fslab = std::max(fslab, size_t(fs) * size_t(B) * L.out);
-      }
-    } else if (L.ftile != TILE_AUTO) {
+    if (L.ftile != TILE_AUTO) {
       // no split: the fused head and the activation need the full K
     } else if (ftiles < 192 && L.in >= 256) {
       // Few rows of a wide layer (S-LBFGS minibatches: 256 x 784 -> 512 is 8 tiles of 128 x 128): split

@@ -40,7 +40,7 @@ __device__ __forceinline__ double t_wave_sum(double v) { return wave_sum_f64(v);
 // per-vector 64-lane reductions. Rows are stored transposed, [nc][nb], so tail_cols reads each
 // column contiguously. 128-column groups halve the grid (n = 101,770: 796 blocks), which keeps every
 // block resident at once (this kernel's SGPR count admits 6 blocks per CU).
-template <int VPW, int U>
+template <int VPW>
 __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   constexpr int TC = TAIL_COLS, C = TAIL_COLS / 64;
   const RedAllArgs &ra = a.ra;
@@ -114,8 +114,7 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
 #pragma unroll
   for (int c = 0; c < C; ++c) acc[c] = 0.0;
   if (S.splits > 0) {
-    // U loads per column in flight per round (clamped duplicates past the end): 8, or 24 when a segment has
-    // more than 32 splits (cfg 2's 82 dW slabs: one round instead of three)
+    constexpr int U = 8; // loads per column in flight per round (clamped duplicates past the end)
     for (int k = stripe; k < S.splits; k += 4 * U) {
       float x[U][C];
 #pragma unroll
@@ -408,24 +407,13 @@ static size_t fin_shmem(const TailArgs &a) {
 
 void tail_reduce(hipStream_t s, const TailArgs &a) {
   if (a.nb <= 0) return;
-  int maxsp = 0;
-  for (int i = 0; i < a.ra.nseg; ++i) maxsp = std::max(maxsp, a.ra.seg[i].splits);
-  static const int force_u = env_int("LBF_TAIL_U", 0);
-  const bool wide = force_u ? force_u > 8 : maxsp > 32;
-  const dim3 grid(unsigned(a.nb)), block(256);
-#define LBF_TR_CASE(V)                                                                                        \
-  case V:                                                                                                    \
-    if (wide) hipLaunchKernelGGL((tail_reduce_kernel<V, 24>), grid, block, 0, s, a);                         \
-    else hipLaunchKernelGGL((tail_reduce_kernel<V, 8>), grid, block, 0, s, a);                               \
-    break;
   switch (tail_vpw(a.h.m)) {
-    LBF_TR_CASE(2)
-    LBF_TR_CASE(4)
-    LBF_TR_CASE(8)
-    LBF_TR_CASE(16)
+  case 2: hipLaunchKernelGGL(tail_reduce_kernel<2>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 4: hipLaunchKernelGGL(tail_reduce_kernel<4>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 8: hipLaunchKernelGGL(tail_reduce_kernel<8>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 16: hipLaunchKernelGGL(tail_reduce_kernel<16>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
   default: throw Error(2, "tail_reduce: history size not supported by the fused tail");
   }
-#undef LBF_TR_CASE
   LBF_KERNEL_CHECK();
   if (!a.cols_done) throw Error(2, "tail_reduce: needs the arrival counter (cols_done)");
   hipLaunchKernelGGL(tail_cols_fin_kernel, dim3(unsigned(a.nc)), dim3(TF_THREADS), fin_shmem(a), s, a);

@@ -134,6 +134,16 @@ class _Net:
     def init_params(self, seed, init):
         return torch.zeros(self.n)
 
+    def new_params(self):
+        return torch.zeros(self.n)
+
+    def loss_grad(self, P, X, Y, inv_scale=None, grad=None):
+        # bench's device warm-up: the same count on every rank, each evaluation one collective (the DP route)
+        g = torch.ones(4, dtype=torch.float64)
+        dist.all_reduce(g)
+        self.warm = getattr(self, "warm", 0) + 1
+        return 0.0, grad
+
 
 class _Run:
     """Stands in for LbfgsRun / SlbfgsRun: every iteration all-reduces a rank-tagged vector through gloo (the
