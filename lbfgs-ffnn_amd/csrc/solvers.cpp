@@ -799,22 +799,11 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
   // ev_g2_[t & 1] and the context thread waits on it after twin_wait(task t); task t + 2 re-records it
   // only after being posted at step t + 1, after that wait.
   std::vector<long long> tk(size_t(std::max(m_inner, 1)), 0);
-  // LBF_DIAG_ANCHOR (timing diagnostics only, wrong results): 1 = no anchor gradients (zeros), the inner
-  // step's chain alone; 2 = the anchor gradient on the context stream right before the step's evaluation
-  static const int diag_anchor = env_int("LBF_DIAG_ANCHOR", 0);
-  if (diag_anchor == 1 && twin_free) LBF_HIP(hipMemsetAsync(ganc_.get(), 0, ganc_.size() * sizeof(float), s));
   auto anchor_ahead = [&](int t) { // twin stream: the anchor half of step t's block
     const Slice sl = mb[t];
     float *gdst = g2(t);
     const float *xr = rows_x(sl), *yr = rows_y(sl);
     hipEvent_t efree = twin_free ? nullptr : ev_free_[t & 1], eg2 = twin_free ? ev_anc_[size_t(t)] : ev_g2_[t & 1];
-    if (diag_anchor == 1 || diag_anchor == 2) {
-      if (diag_anchor == 2)
-        net_->loss_grad(w_.get(), gdst, xr, yr, nullptr, sl.cnt, 1.0 / double(sl.total), prm_.lambda, nullptr,
-                        nullptr);
-      LBF_HIP(hipEventRecord(eg2, ctx_->stream));
-      return;
-    }
     tk[size_t(t)] = twin_post([=]() {
       if (efree) LBF_HIP(hipStreamWaitEvent(tctx_->stream, efree, 0)); // step t - 2's direction read it
       if (dp)
