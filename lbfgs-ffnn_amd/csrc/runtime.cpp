@@ -254,8 +254,6 @@ void Mlp::plan(long long B) {
 // S-LBFGS's b = 256 gives 8 tiles of 128 x 128 for a 512-wide layer), then 32 x 128 (four times the
 // row tiles; the epilogue needs the full K, so no split-K here).
 int Mlp::dx_tile(long long B, int N) const {
-  static const int force = env_int("LBF_DX_TILE", -1); // A/B
-  if (force >= 0 && N >= 128 && cdiv(B, 128) * cdiv((long long)N, 128) < ctx_->cus / 2) return force;
   if (N >= 128 && cdiv(B, 128) * cdiv((long long)N, 128) < ctx_->cus / 2) return TILE_32x128;
   return TILE_AUTO;
 }
