@@ -1,35 +1,39 @@
-"""Inter-kernel gaps on one stream from a rocprofv3 --kernel-trace CSV: for each (kernel, next kernel) pair,
-the median time from the first's end to the second's start (launch latency shows inside the durations; a
-gap is extra idle time).   python3 profiles/gaps.py run_kernel_trace.csv [--top 8]"""
+"""Idle gaps on the GPU timeline of a rocprofv3 kernel trace: for every kernel name, how long the device
+sat idle (no kernel of this process running) right before that kernel started, over the last `--tail`
+dispatches (the timed region). A large gap before one kernel means the host (or a wait) was late with it.
+
+    python3 profiles/gaps.py gpurun_out/.../run_kernel_trace.csv [--tail 2000]
+"""
 import argparse
-import collections
 import csv
-import statistics
+from collections import defaultdict
+
+
+def short(name):
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
+    return n.replace("void ", "").replace("lbf::", "")[:70]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--top", type=int, default=8)
+    ap.add_argument("--tail", type=int, default=2000)
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
-    by = collections.defaultdict(list)
-    for r in rows:
-        by[r["Stream_Id"]].append(r)
-    for sid, v in sorted(by.items(), key=lambda kv: -len(kv[1])):
-        if len(v) < 20:
-            continue
-        v.sort(key=lambda r: int(r["Start_Timestamp"]))
-        gaps = collections.defaultdict(list)
-        for x, y in zip(v[len(v) // 4:-1], v[len(v) // 4 + 1:]):
-            g = (int(y["Start_Timestamp"]) - int(x["End_Timestamp"])) / 1e3
-            if -1 < g < 200:
-                gaps[(x["Kernel_Name"][:38], y["Kernel_Name"][:38])].append(g)
-        busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in v[len(v) // 4:]) / 1e6
-        span = (int(v[-1]["End_Timestamp"]) - int(v[len(v) // 4]["Start_Timestamp"])) / 1e6
-        print(f"stream {sid}: {len(v)} launches, last 3/4: busy {busy:.2f} ms of {span:.2f} ms")
-        for k, g in sorted(gaps.items(), key=lambda kv: -sum(kv[1]))[:a.top]:
-            print(f"  {k[0]:38s} -> {k[1]:38s} n={len(g):5d} med={statistics.median(g):6.2f} sum={sum(g) / 1e3:7.2f} ms")
+    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows)
+    ev = ev[-a.tail:]
+    gap = defaultdict(list)
+    busy = 0
+    end = ev[0][1]
+    for s, e, n in ev[1:]:
+        gap[n].append(max(0, s - end) / 1000.0)
+        busy += e - max(s, end) if e > end else 0
+        end = max(end, e)
+    span = (ev[-1][1] - ev[0][0]) / 1000.0
+    print(f"span {span:.1f} us over {len(ev)} dispatches, busy {busy / 1000.0:.1f} us ({busy / 10.0 / span:.1f} %)")
+    for n, g in sorted(gap.items(), key=lambda kv: -sum(kv[1])):
+        g2 = sorted(g)
+        print(f"{n:72s} n={len(g):5d} gap avg {sum(g) / len(g):7.2f} med {g2[len(g2) // 2]:7.2f} total {sum(g):9.1f} us")
 
 
 if __name__ == "__main__":
