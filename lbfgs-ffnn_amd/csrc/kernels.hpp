@@ -190,6 +190,7 @@ struct RedAllArgs {
   double inv_scale = 1.0;
   double *scal = nullptr;
   const int *abort = nullptr;
+  float *sse_hilo = nullptr;    // data parallel: one extra block packs sum(sse_part[0..nsse)) as fp32 (hi, lo) here
 };
 constexpr int RA_COLS = 64;
 constexpr int RA_GPB = 4; // column groups per reduce_all block for single-pass segments

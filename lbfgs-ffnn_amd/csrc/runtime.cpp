@@ -719,9 +719,11 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     if (empty) return; // zero-filled at entry
     RedAllArgs loc = ra;
     loc.dots = 0;
+    loc.sse_part = loss_part_.get(); // the SSE words in an extra block of the same launch
+    loc.nsse = nloss;
+    loc.sse_hilo = Gl + nparams_;
     ProfScope ps(ctx_, PK_SLAB, 0);
     reduce_all(s, loc);
-    sse_pack(s, loss_part_.get(), nloss, Gl + nparams_, ctx_->abort);
   };
   bool tail_ok = tf != nullptr && !local;
   for (int l = 0; l < nl && tail_ok; ++l) tail_ok = ra.seg[l].parts == 1;

@@ -343,11 +343,27 @@ __device__ __forceinline__ void ra_block(const RedAllArgs &a, const RedSeg &S, i
   ra_columns<J>(a, S, S.cg0 + int(cgl0), cgl0, colsum);
 }
 
+// One wave (lane t < 64): the rank's SSE partials in a fixed order, stored as an fp32 (hi, lo) pair.
+__device__ __forceinline__ void sse_pack_body(const double *sse_part, int nsse, float *hilo, int t) {
+  double s = 0.0;
+  for (int r = t; r < nsse; r += 64) s += sse_part[r];
+  s = wave_sum(s);
+  if (t == 0) {
+    const float hi = float(s);
+    hilo[0] = hi;
+    hilo[1] = float(s - double(hi));
+  }
+}
+
 __global__ __launch_bounds__(256) void reduce_all_kernel(const RedAllArgs a) {
   if (a.abort && *a.abort) return;
   __shared__ double part[4][RA_GPB * RA_COLS];
   const int t = threadIdx.x, lane = t & 63, stripe = t >> 6;
   const int b = blockIdx.x;
+  if (b == a.nwg) { // the extra block of a data-parallel local reduction: the SSE words (sse_pack's launch)
+    if (t < 64) sse_pack_body(a.sse_part, a.nsse, a.sse_hilo, t);
+    return;
+  }
   int si = 0;
   while (si + 1 < a.nseg && a.seg[si + 1].wg0 <= b) ++si;
   const RedSeg S = a.seg[si];
@@ -478,8 +494,8 @@ void sse_loss(hipStream_t s, const double *sse_part, int nsse, const float *hilo
 }
 
 void reduce_all(hipStream_t s, const RedAllArgs &a) {
-  if (a.nwg <= 0) return;
-  hipLaunchKernelGGL(reduce_all_kernel, dim3(unsigned(a.nwg)), dim3(256), 0, s, a);
+  if (a.nwg <= 0 && !a.sse_hilo) return;
+  hipLaunchKernelGGL(reduce_all_kernel, dim3(unsigned(a.nwg + (a.sse_hilo ? 1 : 0))), dim3(256), 0, s, a);
   LBF_KERNEL_CHECK();
   if (a.nfin > 0 || a.dots) {
     hipLaunchKernelGGL(reduce_fin_kernel, dim3(1), dim3(RF_THREADS), 0, s, a);
@@ -1357,18 +1373,11 @@ void eval_tail(hipStream_t s, const double *dots_part, int nd, const double *sse
 }
 
 // Data-parallel: reduce this rank's SSE partials and store them as an fp32 (hi, lo) pair behind the
-// gradient, so one all-reduce of [grad | hi | lo] carries the loss with ~fp64 accuracy.
+// gradient, so one all-reduce of [grad | hi | lo] carries the loss with ~fp64 accuracy (sse_pack_body).
 __global__ __launch_bounds__(64) void sse_pack_kernel(const double *sse_part, int nsse, float *hilo,
                                                       const int *abort) {
   if (abort && *abort) return;
-  double s = 0.0;
-  for (int r = threadIdx.x; r < nsse; r += 64) s += sse_part[r];
-  s = wave_sum(s);
-  if (threadIdx.x == 0) {
-    const float hi = float(s);
-    hilo[0] = hi;
-    hilo[1] = float(s - double(hi));
-  }
+  sse_pack_body(sse_part, nsse, hilo, threadIdx.x);
 }
 
 void sse_pack(hipStream_t s, const double *sse_part, int nsse, float *hilo, const int *abort) {
