@@ -190,31 +190,67 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
 template <int NJ, int OP>
 __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
   if (a.abort && *a.abort) return;
-  extern __shared__ __attribute__((aligned(16))) float red[]; // [4][(H + 1) * Out]
+  // [4][(H + 1) * Out] the waves' partials | [(H + 1) * Out] the output layer's W and bias
+  extern __shared__ __attribute__((aligned(16))) float red[];
   __shared__ double ssew[4];
-  constexpr int SU = 8; // splits per column in flight per round
+  constexpr int SU = 8;                                  // splits per column in flight per round
+  constexpr int WST = ((64 * NJ + 1) * OP + 255) / 256; // staging loads of [W ; b] per thread
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int H = a.H, Out = a.Out, per = (H + 1) * Out;
   const long long rbase = ((long long)blockIdx.x * 4 + wave) * a.rpw;
-  // the output layer's weights of this lane's columns, both biases: unconditional loads from clamped
-  // addresses, NOT masked (a masked load compiles to a branch around it and a wait inside, one round trip
-  // per value). The clamped entries only ever meet zeros: av = 0 on columns past H, dZ = 0 on outputs past
-  // Out, and those products are never stored.
-  float w2[NJ][OP], hb[NJ];
+  float *wl = red + 4 * per;
+  // The output layer's [W ; b] (contiguous, (H + 1) Out floats) through LDS: the block reads it with
+  // lane-contiguous loads; read per lane (its columns' rows of W, Out apart) the same values were 48
+  // strided load instructions per wave, each touching ~40 cache lines. Every load below is unconditional
+  // from a clamped address, NOT masked (a masked load compiles to a branch around it and a wait inside,
+  // one round trip per value); clamped entries only ever meet zeros (av = 0 on columns past H, dZ = 0 on
+  // outputs past Out) and those products are never stored.
+  float wst[WST];
+#pragma unroll
+  for (int u = 0; u < WST; ++u) {
+    const int e = t + 256 * u;
+    wst[u] = a.P[e < per ? e : per - 1];
+  }
+  float hb[NJ];
   bool cv[NJ];
+  int ccj[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int c = lane + 64 * j;
     cv[j] = c < H;
-    const int cc = cv[j] ? c : H - 1;
-    hb[j] = a.hbias[cc];
-#pragma unroll
-    for (int o = 0; o < OP; ++o) w2[j][o] = a.P[(long long)cc * Out + (o < Out ? o : Out - 1)];
+    ccj[j] = cv[j] ? c : H - 1;
+    hb[j] = a.hbias[ccj[j]];
   }
-  float b2[OP], dbacc[OP];
+  // the wave's first row (clamped into the batch): its target and slab values in the same round trip
+  const bool pre = a.splits <= SU; // wave-uniform
+  float ypre[OP], vpre[NJ][SU];
+  {
+    const long long b = rbase < a.B ? rbase : a.B - 1;
+    const long long yrow = a.idx ? (long long)a.idx[b] : b;
+#pragma unroll
+    for (int o = 0; o < OP; ++o) ypre[o] = a.Y[yrow * Out + (o < Out ? o : Out - 1)];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const float *src = a.fslab + b * H + ccj[j];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) vpre[j][u] = src[(long long)min(u, a.splits - 1) * a.stride];
+    }
+  }
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int u = 0; u < WST; ++u) {
+    const int e = t + 256 * u;
+    if (e < per) wl[e] = wst[u];
+  }
+  lds_barrier();
+  float w2[NJ][OP], b2[OP], dbacc[OP];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int o = 0; o < OP; ++o) w2[j][o] = wl[ccj[j] * Out + (o < Out ? o : Out - 1)];
 #pragma unroll
   for (int o = 0; o < OP; ++o) {
-    b2[o] = a.P[(long long)H * Out + (o < Out ? o : Out - 1)];
+    b2[o] = wl[H * Out + (o < Out ? o : Out - 1)];
     dbacc[o] = 0.0f;
   }
   float *mine = red + wave * per;
@@ -223,30 +259,40 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
   for (; r < a.rpw; ++r) {
     const long long b = rbase + r;
     if (b >= a.B) break; // wave-uniform
-    // ---- loads: the target row first (two deep through idx), then the slabs ----
-    const long long yrow = a.idx ? (long long)a.idx[b] : b;
     float yv[OP];
-#pragma unroll
-    for (int o = 0; o < OP; ++o) yv[o] = a.Y[yrow * Out + (o < Out ? o : Out - 1)];
     float sum[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) sum[j] = 0.0f;
-    for (int k0 = 0; k0 < a.splits; k0 += SU) {
-      float v[NJ][SU];
+    if (r == 0 && pre) { // loaded above
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const float *src = a.fslab + b * H + (cv[j] ? lane + 64 * j : H - 1);
-#pragma unroll
-        for (int u = 0; u < SU; ++u) v[j][u] = src[(long long)min(k0 + u, a.splits - 1) * a.stride];
-      }
-      // every load of the round (and the targets) issued before the first use: the compiler may not sink
-      // a load into the uniform branches below
-      asm volatile("" ::: "memory");
+      for (int o = 0; o < OP; ++o) yv[o] = ypre[o];
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int u = 0; u < SU; ++u)
-          if (k0 + u < a.splits) sum[j] += v[j][u];
+          if (u < a.splits) sum[j] += vpre[j][u];
+    } else {
+      // ---- loads: the target row first (two deep through idx), then the slabs ----
+      const long long yrow = a.idx ? (long long)a.idx[b] : b;
+#pragma unroll
+      for (int o = 0; o < OP; ++o) yv[o] = a.Y[yrow * Out + (o < Out ? o : Out - 1)];
+      for (int k0 = 0; k0 < a.splits; k0 += SU) {
+        float v[NJ][SU];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const float *src = a.fslab + b * H + ccj[j];
+#pragma unroll
+          for (int u = 0; u < SU; ++u) v[j][u] = src[(long long)min(k0 + u, a.splits - 1) * a.stride];
+        }
+        // every load of the round (and the targets) issued before the first use: the compiler may not sink
+        // a load into the uniform branches below
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int u = 0; u < SU; ++u)
+            if (k0 + u < a.splits) sum[j] += v[j][u];
+      }
     }
     // ---- activations (fwd_reduce_act's arithmetic) ----
     float av[NJ];
@@ -325,7 +371,7 @@ int rowhead_nwg(long long B) { return int(cdiv(std::max(1LL, B), 4LL * rowhead_r
 
 void rowhead(hipStream_t s, const RowHeadArgs &a) {
   LBF_REQUIRE(rowhead_supported(a.H, a.Out) && a.splits >= 1 && a.rpw == rowhead_rpw(a.B), "rowhead: shape");
-  const size_t shmem = size_t(4) * (a.H + 1) * a.Out * sizeof(float);
+  const size_t shmem = size_t(5) * (a.H + 1) * a.Out * sizeof(float); // 4 wave partials + [W ; b]
   const int nj = (a.H + 63) / 64, op = (a.Out + 3) / 4 * 4;
   const dim3 grid(unsigned(rowhead_nwg(a.B))), block(256);
   // <NJ, OP> for hidden widths up to 256 and outputs up to 16; the attribute once per instance (thread-safe)
