@@ -25,14 +25,6 @@ namespace lbf {
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void dir_lds_void_t;
-typedef __attribute__((address_space(1))) void dir_glb_void_t;
-
-// 16 B per lane, global -> LDS (global_load_lds_dwordx4): lane l's value lands at lds_wave_base + 16 l
-__device__ __forceinline__ void dir_glds16(const float *src, float *lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((dir_glb_void_t *)src, (dir_lds_void_t *)lds_wave_base, 16, 0, 0);
-}
-__device__ __forceinline__ void dir_vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // C columns per lane (64*C per block) as Q = C/4 quads, lane l owning columns 256q + 4l .. +3 of quad q;
 // VPW history vectors per wave (v = wave + 4j).
@@ -65,6 +57,23 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) live[q][c] = col0[q] + c < h.n;
   }
+  f32x4 vv[VPW][Q];
+  unsigned zero_mask = 0; // bit j: vector j of this wave is not live (or is the slot being overwritten)
+#pragma unroll
+  for (int j = 0; j < VPW; ++j) {
+    const int v = wave + 4 * j; // wave-uniform: the branch is scalar, no per-lane wait
+#pragma unroll
+    for (int q = 0; q < Q; ++q) vv[j][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (v < nvec) {
+      const int slot = __builtin_amdgcn_readfirstlane(ist[IST_ORDER + (v < count0 ? v : v - count0)]);
+      const float *base = (v < count0 ? h.S : h.Y) + (long long)slot * h.ld;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) vv[j][q] = *reinterpret_cast<const f32x4 *>(base + e4[q]);
+      if (g.has_pair && slot == w) zero_mask |= 1u << j;
+    } else {
+      zero_mask |= 1u << j;
+    }
+  }
   // g.ga from its split-K slabs (gred_on): wave w sums the splits k = w (mod 4) of this lane's quads in split
   // order (reduce_all_kernel's stripes) into LDS; wave 0 adds the four stripes after the barrier,
   // ((0 + 1) + 2) + 3 as reduce_all does: bitwise its gradient. History::update defers only segment tables
@@ -89,64 +98,15 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
       }
     }
   };
-  // The first round of the gradient's slabs (split k = wave; at most four splits is one round, cfg 4) is
-  // requested BEFORE the history values: the split sums then wait only for these loads (the later loads
-  // stay in flight), where a wait for the most recent load would drain every load of the wave.
-  f32x4 x0[Q];
-  int nsp0[Q];
-  int kmax = 0; // (scalar loop over the table: ahead of the loads, so no loop separates them from their use)
-  if (a.gred_on)
-    for (int si = 0; si < a.gred.nseg; ++si) kmax = max(kmax, a.gred.seg[si].splits);
-  if (a.gred_on) {
-#pragma unroll
-    for (int q = 0; q < Q; ++q) { // unconditional, clamped into the quad's slabs (or G itself)
-      const float *base;
-      long long col, strd;
-      seg_of(e4[q], base, col, strd, nsp0[q]);
-      const int kc = min(wave, max(nsp0[q] - 1, 0));
-      x0[q] = *reinterpret_cast<const f32x4 *>(base + col + (long long)kc * strd);
-    }
-  }
-  f32x4 vv[VPW][Q];
-  unsigned zero_mask = 0; // bit j: vector j of this wave is not live (or is the slot being overwritten)
-#pragma unroll
-  for (int j = 0; j < VPW; ++j) {
-    const int v = wave + 4 * j; // wave-uniform: the branch is scalar, no per-lane wait
-#pragma unroll
-    for (int q = 0; q < Q; ++q) vv[j][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (v < nvec) {
-      const int slot = __builtin_amdgcn_readfirstlane(ist[IST_ORDER + (v < count0 ? v : v - count0)]);
-      const float *base = (v < count0 ? h.S : h.Y) + (long long)slot * h.ld;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) vv[j][q] = *reinterpret_cast<const f32x4 *>(base + e4[q]);
-      if (g.has_pair && slot == w) zero_mask |= 1u << j;
-    } else {
-      zero_mask |= 1u << j;
-    }
-  }
-  // the operands of v = g - gb + gc that wave 0 reads after the stripes' barrier: requested now, in the same
-  // round trip as the history and slab values (gw, gb, gc by LDS-DMA, no registers held; w into registers)
-  __shared__ __attribute__((aligned(16))) float gx[3][TC];
-  float wwp[Q][4];
-  if (a.gred_on && wave == 0) {
-    const RedAllArgs &R = a.gred;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      dir_glds16(R.G + e4[q], &gx[0][256 * q]); // unsplit segments: G as written
-      dir_glds16((g.gb ? g.gb : R.G) + e4[q], &gx[1][256 * q]);
-      dir_glds16((g.gc ? g.gc : R.G) + e4[q], &gx[2][256 * q]);
-      const float *wsrc = R.w ? R.w : R.G; // unconditional loads (used only when l2 and lambda are set)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) wwp[q][c] = wsrc[min(e4[q] + c, h.n - 1)]; // w is exactly n long
-    }
-  }
   if (a.gred_on) { // (History::update: has_g, no pair)
     const RedAllArgs &R = a.gred;
+    int kmax = 0;
+    for (int si = 0; si < R.nseg; ++si) kmax = max(kmax, R.seg[si].splits);
 #pragma unroll
     for (int q = 0; q < Q; ++q)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) gpart[wave][256 * q + 4 * lane + c] = wave < nsp0[q] ? 0.0 + double(x0[q][c]) : 0.0; // as 0 += x
-    for (int k0 = wave + 4; k0 < kmax; k0 += 4) { // further rounds: one round trip per four splits
+      for (int c = 0; c < 4; ++c) gpart[wave][256 * q + 4 * lane + c] = 0.0;
+    for (int k0 = wave; k0 < kmax; k0 += 4) { // one round trip per four splits
       f32x4 x[Q];
       int nsp[Q];
 #pragma unroll
@@ -165,18 +125,20 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
     }
     lds_barrier();
     if (wave == 0) {
-      dir_vm_wait0(); // this wave's LDS-DMA of gx has landed
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const float *base;
         long long col, strd;
         int nsp;
         seg_of(e4[q], base, col, strd, nsp);
-        const f32x4 gw = *reinterpret_cast<const f32x4 *>(&gx[0][256 * q + 4 * lane]);
+        const f32x4 gw = *reinterpret_cast<const f32x4 *>(R.G + e4[q]); // unsplit segments: G as written
         // the other operands of v = g - gb + gc (null operands read G, masked)
-        const f32x4 gb4 = *reinterpret_cast<const f32x4 *>(&gx[1][256 * q + 4 * lane]);
-        const f32x4 gc4 = *reinterpret_cast<const f32x4 *>(&gx[2][256 * q + 4 * lane]);
-        const float *ww = wwp[q];
+        const f32x4 gb4 = *reinterpret_cast<const f32x4 *>((g.gb ? g.gb : R.G) + e4[q]);
+        const f32x4 gc4 = *reinterpret_cast<const f32x4 *>((g.gc ? g.gc : R.G) + e4[q]);
+        float ww[4] = {0.f, 0.f, 0.f, 0.f};
+        if (R.l2 && R.lambda != 0.0) // uniform; w is exactly n long
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ww[c] = R.w[min(e4[q] + c, h.n - 1)];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int qq = 256 * q + 4 * lane + c;
