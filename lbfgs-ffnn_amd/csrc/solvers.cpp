@@ -52,6 +52,9 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
   // (LBF_SPEC_DEPTH, default 3; 0 = host-driven). Host callbacks synchronise anyway.
   depth_ = 3;
   if (const char *e = std::getenv("LBF_SPEC_DEPTH")) depth_ = std::max(0, std::min(16, std::atoi(e)));
+  // Wolfe retries: the trial's backward phase enqueued with its loss-only forward, so the host waits once
+  // per trial instead of twice (LBF_SPEC_GRAD=0: the gradient only after the Armijo test)
+  spec_grad_ = env_int("LBF_SPEC_GRAD", 1) != 0;
   if (!obj_->async()) depth_ = 0;
   // Fused optimizer tail on the speculative path (LBF_FUSED_TAIL=0 disables). It is a latency design
   // (one block per 64 coordinates, a partial row each): past kFusedTailMaxN the classic Gram sweep +
@@ -231,6 +234,10 @@ void LbfgsSolver::finish_wolfe(lbf_record *rec) {
         if (split) { // f(x + alpha p) first; the gradient only once Armijo holds (:136-146)
           obj_->eval_loss(xt_, hist_.scal());
           have_grad = false;
+          if (spec_grad_) { // enqueued before the test: one wait per trial (wasted only if Armijo fails)
+            obj_->eval_grad_after_loss(xt_, gt_, p_.get(), hist_.scal());
+            have_grad = true;
+          }
         } else {
           eval(xt_, gt_, p_.get());
         }
@@ -385,8 +392,11 @@ void LbfgsSolver::wait_record(int seq, SpecRecord *out) {
   out->seq = r->seq;
 }
 
-// Waits for everything queued, clears the abort flag and forgets the aborted iterations.
-void LbfgsSolver::drain(std::deque<Flight> &q, size_t prof_end) {
+// Waits for everything queued, clears the abort flag and forgets the aborted iterations. status: the
+// status block is copied to the host behind the aborted launches, in the same wait (read_status's copy).
+void LbfgsSolver::drain(std::deque<Flight> &q, size_t prof_end, bool status) {
+  if (status)
+    LBF_HIP(hipMemcpyAsync(hs_.get(), hist_.scal(), SC_N * sizeof(double), hipMemcpyDeviceToHost, ctx_->stream));
   LBF_HIP(hipStreamSynchronize(ctx_->stream));
   LBF_HIP(hipMemsetAsync(abort_.get(), 0, sizeof(int), ctx_->stream));
   obj_->discard_evals((long long)q.size());
@@ -469,10 +479,9 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
     if (r.seq != f.seq) throw Error(2, "speculative line search: record out of sequence");
     if (f.roles.pair) mark_prev_accepted(rec, r.accept_prev);
     if (r.status == SPEC_REJECT) {
-      drain(q, f.prof_end);
-      dir_ready_ = false; // the host finishes this iteration; the next one builds its direction
+      drain(q, f.prof_end, true); // + the status block as the rejected trial left it (one wait)
+      dir_ready_ = false;         // the host finishes this iteration; the next one builds its direction
       restore(f.roles);
-      read_status();
       if (armijo)
         finish_armijo(f.alpha, rec);
       else
