@@ -52,9 +52,6 @@ LbfgsSolver::LbfgsSolver(Objective *obj, const lbf_lbfgs_params &prm, float *d_p
   // (LBF_SPEC_DEPTH, default 3; 0 = host-driven). Host callbacks synchronise anyway.
   depth_ = 3;
   if (const char *e = std::getenv("LBF_SPEC_DEPTH")) depth_ = std::max(0, std::min(16, std::atoi(e)));
-  // Wolfe retries: the trial's backward phase enqueued with its loss-only forward, so the host waits once
-  // per trial instead of twice (LBF_SPEC_GRAD=0: the gradient only after the Armijo test)
-  spec_grad_ = env_int("LBF_SPEC_GRAD", 1) != 0;
   if (!obj_->async()) depth_ = 0;
   // Fused optimizer tail on the speculative path (LBF_FUSED_TAIL=0 disables). It is a latency design
   // (one block per 64 coordinates, a partial row each): past kFusedTailMaxN the classic Gram sweep +
@@ -234,10 +231,6 @@ void LbfgsSolver::finish_wolfe(lbf_record *rec) {
         if (split) { // f(x + alpha p) first; the gradient only once Armijo holds (:136-146)
           obj_->eval_loss(xt_, hist_.scal());
           have_grad = false;
-          if (spec_grad_) { // enqueued before the test: one wait per trial (wasted only if Armijo fails)
-            obj_->eval_grad_after_loss(xt_, gt_, p_.get(), hist_.scal());
-            have_grad = true;
-          }
         } else {
           eval(xt_, gt_, p_.get());
         }

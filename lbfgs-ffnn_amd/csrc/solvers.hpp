@@ -140,7 +140,6 @@ private:
     int seq;
     size_t prof_end;
   };
-  bool spec_grad_ = true; // Wolfe retries: gradient enqueued with the loss-only trial
   void drain(std::deque<Flight> &q, size_t prof_end, bool status = false);
   void wait_record(int seq, SpecRecord *out);
   static constexpr int kSpecRing = 32;

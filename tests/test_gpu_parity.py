@@ -409,9 +409,8 @@ def test_loss_only_equals_fused_loss(ctx, pkg, O, dims, acts, N):
 
 
 def test_armijo_rejections_run_forward_only(ctx, pkg, monkeypatch):
-    """Trials after a rejected first trial are a forward + loss pass whose loss decides Armijo (the reference's
-    line_search evaluates f first and Gradient only then, full_batch_minimizer.hpp:136-146); the backward
-    phase of the same pass is enqueued right behind it and its gradient used only once Armijo holds, so the
+    """Trials after a rejected first trial are forward + loss only until Armijo holds (the reference's
+    line_search evaluates f first and Gradient only then, full_batch_minimizer.hpp:136-146); the
     trajectory is the one every other route takes (test_speculative_line_search_is_exact)."""
     monkeypatch.setenv("LBF_SPEC_DEPTH", "3")
     dims, acts = [784, 32, 10], ["relu", "linear"]
