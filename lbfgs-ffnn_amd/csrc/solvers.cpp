@@ -835,11 +835,7 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     LBF_HIP(hipEventRecord(ev_fork_, s));
     LBF_HIP(hipStreamWaitEvent(tctx_->stream, ev_fork_, 0));
   }
-  // how many steps ahead the twin's anchor gradients are posted (free-running buffers: any depth; the
-  // double-buffered fallback: one)
-  static const int ahead_env = env_int("LBF_TWIN_AHEAD", 1);
-  const int ahead = twin_free ? std::max(1, std::min(ahead_env, m_inner)) : 1;
-  for (int t = 0; t < ahead; ++t) anchor_ahead(t);
+  anchor_ahead(0);
   RedAllArgs gred; // the main evaluation's split-K slabs, finished by the direction sweep
   for (int t = 0; t < m_inner; ++t) {
     const Slice &sl = mb[t];
@@ -847,7 +843,7 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     const float *gb = g2(t);
     {
       auto h0 = tick();
-      if (t + ahead < m_inner) anchor_ahead(t + ahead);
+      if (t + 1 < m_inner) anchor_ahead(t + 1);
       tock(0, h0);
       h0 = tick();
       if (dp)
