@@ -190,6 +190,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float *A, int H, const 
 template <int NJ, int OP>
 __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
   if (a.abort && *a.abort) return;
+  KT(40);
   // [4][(H + 1) * Out] the waves' partials | [(H + 1) * Out] the output layer's W and bias
   extern __shared__ __attribute__((aligned(16))) float red[];
   __shared__ double ssew[4];
@@ -237,12 +238,14 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
     }
   }
   asm volatile("" ::: "memory");
+  KT(41);
 #pragma unroll
   for (int u = 0; u < WST; ++u) {
     const int e = t + 256 * u;
     if (e < per) wl[e] = wst[u];
   }
   lds_barrier();
+  KT(42);
   float w2[NJ][OP], b2[OP], dbacc[OP];
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
@@ -294,6 +297,7 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
             if (k0 + u < a.splits) sum[j] += v[j][u];
       }
     }
+    KT(43);
     // ---- activations (fwd_reduce_act's arithmetic) ----
     float av[NJ];
     with_act(a.act_prev, [&](auto AC) __attribute__((always_inline)) {
@@ -320,6 +324,7 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
         }
       }
     });
+    KT(44);
     // ---- delta = (dZ W^T) .* act_prev'(a), [dW ; db] += [a | 1]^T dZ ----
     with_act(a.act_prev, [&](auto AC) __attribute__((always_inline)) {
       constexpr int A = decltype(AC)::value;
@@ -349,6 +354,7 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
 #pragma unroll
         for (int o = 0; o < OP; ++o)
           if (o < Out) mine[(lane + 64 * j) * Out + o] = 0.0f;
+  KT(45);
   // ---- the block's slab: the four waves' partials summed in wave order ----
   if (lane == 0) {
 #pragma unroll
@@ -357,9 +363,11 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
     ssew[wave] = sse; // every lane holds the same sum
   }
   lds_barrier();
+  KT(46);
   float *slab = a.slab + (long long)blockIdx.x * per;
   for (int e = t; e < per; e += 256) slab[e] = ((red[e] + red[per + e]) + red[2 * per + e]) + red[3 * per + e];
   if (t == 0) a.sse_part[blockIdx.x] = ((ssew[0] + ssew[1]) + ssew[2]) + ssew[3];
+  KT(47);
 }
 
 } // namespace
