@@ -336,14 +336,27 @@ __global__ __launch_bounds__(256) void rowhead_kernel(const RowHeadArgs a) {
         if (cv[j]) a.delta[b * H + lane + 64 * j] = dd * dact_c<A>(av[j]);
       }
     });
+    // the row's [a | 1]^T dZ into the wave's LDS partial: the first row stores (a wave-uniform branch, so no
+    // LDS read is speculated and waited for per element, as the select form compiled to), later rows add
+    if (r == 0) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      if (cv[j]) {
-        float *row = mine + (lane + 64 * j) * Out;
+      for (int j = 0; j < NJ; ++j)
+        if (cv[j]) {
+          float *row = mine + (lane + 64 * j) * Out;
 #pragma unroll
-        for (int o = 0; o < OP; ++o)
-          if (o < Out) row[o] = r == 0 ? av[j] * dz[o] : row[o] + av[j] * dz[o];
-      }
+          for (int o = 0; o < OP; ++o)
+            if (o < Out) row[o] = av[j] * dz[o];
+        }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        if (cv[j]) {
+          float *row = mine + (lane + 64 * j) * Out;
+#pragma unroll
+          for (int o = 0; o < OP; ++o)
+            if (o < Out) row[o] = row[o] + av[j] * dz[o];
+        }
+    }
 #pragma unroll
     for (int o = 0; o < OP; ++o) dbacc[o] += dz[o];
   }
