@@ -265,6 +265,10 @@ int lbf_slbfgs_begin(lbf_mlp *net, const lbf_slbfgs_params *prm, float *d_params
                      const float *d_Y, long long N, lbf_slbfgs **out);
 int lbf_slbfgs_iterate(lbf_slbfgs *s, int epochs, lbf_record *rec, lbf_solve_info *info);
 int lbf_slbfgs_end(lbf_slbfgs *s);
+/* Diagnostics (pair_trace on): the first traced curvature-pair candidate's iterate w_t after inner step t,
+ * the iterate average u, s = u - u_prev and the y stored for it (s_lbfgs.hpp:236-256), n floats each into
+ * device buffers (any may be NULL). LBF_ERR_INVALID until a candidate has been traced. */
+int lbf_slbfgs_pair0(lbf_slbfgs *s, float *d_wt, float *d_u, float *d_s, float *d_y);
 
 /* ---- profiling: HIP-event timing of every kernel class on the context stream (benchmark use).
  * Section id = kind*16 + layer; kinds: 0 fwd GEMM, 1 dW GEMM, 2 dX GEMM, 3 loss, 4 split-K reduce,

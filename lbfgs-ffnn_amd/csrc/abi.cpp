@@ -581,6 +581,13 @@ int lbf_slbfgs_iterate(lbf_slbfgs *s, int epochs, lbf_record *rec, lbf_solve_inf
   });
 }
 
+int lbf_slbfgs_pair0(lbf_slbfgs *s, float *d_wt, float *d_u, float *d_s, float *d_y) {
+  return guard([&] {
+    LBF_REQUIRE(s, "null argument");
+    LBF_REQUIRE(s->s->pair0(d_wt, d_u, d_s, d_y), "no curvature-pair candidate traced (pair_trace off, or none yet)");
+  });
+}
+
 int lbf_slbfgs_end(lbf_slbfgs *s) {
   return guard([&] { delete s; });
 }

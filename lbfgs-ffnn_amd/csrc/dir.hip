@@ -27,8 +27,10 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // C columns per lane (64*C per block) as Q = C/4 quads, lane l owning columns 256q + 4l .. +3 of quad q;
-// VPW history vectors per wave (v = wave + 4j).
-template <int C, int VPW>
+// VPW history vectors per wave (v = wave + 4j). GRED: a.gred_on (the deferred split-K reduction's 16 KB
+// of fp64 stripes in LDS are only declared where they are used, so the pair and sliced-DP sweeps keep the
+// ~6 KB footprint).
+template <int C, int VPW, bool GRED>
 __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
   constexpr int TC = 64 * C, Q = C / 4;
   static_assert(C % 4 == 0, "dir_sweep: whole quads per lane");
@@ -80,7 +82,7 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
   // whose offsets, counts and strides are multiples of 4 floats (16-B aligned slabs), so a lane's quad lies
   // in one segment and is one 16-B load per split. The segment is found by a loop over the (kernel-argument)
   // table with a wave-uniform index: no lane waits on a load of the table.
-  __shared__ double gpart[4][TC];
+  __shared__ double gpart[GRED ? 4 : 1][GRED ? TC : 1];
   auto seg_of = [&](long long e, const float *&base, long long &col, long long &strd, int &nsp) {
     const RedAllArgs &R = a.gred;
     base = R.G;
@@ -98,7 +100,7 @@ __global__ __launch_bounds__(256) void dir_sweep_kernel(const DirArgs a) {
       }
     }
   };
-  if (a.gred_on) { // (History::update: has_g, no pair)
+  if (GRED) { // a.gred_on (History::update: has_g, no pair)
     const RedAllArgs &R = a.gred;
     int kmax = 0;
     for (int si = 0; si < R.nseg; ++si) kmax = max(kmax, R.seg[si].splits);
@@ -486,13 +488,13 @@ __global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const
   }
 }
 
-template <int C>
+template <int C, bool GRED>
 void launch_sweep(hipStream_t s, const DirArgs &a, int vpw) {
   switch (vpw) {
-  case 2: hipLaunchKernelGGL((dir_sweep_kernel<C, 2>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
-  case 4: hipLaunchKernelGGL((dir_sweep_kernel<C, 4>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
-  case 6: hipLaunchKernelGGL((dir_sweep_kernel<C, 6>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
-  case 8: hipLaunchKernelGGL((dir_sweep_kernel<C, 8>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 2: hipLaunchKernelGGL((dir_sweep_kernel<C, 2, GRED>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 4: hipLaunchKernelGGL((dir_sweep_kernel<C, 4, GRED>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 6: hipLaunchKernelGGL((dir_sweep_kernel<C, 6, GRED>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 8: hipLaunchKernelGGL((dir_sweep_kernel<C, 8, GRED>), dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
   default: throw Error(2, "dir_sweep: history size not supported");
   }
 }
@@ -520,7 +522,8 @@ void dir_sweep(hipStream_t s, const DirArgs &a) {
   LBF_REQUIRE(dir_supported(a.g.h.m, a.g.h.n), "dir_sweep: history size / vector length");
   LBF_REQUIRE(a.want_dir == 0 || a.want_dir == 1, "dir_sweep: want_dir 0 / 1");
   LBF_REQUIRE(a.nb == int(cdiv(a.g.h.n, dir_cols_per_block(a.g.h.m, a.g.h.n))), "dir_sweep: block count");
-  launch_sweep<8>(s, a, dir_vpw(a.g.h.m));
+  if (a.gred_on) launch_sweep<8, true>(s, a, dir_vpw(a.g.h.m));
+  else launch_sweep<8, false>(s, a, dir_vpw(a.g.h.m));
   LBF_KERNEL_CHECK();
 }
 

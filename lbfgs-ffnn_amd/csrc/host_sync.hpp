@@ -38,11 +38,16 @@ public:
       cv_.notify_all();
       return;
     }
-    // a system_clock deadline: libstdc++ waits on it with pthread_cond_timedwait, which ThreadSanitizer
-    // intercepts (wait_for's steady clock maps to pthread_cond_clockwait, which gcc 11's TSan does not, and
-    // then reports a bogus double lock); a clock jump only moves the timeout
-    const auto deadline = std::chrono::system_clock::now() + timeout_;
-    const bool ok = cv_.wait_until(lk, deadline, [&] { return gen_ != g || broken_; });
+    // the steady clock (a wall-clock jump cannot stretch or cut the rank-failure timeout); only the
+    // ThreadSanitizer build of the host harness waits on a system_clock deadline: libstdc++ maps that to
+    // pthread_cond_timedwait, which gcc 11's TSan intercepts, while the steady clock's
+    // pthread_cond_clockwait is not intercepted there and reports a bogus double lock
+#if defined(__SANITIZE_THREAD__)
+    const bool ok = cv_.wait_until(lk, std::chrono::system_clock::now() + timeout_,
+                                   [&] { return gen_ != g || broken_; });
+#else
+    const bool ok = cv_.wait_for(lk, timeout_, [&] { return gen_ != g || broken_; });
+#endif
     if (gen_ != g) return;
     broken_ = true;
     lk.unlock();
@@ -74,8 +79,9 @@ private:
 };
 
 // One worker thread running posted tasks in order. `init` runs first on the worker (e.g. hipSetDevice);
-// if it fails, or a task throws, every later task is skipped (its ticket still completes) and the first
-// error is rethrown by the next wait(). The destructor runs what is queued, then joins.
+// if it fails, or a task throws, the FIFO is failed for good: every later task is skipped (its ticket
+// still completes) and every later wait() rethrows that first error. The destructor runs (or skips) what is
+// queued, then joins.
 class TaskFifo {
 public:
   explicit TaskFifo(std::function<void()> init = nullptr) {
@@ -133,7 +139,8 @@ public:
     cv_.notify_one();
     return ticket;
   }
-  // Returns once task `ticket` has run (or been skipped); rethrows the first error once. ticket <= 0: no-op.
+  // Returns once task `ticket` has run (or been skipped); rethrows the first error if the FIFO has failed
+  // (sticky: the error is not consumed). ticket <= 0: no-op.
   void wait(long long ticket) {
     if (ticket <= 0) return;
     for (int spin = 0; done_.load(std::memory_order_acquire) < ticket; ++spin)
@@ -142,7 +149,6 @@ public:
     {
       std::lock_guard<std::mutex> lk(mu_);
       e = err_;
-      err_ = nullptr;
     }
     if (e) std::rethrow_exception(e);
   }

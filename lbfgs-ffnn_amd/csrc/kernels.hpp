@@ -248,6 +248,8 @@ void lincomb(hipStream_t s, long long n, const float *a, double c, const float *
 void add_l2_rows(hipStream_t s, long long n, int rows, long long ld, float *G, const float *w, double lambda);
 void gather_rows(hipStream_t s, const float *src, long long ld, const int *idx, long long count, int cols,
                  float *dst);
+// order-independent fingerprints of x into out[4 slot .. 4 slot + 3] (exact 16-bit halves as floats)
+void fingerprint(hipStream_t s, long long n, const float *x, int slot, float *out);
 void diff_scale(hipStream_t s, long long n, const float *a, const float *b, float scale, float *out);
 void zero_fill(hipStream_t s, long long n, float *x, const int *abort = nullptr);
 // dst = sum_i src[i] over the ranks of an in-process group, in rank order (comm.cpp LocalComm)

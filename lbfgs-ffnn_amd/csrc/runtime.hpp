@@ -131,7 +131,9 @@ public:
   // loss_grad without the last launch (a single rank's gradient only: scal == nullptr): the split-K slabs
   // are left for the consumer, which finishes each gradient value with reduce_all's arithmetic (the S-LBFGS
   // direction sweep, dir.hip). *red describes the slabs; red->nseg == 0 when a segment needs the multi-part
-  // reduction (then G is complete as with loss_grad).
+  // reduction (then G is complete as with loss_grad). When red->nseg > 0, G is left INCOMPLETE: the split
+  // segments of G keep whatever they held (the consumer forms those values in registers and does not store
+  // them back; the S-LBFGS sweep writes only v = g - gb + mu). No reader of G exists on that route.
   void loss_grad_deferred(const float *P, float *G, const float *X, const float *Y, const int *idx, long long B,
                           double inv_scale, double lambda, RedAllArgs *red);
   // The same evaluation in two steps (a line-search trial needs f first and the gradient only once

@@ -950,8 +950,10 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
   const int done0 = iters_;
   while (iters_ < target && !converged_) {
     if (!mu_valid_) {
+      if (repl_ && nr > 1) replica_fingerprints(); // the caller's parameters must agree too
       eval_full(w_.get(), mu_.get());
       read();
+      if (repl_ && nr > 1) replica_check();
     }
     if (std::sqrt(hs_[SC_TGG]) < prm_.tol) { // s_lbfgs.hpp:208
       converged_ = true;
@@ -1003,9 +1005,11 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
     // anchor reset (s_lbfgs.hpp:265-270)
     const float *anchor = pick >= 0 ? wh_.get() + wh_slot(pick) * ld : wt_.get();
     LBF_HIP(hipMemcpyAsync(w_.get(), anchor, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
+    if (repl_ && nr > 1) replica_fingerprints(); // compared after read(): no extra host wait
     // recorder (s_lbfgs.hpp:274-284): full loss and gradient at the new anchor == next epoch's mu
     eval_full(w_.get(), mu_.get());
     read();
+    if (repl_ && nr > 1) replica_check();
     mu_valid_ = true;
     last_loss_ = hs_[SC_LOSS];
     last_gnorm_ = std::sqrt(hs_[SC_TGG]);
@@ -1030,6 +1034,27 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
   return iters_ - done0;
 }
 
+void SlbfgsSolver::replica_fingerprints() {
+  hipStream_t s = ctx_->stream;
+  const size_t cnt = 4 * size_t(ctx_->nranks);
+  fp_.ensure(cnt);
+  hfp_.ensure(cnt);
+  LBF_HIP(hipMemsetAsync(fp_.get(), 0, cnt * sizeof(float), s));
+  fingerprint(s, n_, w_.get(), ctx_->rank, fp_.get());
+  ctx_->allreduce(fp_.get(), cnt);
+  LBF_HIP(hipMemcpyAsync(hfp_.get(), fp_.get(), cnt * sizeof(float), hipMemcpyDeviceToHost, s));
+}
+
+void SlbfgsSolver::replica_check() const {
+  const float *f = hfp_.get();
+  for (int r = 1; r < ctx_->nranks; ++r)
+    for (int i = 0; i < 4; ++i)
+      if (f[4 * r + i] != f[i])
+        throw Error(LBF_ERR_STATE, "S-LBFGS replicated data parallelism: rank " + std::to_string(r) +
+                                       "'s anchor differs from rank 0's at the full-batch evaluation of epoch " +
+                                       std::to_string(iters_) + " (the replicated ranks' parameters drifted apart)");
+}
+
 // Diagnostics row of the pair just offered to the ring (lbf_slbfgs_params.pair_trace): synchronous.
 void SlbfgsSolver::trace_pair(int epoch, int t) {
   hipStream_t s = ctx_->stream;
@@ -1043,10 +1068,29 @@ void SlbfgsSolver::trace_pair(int epoch, int t) {
   LBF_HIP(hipMemcpyAsync(&ss, v.SS + d, sizeof(double), hipMemcpyDeviceToHost, s));
   LBF_HIP(hipMemcpyAsync(&yy, v.YY + d, sizeof(double), hipMemcpyDeviceToHost, s));
   LBF_HIP(hipStreamSynchronize(s));
+  if (npairs_ == 0) { // the iterate after step t, u, s = u - u_prev and the y just stored in the ring
+    const size_t nb = size_t(n_) * sizeof(float), ld = size_t(round4(n_));
+    p0_.resize(4 * ld);
+    const float *src[4] = {wt_.get(), u_.get(), s_.get(), v.Y + size_t(wslot) * size_t(v.ld)};
+    for (int i = 0; i < 4; ++i)
+      LBF_HIP(hipMemcpyAsync(p0_.get() + i * ld, src[i], nb, hipMemcpyDeviceToDevice, s));
+    LBF_HIP(hipStreamSynchronize(s));
+    p0_set_ = true;
+  }
   double *row = prm_.pair_trace + size_t(npairs_++) * LBF_PAIR_TRACE_COLS;
   const double vals[LBF_PAIR_TRACE_COLS] = {double(epoch), double(t), hs_[SC_YS], ss, yy, hs_[SC_ACCEPT],
                                             hs_[SC_COUNT], 0.0};
   for (int i = 0; i < LBF_PAIR_TRACE_COLS; ++i) row[i] = vals[i];
+}
+
+bool SlbfgsSolver::pair0(float *wt, float *u, float *s, float *y) const {
+  if (!p0_set_) return false;
+  const size_t nb = size_t(n_) * sizeof(float), ld = size_t(round4(n_));
+  float *dst[4] = {wt, u, s, y};
+  for (int i = 0; i < 4; ++i)
+    if (dst[i]) LBF_HIP(hipMemcpyAsync(dst[i], p0_.get() + i * ld, nb, hipMemcpyDeviceToDevice, ctx_->stream));
+  LBF_HIP(hipStreamSynchronize(ctx_->stream));
+  return true;
 }
 
 void SlbfgsSolver::info(lbf_solve_info *out) const {

@@ -177,6 +177,9 @@ public:
   int run(lbf_record *rec);                 // prm.max_epochs epochs (lbf_slbfgs_solve)
   int iterate(int epochs, lbf_record *rec); // up to `epochs` more (lbf_slbfgs_begin / iterate / end)
   void info(lbf_solve_info *out) const;
+  // copies the first traced curvature-pair candidate's iterate w_t, average u, s and y (n floats each);
+  // false when no candidate was traced yet
+  bool pair0(float *wt, float *u, float *s, float *y) const;
 
 private:
   struct Slice {
@@ -207,6 +210,13 @@ private:
   // evaluates its 1/p slice of every minibatch and Hessian batch, one all-reduce per inner step.
   bool repl_ = false;
   bool dp_inner() const { return ctx_->dp() && !repl_; }
+  // Replicated mode's guard: every epoch, fingerprints of each rank's new anchor w are all-reduced before
+  // the sharded full-batch evaluation, and a mismatch (ranks whose inner chains drifted apart, which would
+  // make that all-reduce sum gradients taken at different points) fails the solve.
+  DevBuf<float> fp_;
+  PinnedBuf<float> hfp_;
+  void replica_fingerprints();
+  void replica_check() const;
   std::chrono::steady_clock::time_point t0_;
   // Two independent batch gradients of one step (the FD pair at u +- eps s) into one [ga | gb] block
   // (gb = gab + ng_): the second on the twin's stream when there is one, joined before the next launch.
@@ -217,6 +227,9 @@ private:
   void reduce_pair(const float *wa, const float *wb, float *gab, double inv_scale);
   void trace_pair(int epoch, int t);
   int npairs_ = 0;
+  // diagnostics (pair_trace on): the first traced candidate's w_t, u, s, y (lbf_slbfgs_pair0)
+  DevBuf<float> p0_;
+  bool p0_set_ = false;
   Mlp *net_;
   Ctx *ctx_;
   lbf_slbfgs_params prm_;

@@ -733,6 +733,40 @@ void sum_ranks(hipStream_t s, const RankSrcs &r, long long count, float *dst) {
   LBF_KERNEL_CHECK();
 }
 
+// Order-independent 32-bit fingerprints (a sum and an xor of mixed element bits) of x[0 .. n), stored in
+// out[4 slot .. 4 slot + 3] as four exact 16-bit halves in floats, so that a sum all-reduce of a zeroed
+// [4 nranks] buffer in which each rank filled its own slot hands every rank every rank's fingerprints.
+// One workgroup: called once per S-LBFGS epoch (the replicated data-parallel check).
+__global__ __launch_bounds__(1024) void fingerprint_kernel(long long n, const float *x, int slot, float *out) {
+  const int t = threadIdx.x;
+  unsigned hs = 0u, hx = 0u;
+  for (long long e = t; e < n; e += 1024) {
+    unsigned h = (__float_as_uint(x[e]) ^ (unsigned(e) * 0x9E3779B9u)) * 0x85EBCA6Bu;
+    h ^= h >> 13;
+    hs += h;
+    hx ^= h * 0xC2B2AE35u;
+  }
+  __shared__ unsigned ss[1024], sx[1024];
+  ss[t] = hs;
+  sx[t] = hx;
+  __syncthreads();
+  for (int k = 512; k > 0; k >>= 1) {
+    if (t < k) {
+      ss[t] += ss[t + k];
+      sx[t] ^= sx[t + k];
+    }
+    __syncthreads();
+  }
+  if (t < 4) {
+    const unsigned v = t < 2 ? ss[0] : sx[0];
+    out[4 * slot + t] = float((t & 1) ? (v >> 16) : (v & 0xffffu));
+  }
+}
+void fingerprint(hipStream_t s, long long n, const float *x, int slot, float *out) {
+  hipLaunchKernelGGL(fingerprint_kernel, dim3(1), dim3(1024), 0, s, n, x, slot, out);
+  LBF_KERNEL_CHECK();
+}
+
 // y = (a - b) * scale in fp32: the pair sweep's y of a finite-difference HVP (gram_kernel forms the
 // same product when it writes the ring slot)
 __global__ __launch_bounds__(256) void diff_scale_kernel(long long n, const float *a, const float *b, float scale,

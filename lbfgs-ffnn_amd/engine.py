@@ -377,9 +377,14 @@ class SlbfgsRun:
     iterate() calls (the breakdown, warmup and timed epochs), bitwise one lbf_slbfgs_solve."""
 
     def __init__(self, net: Mlp, params: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, record_cap: int = 100000,
-                 **kw):
+                 pair_trace: int = 0, **kw):
         self.p = slbfgs_params(**kw)
         self.p.max_epochs = max(int(self.p.max_epochs), 1 << 30)
+        self.trace = None
+        if pair_trace > 0:  # diagnostics: rows as slbfgs_solve's hist["pairs"], and pair0()
+            self.trace = np.full((int(pair_trace), 8), np.nan)
+            self.p.pair_trace = self.trace.ctypes.data_as(C.POINTER(C.c_double))
+            self.p.pair_trace_cap = int(pair_trace)
         self.hist = History(record_cap)
         self.info = SolveInfo()
         self._keep = (net, params, X, Y)
@@ -392,6 +397,16 @@ class SlbfgsRun:
         check(lib().lbf_slbfgs_iterate(self.h, epochs, C.byref(self.hist.rec), C.byref(self.info)),
               "lbf_slbfgs_iterate")
         return self.info
+
+    def pairs(self):
+        return None if self.trace is None else self.trace[~np.isnan(self.trace[:, 0])]
+
+    def pair0(self):
+        """The first traced curvature-pair candidate's (w_t, u, s, y) as device tensors (lbf_slbfgs_pair0)."""
+        n = int(self._keep[1].numel())
+        out = [torch.empty(n, dtype=torch.float32, device=self._keep[1].device) for _ in range(4)]
+        check(lib().lbf_slbfgs_pair0(self.h, *[ptr(t) for t in out]), "lbf_slbfgs_pair0")
+        return out
 
     def close(self):
         if self.h:

@@ -693,9 +693,11 @@ Vec<T> slbfgs(Vec<T> weights, BG &&batch_g, BF &&batch_f, const SlbfgsParams &pr
           auto hb = sample_minibatch_indices(size_t(prm.N), size_t(prm.b_H), rng);
           if (sampled) sampled->push_back(hb);
           Vec<T> y = finite_difference_hvp_batch<T>(batch_g, u, s, hb, 1e-4);
-          if (pair0_us && pair0_us->empty()) { // diagnostics: the first candidate's u and s (fp64 copies)
-            pair0_us->assign(u.begin(), u.end());
+          if (pair0_us && pair0_us->empty()) { // diagnostics: the first candidate's w_t, u, s, y (fp64 copies)
+            pair0_us->assign(wt.begin(), wt.end());
+            pair0_us->insert(pair0_us->end(), u.begin(), u.end());
             pair0_us->insert(pair0_us->end(), s.begin(), s.end());
+            pair0_us->insert(pair0_us->end(), y.begin(), y.end());
           }
           double ys = double(dot(y, s));
           const bool acc = std::abs(ys) > 1e-10;

@@ -76,6 +76,7 @@ def lib():
         L.oracle_synth_mnist.argtypes = [C.c_longlong, C.c_int, C.c_int, C.c_uint, _dp, _dp]
         L.oracle_ring_trace.argtypes = [C.c_int, C.c_int, _ip, _ip]
         L.oracle_num_threads.restype = C.c_int
+        L.oracle_set_threads.argtypes = [C.c_int]
         _lib = L
     return _lib
 
@@ -194,7 +195,8 @@ class Net:
                want_idx=False, pair_trace=0, pair0=None):
         """Returns (params, rec, idx) or, with pair_trace > 0, (params, rec, idx, pairs): one row per curvature
         pair candidate (epoch, t, y.s, s.s, y.y, accepted, live pairs, 0), as the device's pair trace.
-        pair0: an fp64 array of 2 * nparams receiving the first candidate's u and s (diagnostics)."""
+        pair0: an fp64 array of 4 * nparams receiving the first candidate's iterate w_t (after step t), the
+        iterate average u, s = u - u_prev and y (diagnostics; lbf_slbfgs_pair0 on the device)."""
         P = np.array(P, np.float64, copy=True)
         rec = np.zeros((epochs, 6), np.float64)
         it = C.c_int(0)
@@ -261,6 +263,11 @@ def ring_trace(cap: int, npush: int):
 
 def num_threads() -> int:
     return int(lib().oracle_num_threads())
+
+
+def set_threads(n: int) -> None:
+    """OpenMP threads of the oracle's later calls (omp_set_num_threads)."""
+    lib().oracle_set_threads(int(n))
 
 
 # ---- BASELINE config 5 data (test infrastructure; restates lbfgs-ffnn_amd/csrc/synth.hip) ----------

@@ -418,4 +418,13 @@ int oracle_num_threads() {
 #endif
 }
 
+// OpenMP threads of the following oracle calls (bench.py's CPU baseline at the host's physical core count)
+void oracle_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}
+
 } // extern "C"

@@ -5,8 +5,8 @@
 //      rank publishes its buffer pointer and count, meets, reads every other rank's, meets again; a rank
 //      that throws breaks the group and the others fail instead of hanging.
 //   2. TaskFifo (host_sync.hpp) under the S-LBFGS twin's protocol (solvers.cpp epoch_steps): tasks posted in
-//      order, the poster waits by ticket before reading what a task produced, errors surface once at the next
-//      wait, the destructor runs what is queued.
+//      order, the poster waits by ticket before reading what a task produced, an error fails the FIFO for good
+//      (every later task skipped, every later wait rethrows), the destructor runs what is queued.
 //   3. MinibatchSampler (sampler.cpp) against a plain restatement of s_lbfgs.hpp:141-160 (iota(N) per draw).
 #include "host_sync.hpp"
 #include "sampler.hpp"
@@ -118,7 +118,7 @@ static void test_task_fifo() {
     for (int t = 0; t < T; ++t) CHECK(out[size_t(t)] == t);
     CHECK(init_ran.load());
   }
-  // an error surfaces once at the next wait; later tasks are skipped until then, and run again after
+  // an error fails the FIFO for good: later tasks are skipped, every later wait rethrows it
   {
     TaskFifo q;
     std::vector<int> ran(6, 0);
@@ -128,29 +128,37 @@ static void test_task_fifo() {
       throw std::runtime_error("launch failed");
     });
     const long long skipped = q.post([&]() { ran[2] = 1; });
-    bool thrown = false;
+    int thrown = 0;
     try {
       q.wait(skipped);
     } catch (const std::runtime_error &) {
-      thrown = true;
+      ++thrown;
     }
-    CHECK(thrown && bad == 2);
+    CHECK(thrown == 1 && bad == 2);
     const long long after = q.post([&]() { ran[3] = 1; });
-    q.wait(after); // no error left: returns normally
-    CHECK(ran[0] == 1 && ran[1] == 1 && ran[2] == 0 && ran[3] == 1);
+    try {
+      q.wait(after); // still failed: the error is sticky, the task skipped
+    } catch (const std::runtime_error &) {
+      ++thrown;
+    }
+    CHECK(thrown == 2);
+    CHECK(ran[0] == 1 && ran[1] == 1 && ran[2] == 0 && ran[3] == 0);
   }
-  // a failing init (hipSetDevice on the worker) skips every task and is reported by the first wait
+  // a failing init (hipSetDevice on the worker) skips every task, the first wait reports it and so does
+  // every later one (a task must never run on a thread whose device was not set)
   {
     TaskFifo q([]() { throw std::runtime_error("no device"); });
     int ran = 0;
-    const long long t = q.post([&]() { ran = 1; });
-    bool thrown = false;
-    try {
-      q.wait(t);
-    } catch (const std::runtime_error &) {
-      thrown = true;
+    int thrown = 0;
+    for (int k = 0; k < 3; ++k) {
+      const long long t = q.post([&]() { ran = 1; });
+      try {
+        q.wait(t);
+      } catch (const std::runtime_error &) {
+        ++thrown;
+      }
     }
-    CHECK(thrown && ran == 0);
+    CHECK(thrown == 3 && ran == 0);
   }
   // the destructor runs what is still queued, then joins (the solver's teardown)
   {

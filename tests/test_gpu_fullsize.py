@@ -9,8 +9,8 @@ stream seed 123).
 Tolerances: loss relative 1e-5, gradient ||dg||/||g|| 1e-4; trajectories: the first
 10 L-BFGS iterations' losses relative 1e-3 with identical line-search trial counts and pair acceptances
 (src/minimizer/lbfgs.hpp:38-100, full_batch_minimizer.hpp:126-157); S-LBFGS (s_lbfgs.hpp:165-290): one
-epoch's recorded loss within 5 % (chaotic at the rounding level, see the test) and the same number of live
-curvature pairs; the finite-difference
+epoch's recorded loss within 5 % and the same number of live curvature pairs, the first curvature pair
+(after 20 pure SVRG steps) within 1e-4; the finite-difference
 HVP y (s_lbfgs.hpp:88-101): ||dy||/||y|| <= 5e-2 (fp32 cancellation in w +- eps s).
 """
 import numpy as np
@@ -147,48 +147,92 @@ def test_cfg3_loss_grad_full_size(ctx, pkg, O, mnist, N):
     assert rel(host(g), g_ref) <= 1e-4
 
 
-def test_cfg4_slbfgs_one_epoch_full_size(ctx, pkg, O, mnist):
-    """One full S-LBFGS epoch at the cfg-4 network and N = 60000: 234 inner steps of b = 256, a curvature
-    pair every L = 10 steps from the second average on (22 FD-HVPs on b_H = 128), the anchor reset and
-    the recorder's full loss, all on the same host RNG stream as the oracle.
+CFG4_KW = dict(M=10, L=10, b=256, b_H=128, step=0.005)
 
-    Step 0.005: at cfg 4's 0.02 the synthetic problem diverges to NaN within the first epoch in the fp64
-    oracle itself. After 234 SVRG steps with finite-difference curvature pairs (fp32 cancellation in
-    w +- eps s) the epoch's loss is chaotic at the rounding level: the oracle's own fp32
-    instantiation lands 0.4 % (step 0.005) / 1.5 % (step 0.01) from its fp64 run, and a re-rounding of one
-    device GEMM (two k-groups instead of one) moved the device result by 4 %, splitting the dX GEMM's K by
-    5.6 %. The check is therefore the machinery at scale — same number of live pairs, a finite loss within
-    5 % of the fp64 oracle, or within 3x the spread that the oracle's fp32 run or the device's own run from
-    parameters moved by 2 ulp shows, bitwise reproducible — while the step-exact S-LBFGS parity is
-    test_gpu_parity.py::test_slbfgs_matches_oracle and test_gpu_configs.py::test_cfg4_slbfgs_shape."""
+
+@pytest.fixture(scope="module")
+def cfg4_epoch(ctx, pkg, O, mnist):
+    """One full S-LBFGS epoch of cfg 4 at N = 60000 on the device (pair trace and first-pair snapshot on)
+    and in the oracle's fp64 and fp32 instantiations (same host RNG stream, same records)."""
     _, _, X64, Y64, X, Y = mnist
     dims, acts = CFG4
     net = pkg.Mlp(ctx, dims, acts)
-    kw = dict(M=10, L=10, b=256, b_H=128, step=0.005)
     P = net.init_params(123, "cpu")
     P0 = host(P)
-    hist, info = pkg.slbfgs_solve(net, P, X, Y, max_epochs=1, tol=0.0, lam=1e-4, **kw)
-    P2 = net.init_params(123, "cpu")
-    hist2, _ = pkg.slbfgs_solve(net, P2, X, Y, max_epochs=1, tol=0.0, lam=1e-4, **kw)
-    assert np.array_equal(hist["loss"], hist2["loss"]) and torch.equal(P, P2)
+    run = pkg.SlbfgsRun(net, P, X, Y, pair_trace=64, tol=0.0, lam=1e-4, **CFG4_KW)
+    info = run.iterate(1)
+    hist, pairs = run.hist.as_dict(), run.pairs().copy()
+    p0 = [host(t) for t in run.pair0()]
+    run.close()
     onet = O.Net(dims, acts)
-    okw = dict(epochs=1, tol=0.0, M=10, L=10, b=256, bH=128, step=0.005, lam=1e-4)
-    _, rec, _ = onet.slbfgs(P0, X64, Y64, **okw)
-    _, rec32, _ = onet.slbfgs(P0, X64, Y64, fp32=True, **okw)
+    okw = dict(epochs=1, tol=0.0, M=10, L=10, b=256, bH=128, step=0.005, lam=1e-4, pair_trace=64)
+    o64, o32 = np.zeros(4 * P0.size), np.zeros(4 * P0.size)
+    _, rec, _, pairs64 = onet.slbfgs(P0, X64, Y64, pair0=o64, **okw)
+    _, rec32, _, pairs32 = onet.slbfgs(P0, X64, Y64, fp32=True, pair0=o32, **okw)
+    return dict(net=net, P0=P0, P=P, hist=hist, info=info, pairs=pairs, p0=p0, rec=rec, rec32=rec32,
+                pairs64=pairs64, pairs32=pairs32, o64=o64.reshape(4, -1), o32=o32.reshape(4, -1),
+                l0=float(onet.loss(P0, X64, Y64)))
+
+
+def test_cfg4_slbfgs_first_pair_full_size(cfg4_epoch):
+    """The non-chaotic window of the cfg-4 epoch at N = 60000: the first 20 inner steps are pure SVRG (no
+    curvature pair exists until t % L == 0 with two iterate averages, s_lbfgs.hpp:218-261), so the iterate
+    after them, the averages u, s = u_20 - u_10 and the first finite-difference y (s_lbfgs.hpp:88-101,
+    236-256) are a smooth function of the inputs and must agree with the fp64 oracle to fp32 accuracy:
+    ||d||/||ref|| <= 1e-4 for w_t, u and s, |d(y.s)|/|y.s| and |d(s.s)|/|s.s| <= 1e-4 (pair_trace row 0), y
+    within 1e-4 or 3x the oracle's own fp32-vs-fp64 distance (the central difference of two fp32 gradients
+    at u +- 1e-4 s cancels; the reference's algorithm has that error in fp32 by construction)."""
+    r = cfg4_epoch
+    dev, o64, o32 = r["p0"], r["o64"], r["o32"]
+    names = ["w_t", "u", "s", "y"]
+    errs = {k: rel(dev[i], o64[i]) for i, k in enumerate(names)}
+    errs32 = {k: rel(o32[i], o64[i]) for i, k in enumerate(names)}
+    step = rel(dev[0] - r["P0"], o64[0] - r["P0"])  # the 20 steps' displacement alone
+    row, row64, row32 = r["pairs"][0], r["pairs64"][0], r["pairs32"][0]
+    print("first pair (t = %d): " % int(row[1]) + ", ".join(f"{k} {errs[k]:.2e} (oracle fp32 {errs32[k]:.2e})"
+                                                         for k in names) + f", w_t - w_0 {step:.2e}")
+    print(f"first pair y.s device {row[2]:.9e} fp64 {row64[2]:.9e} fp32 {row32[2]:.9e}; "
+          f"s.s device {row[3]:.9e} fp64 {row64[3]:.9e}; y.y device {row[4]:.9e} fp64 {row64[4]:.9e}")
+    assert int(row[0]) == int(row64[0]) == 0 and int(row[1]) == int(row64[1]) == 20
+    for k in ("w_t", "u", "s"):
+        assert errs[k] <= 1e-4, (k, errs[k])
+    assert abs(row[2] - row64[2]) <= 1e-4 * abs(row64[2]), (row[2], row64[2])
+    assert abs(row[3] - row64[3]) <= 1e-4 * abs(row64[3]), (row[3], row64[3])
+    assert errs["y"] <= max(1e-4, 3.0 * errs32["y"]), (errs["y"], errs32["y"])
+
+
+def test_cfg4_slbfgs_one_epoch_full_size(ctx, pkg, O, mnist, cfg4_epoch):
+    """One full S-LBFGS epoch at the cfg-4 network and N = 60000: 234 inner steps of b = 256, a curvature
+    pair every L = 10 steps from the second average on (22 FD-HVPs on b_H = 128), the anchor reset and
+    the recorder's full loss, all on the same host RNG stream as the oracle: the recorded loss within 5 % of
+    the fp64 oracle, the same number of live pairs, bitwise reproducible (also with the pair trace off).
+
+    Step 0.005: at cfg 4's 0.02 the synthetic problem diverges to NaN within the first epoch in the fp64
+    oracle itself. Past the first pairs the epoch is sensitive at the rounding level (finite-difference
+    pairs across ReLU kinks), so the per-candidate record (y.s, s.s, y.y of all 22 pairs for
+    the device and both oracle instantiations) is printed beside the bound; the non-chaotic window is
+    test_cfg4_slbfgs_first_pair_full_size, the step-exact parity test_gpu_parity.py::test_slbfgs_matches_oracle."""
+    _, _, X64, Y64, X, Y = mnist
+    r = cfg4_epoch
+    hist, rec, rec32 = r["hist"], r["rec"], r["rec32"]
+    P2 = r["net"].init_params(123, "cpu")
+    hist2, _ = pkg.slbfgs_solve(r["net"], P2, X, Y, max_epochs=1, tol=0.0, lam=1e-4, **CFG4_KW)
+    assert np.array_equal(hist["loss"], hist2["loss"]) and torch.equal(r["P"], P2)
     assert len(hist["loss"]) == 1 and len(rec) == 1 and len(rec32) == 1
-    spread = abs(rec32[0, 0] - rec[0, 0]) / abs(rec[0, 0])
-    # the device's own sensitivity: the same epoch from parameters moved by ~2 ulp (relative 2^-22)
-    P3 = net.init_params(123, "cpu")
-    P3.mul_(1.0 + 2.0 ** -22)
-    hist3, _ = pkg.slbfgs_solve(net, P3, X, Y, max_epochs=1, tol=0.0, lam=1e-4, **kw)
-    dev_spread = abs(hist3["loss"][0] - hist["loss"][0]) / abs(rec[0, 0])
-    r = abs(hist["loss"][0] - rec[0, 0]) / abs(rec[0, 0])
-    print(f"cfg4 epoch loss: device {hist['loss'][0]:.6f} oracle fp64 {rec[0, 0]:.6f} fp32 {rec32[0, 0]:.6f} "
-          f"device from 2-ulp-moved parameters {hist3['loss'][0]:.6f}")
-    assert np.isfinite(hist["loss"][0]) and hist["loss"][0] < 0.5 * float(onet.loss(P0, X64, Y64))
-    assert r <= max(5e-2, 3.0 * spread, 3.0 * dev_spread), (r, spread, dev_spread)
+    dv, o, o32 = r["pairs"], r["pairs64"], r["pairs32"]
+    print("cand  t    y.s device / fp64 / fp32                    s.s device / fp64          live d/64/32")
+    for i in range(min(len(dv), len(o), len(o32))):
+        print(f"{i:3d} {int(dv[i, 1]):4d}  {dv[i, 2]: .6e} {o[i, 2]: .6e} {o32[i, 2]: .6e}  "
+              f"{dv[i, 3]:.6e} {o[i, 3]:.6e}  {int(dv[i, 6])}/{int(o[i, 6])}/{int(o32[i, 6])}")
+    dev_r = abs(hist["loss"][0] - rec[0, 0]) / abs(rec[0, 0])
+    r32 = abs(rec32[0, 0] - rec[0, 0]) / abs(rec[0, 0])
+    print(f"cfg4 epoch loss: device {hist['loss'][0]:.6f} oracle fp64 {rec[0, 0]:.6f} fp32 {rec32[0, 0]:.6f}: "
+          f"device {dev_r:.4f}, oracle fp32 {r32:.4f} from the fp64 oracle")
+    assert np.isfinite(hist["loss"][0]) and hist["loss"][0] < 0.5 * r["l0"]
+    assert dev_r <= 5e-2, dev_r
     assert int(hist["accepted"][0]) == int(rec[0, 3]) == 10   # M = 10 live pairs after 22 candidates
-    assert info.n_evals >= 2 * 234
+    assert len(dv) == len(o) == 22
+    assert r["info"].n_evals >= 2 * 234
 
 
 def test_fd_hvp_matches_oracle_cfg4(ctx, pkg, O, mnist):
