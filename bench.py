@@ -67,7 +67,7 @@ def parse(argv=None):
                          "order) instead of before them")
     ap.add_argument("--comm1", action="store_true",
                     help="at N=1, route evaluations through a 1-rank RCCL communicator (the DP code path)")
-    ap.add_argument("--cpu-iters", type=int, default=64)  # ~20 s of the oracle at N = 60000 on 16 threads
+    ap.add_argument("--cpu-iters", type=int, default=64)  # at most; a probe bounds each run to CPU_BUDGET_S
     ap.add_argument("--cpu-samples", type=int, default=0,
                     help="rows of the CPU-baseline sample (0: all rows up to 60000, else 2000; scaled to N)")
     ap.add_argument("--data", choices=["mnist", "regression"], default="mnist",
@@ -123,46 +123,105 @@ def route_env():
     return {k: v for k, v in sorted(os.environ.items()) if k.startswith("LBF_")}
 
 
-THREADS_NOTE = ("OpenMP threads = OMP_NUM_THREADS as the GPU box sets it (16): one GPU's 1/8 share of the "
-                "host's physical cores, the CPU share a one-GPU job gets on an 8-GPU node; the reference's own "
-                "CPU numbers (BASELINE.md) do not state their thread count")
+def cgroup_cpus():
+    """CPUs the job's cgroup may use (cpu.max quota / period), or None when unlimited / unknown."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else round(q / p, 2)
+    except (OSError, ValueError):
+        return None
+
+
+THREADS_NOTE = ("value: OpenMP threads = the CPUs this job may use: the host's physical cores, capped by the "
+                "job's cgroup CPU quota (16 of the 128 physical cores on the GPU box; OMP_NUM_THREADS is 16 there "
+                "too); at_physical_cores: the same oracle at one thread per physical core (BASELINE.md §2), which "
+                "on the GPU box oversubscribes the 16-CPU quota and runs slower; the reference's own CPU numbers "
+                "(BASELINE.md) do not state their thread count")
+CPU_BUDGET_S = 30.0   # bound on the primary CPU-baseline run (the sample shrinks when a probe predicts more)
+CPU_BUDGET_PHYS_S = 15.0   # bound on the physical-core run
+
+
+def baseline_threads(O):
+    """(usable threads, physical-core threads, host info) for the CPU baseline's two runs."""
+    hc = host_cpu()
+    hc["cgroup_cpus"] = cgroup_cpus()
+    phys = int(hc["physical_cores"] or os.cpu_count() or 1)
+    usable = min(phys, int(hc["usable_cpus"] or phys))
+    if hc["cgroup_cpus"]:
+        usable = min(usable, max(1, int(hc["cgroup_cpus"])))
+    return usable, phys, hc
+
+
+def timed_threads(O, threads, fn):
+    O.set_threads(threads)
+    t0 = time.perf_counter()
+    r = fn()
+    return r, time.perf_counter() - t0
+
+
+def bounded_iters(O, threads, fn2, budget, cap):
+    """Iterations of an L-BFGS sample that a 2-iteration probe at `threads` predicts to fit `budget` s."""
+    _, probe_s = timed_threads(O, threads, fn2)
+    return int(max(4, min(cap, budget / max(probe_s / 2, 1e-6))))
 
 
 def cpu_baseline(dims, acts, N, m, iters, data, rows):
     """The oracle (fp64 C++/OpenMP restatement of the reference CPU path, literal call pattern incl. its
-    redundant f/grad re-evaluations) timed on this host; bounded sample of the same workload: `rows` of
-    the N samples (the full-batch cost is linear in N, so the rate is scaled by rows / N)."""
+    redundant f/grad re-evaluations) timed on this host at the CPUs the job may use (`value`) and at one
+    thread per physical core (`at_physical_cores`); bounded sample of the same workload: `rows` of the N
+    samples (the full-batch cost is linear in N, so the rate is scaled by rows / N), for as many iterations
+    (at most `iters`) as a 2-iteration probe predicts to fit the run's time budget."""
     O = __graft_entry__.load_oracle()
     O.lib()
     X, Y = O.synth_mnist(rows, dims[0], dims[-1]) if data == "mnist" else O.synth_regression(rows, dims[0])
     net = O.Net(dims, acts)
     P = net.init_cpu(123)
-    _, rec, info = net.lbfgs_wolfe(P, X, Y, m=m, max_iters=iters)
-    ms = info["ms"]
+    usable, phys, hc = baseline_threads(O)
     scale = rows / N
-    return dict(value=round(iters / (ms / 1e3) * scale, 6), unit="iters/s", cores=O.num_threads(), kind="port",
-                host=host_cpu(), threads_note=THREADS_NOTE,
-                sample=f"{iters} L-BFGS iterations (Wolfe, m={m}) of the {'-'.join(map(str, dims))} MLP on "
-                       f"{rows} of the N={N} rows{f' (rate scaled by {rows}/{N})' if rows != N else ''}, fp64 "
-                       f"oracle (oracle/oracle.hpp) with the reference's f/grad call pattern "
-                       f"({info['n_fwd']} forward, {info['n_bwd']} backward passes), "
-                       f"{O.num_threads()} OpenMP threads, {ms / 1e3:.1f} s")
+    probe = lambda: net.lbfgs_wolfe(P, X, Y, m=m, max_iters=2)  # noqa: E731
+
+    def one(threads, n_it):
+        (_, rec, info), _ = timed_threads(O, threads, lambda: net.lbfgs_wolfe(P, X, Y, m=m, max_iters=n_it))
+        ms = info["ms"]
+        return dict(value=round(n_it / (ms / 1e3) * scale, 6), cores=threads, iters=n_it,
+                    seconds=round(ms / 1e3, 2), passes=f"{info['n_fwd']} forward, {info['n_bwd']} backward")
+
+    main_run = one(usable, bounded_iters(O, usable, probe, CPU_BUDGET_S, iters))
+    phys_run = one(phys, bounded_iters(O, phys, probe, CPU_BUDGET_PHYS_S, iters)) if phys != usable else None
+    O.set_threads(usable)
+    out = dict(value=main_run["value"], unit="iters/s", cores=usable, kind="port", host=hc, threads_note=THREADS_NOTE,
+               sample=f"{main_run['iters']} L-BFGS iterations (Wolfe, m={m}) of the {'-'.join(map(str, dims))} MLP "
+                      f"on {rows} of the N={N} rows{f' (rate scaled by {rows}/{N})' if rows != N else ''}, fp64 "
+                      f"oracle (oracle/oracle.hpp) with the reference's f/grad call pattern ({main_run['passes']} "
+                      f"passes), {usable} OpenMP threads, {main_run['seconds']} s")
+    if phys_run:
+        out["at_physical_cores"] = {k: phys_run[k] for k in ("value", "cores", "iters", "seconds")}
+    return out
 
 
 def slbfgs_cpu_baseline(dims, acts, N, step, epochs=1):
-    """The oracle's S-LBFGS (fp64 restatement of s_lbfgs.hpp:165-290, OpenMP) for one epoch at full N."""
+    """The oracle's S-LBFGS (fp64 restatement of s_lbfgs.hpp:165-290, OpenMP) for one epoch at full N, at the
+    CPUs the job may use (an oversubscribed physical-core run of a whole epoch would take ~1 min on the GPU
+    box: the cfg-2 line carries that comparison)."""
     O = __graft_entry__.load_oracle()
     X, Y = O.synth_mnist(N, dims[0], dims[-1])
     net = O.Net(dims, acts)
     P = net.init_cpu(123)
-    t0 = time.perf_counter()
-    net.slbfgs(P, X, Y, epochs=epochs, tol=0.0, M=10, L=10, b=256, bH=128, step=step, lam=1e-4)
-    dt = time.perf_counter() - t0
-    return dict(value=round(epochs / dt, 6), unit="epochs/s", cores=O.num_threads(), kind="port", host=host_cpu(),
-                threads_note=THREADS_NOTE,
-                sample=f"{epochs} S-LBFGS epoch(s) of the {'-'.join(map(str, dims))} MLP on all N={N} rows (b=256, "
-                       f"b_H=128, L=M=10), fp64 oracle (oracle/oracle.hpp), {O.num_threads()} OpenMP threads, "
-                       f"{dt:.1f} s")
+    usable, _, hc = baseline_threads(O)
+    kw = dict(epochs=epochs, tol=0.0, M=10, L=10, b=256, bH=128, step=step, lam=1e-4)
+    _, dt = timed_threads(O, usable, lambda: net.slbfgs(P, X, Y, **kw))
+    out = dict(value=round(epochs / dt, 6), unit="epochs/s", cores=usable, kind="port", host=hc,
+               threads_note=THREADS_NOTE,
+               sample=f"{epochs} S-LBFGS epoch(s) of the {'-'.join(map(str, dims))} MLP on all N={N} rows (b=256, "
+                      f"b_H=128, L=M=10), fp64 oracle (oracle/oracle.hpp), {usable} OpenMP threads, {dt:.1f} s")
+    O.set_threads(usable)
+    return out
 
 
 class Device:

@@ -7,6 +7,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r05a
 mkdir -p $O
 cd $R
+timeout -k 10 90 ./profiles/micro/delivery > $O/delivery.txt 2>&1; echo "delivery rc $?"; cat $O/delivery.txt
 timeout -k 10 300 python -u profiles/r05/cpu_threads.py 16 32 64 128 > $O/cpu_threads.txt 2>&1; echo "cpu probe rc $?"; cat $O/cpu_threads.txt
 timeout -k 10 600 python -u -m pytest -v -s --timeout 400 --timeout-method thread tests/test_gpu_fullsize.py -k "cfg4" > $O/cfg4_fullsize.log 2>&1; echo "cfg4 fullsize rc $?"
 grep -E "first pair|cfg4 epoch|PASS|FAIL|Error|assert" $O/cfg4_fullsize.log | head -40

@@ -10,7 +10,7 @@ Tolerances: loss relative 1e-5, gradient ||dg||/||g|| 1e-4; t
 10 L-BFGS iterations' losses relative 1e-3 with identical line-search trial counts and pair acceptances
 (src/minimizer/lbfgs.hpp:38-100, full_batch_minimizer.hpp:126-157); S-LBFGS (s_lbfgs.hpp:165-290): one
 epoch's recorded loss within 5 % and the same number of live curvature pairs, the first curvature pair
-(after 20 pure SVRG steps) within 1e-4; the finite-difference
+(after 20 pure SVRG steps: iterate and ||s|| within 1e-4, y.s within 5e-3); the finite-difference
 HVP y (s_lbfgs.hpp:88-101): ||dy||/||y|| <= 5e-2 (fp32 cancellation in w +- eps s).
 """
 import numpy as np
@@ -167,21 +167,28 @@ def cfg4_epoch(ctx, pkg, O, mnist):
     onet = O.Net(dims, acts)
     okw = dict(epochs=1, tol=0.0, M=10, L=10, b=256, bH=128, step=0.005, lam=1e-4, pair_trace=64)
     o64, o32 = np.zeros(4 * P0.size), np.zeros(4 * P0.size)
-    _, rec, _, pairs64 = onet.slbfgs(P0, X64, Y64, pair0=o64, **okw)
+    _, rec, idx64, pairs64 = onet.slbfgs(P0, X64, Y64, pair0=o64, want_idx=True, **okw)
     _, rec32, _, pairs32 = onet.slbfgs(P0, X64, Y64, fp32=True, pair0=o32, **okw)
     return dict(net=net, P0=P0, P=P, hist=hist, info=info, pairs=pairs, p0=p0, rec=rec, rec32=rec32,
                 pairs64=pairs64, pairs32=pairs32, o64=o64.reshape(4, -1), o32=o32.reshape(4, -1),
-                l0=float(onet.loss(P0, X64, Y64)))
+                l0=float(onet.loss(P0, X64, Y64)), onet=onet, idx64=idx64)
 
 
-def test_cfg4_slbfgs_first_pair_full_size(cfg4_epoch):
-    """The non-chaotic window of the cfg-4 epoch at N = 60000: the first 20 inner steps are pure SVRG (no
-    curvature pair exists until t % L == 0 with two iterate averages, s_lbfgs.hpp:218-261), so the iterate
-    after them, the averages u, s = u_20 - u_10 and the first finite-difference y (s_lbfgs.hpp:88-101,
-    236-256) are a smooth function of the inputs and must agree with the fp64 oracle to fp32 accuracy:
-    ||d||/||ref|| <= 1e-4 for w_t, u and s, |d(y.s)|/|y.s| and |d(s.s)|/|s.s| <= 1e-4 (pair_trace row 0), y
-    within 1e-4 or 3x the oracle's own fp32-vs-fp64 distance (the central difference of two fp32 gradients
-    at u +- 1e-4 s cancels; the reference's algorithm has that error in fp32 by construction)."""
+def test_cfg4_slbfgs_first_pair_full_size(mnist, cfg4_epoch):
+    """The first curvature pair of the cfg-4 epoch at N = 60000. The first 20 inner steps are pure SVRG (no
+    pair exists until t % L == 0 with two iterate averages, s_lbfgs.hpp:218-261), then u = mean(w_10..w_20),
+    s = u - u_prev and the finite-difference y on the first Hessian batch (s_lbfgs.hpp:88-101, 236-256).
+
+    Against the fp64 oracle on the same RNG stream: the iterate w_t after the 20 steps and u within
+    ||d||/||ref|| <= 1e-4; ||s|| (pair_trace row 0's s.s) within 1e-4; s itself, a difference of two averages
+    10 steps apart (||s|| ~ 1e-3 ||u||, so the iterates' rounding-level differences are ~1e-3 of it), within
+    1e-2; y.s within 5e-3. The finite difference cancels: u +- 1e-4 s moves a typical parameter by a few fp32
+    ulps, so the rounding of the two evaluation points alone moves y by ~1e-2 (the reference runs it in
+    fp64; the oracle's own fp32 run lands 5x off here, at a ReLU kink). The device's y is therefore also
+    checked at ITS OWN fp32 evaluation points: the fp64 oracle's gradients at fl32(u +- eps s), differenced
+    and scaled as the device does, must match the device y to 5e-3 (what remains: the two fp32 batch
+    gradients' own rounding, amplified by the difference)."""
+    _, _, X64, Y64, _, _ = mnist
     r = cfg4_epoch
     dev, o64, o32 = r["p0"], r["o64"], r["o32"]
     names = ["w_t", "u", "s", "y"]
@@ -189,16 +196,29 @@ def test_cfg4_slbfgs_first_pair_full_size(cfg4_epoch):
     errs32 = {k: rel(o32[i], o64[i]) for i, k in enumerate(names)}
     step = rel(dev[0] - r["P0"], o64[0] - r["P0"])  # the 20 steps' displacement alone
     row, row64, row32 = r["pairs"][0], r["pairs64"][0], r["pairs32"][0]
+    # the device's FD at its own fp32 points (lincomb: fl32(u + eps s) from fp64 arithmetic), fp64 gradients
+    eps = 1e-4
+    u, s = dev[1], dev[2]
+    wp = (u + eps * s).astype(np.float32).astype(np.float64)
+    wm = (u - eps * s).astype(np.float32).astype(np.float64)
+    hb = r["idx64"][21 * 256: 21 * 256 + 128]        # minibatches 0..20, then the first Hessian batch
+    _, gp = r["onet"].loss_grad(wp, X64, Y64, idx=hb, lam=1e-4)
+    _, gm = r["onet"].loss_grad(wm, X64, Y64, idx=hb, lam=1e-4)
+    y_pts = (gp - gm) * float(np.float32(1.0 / (2.0 * eps)))
+    e_pts = rel(dev[3], y_pts)
+    ns, ns64 = float(np.sqrt(row[3])), float(np.sqrt(row64[3]))
     print("first pair (t = %d): " % int(row[1]) + ", ".join(f"{k} {errs[k]:.2e} (oracle fp32 {errs32[k]:.2e})"
                                                          for k in names) + f", w_t - w_0 {step:.2e}")
-    print(f"first pair y.s device {row[2]:.9e} fp64 {row64[2]:.9e} fp32 {row32[2]:.9e}; "
-          f"s.s device {row[3]:.9e} fp64 {row64[3]:.9e}; y.y device {row[4]:.9e} fp64 {row64[4]:.9e}")
+    print(f"first pair y.s device {row[2]:.9e} fp64 {row64[2]:.9e} fp32 {row32[2]:.9e}; ||s|| device {ns:.9e} "
+          f"fp64 {ns64:.9e}; y.y device {row[4]:.9e} fp64 {row64[4]:.9e}; device y vs fp64 at its fp32 points "
+          f"{e_pts:.2e}")
     assert int(row[0]) == int(row64[0]) == 0 and int(row[1]) == int(row64[1]) == 20
-    for k in ("w_t", "u", "s"):
+    for k in ("w_t", "u"):
         assert errs[k] <= 1e-4, (k, errs[k])
-    assert abs(row[2] - row64[2]) <= 1e-4 * abs(row64[2]), (row[2], row64[2])
-    assert abs(row[3] - row64[3]) <= 1e-4 * abs(row64[3]), (row[3], row64[3])
-    assert errs["y"] <= max(1e-4, 3.0 * errs32["y"]), (errs["y"], errs32["y"])
+    assert abs(ns - ns64) <= 1e-4 * ns64, (ns, ns64)
+    assert errs["s"] <= 1e-2, errs["s"]
+    assert abs(row[2] - row64[2]) <= 5e-3 * abs(row64[2]), (row[2], row64[2])
+    assert e_pts <= 5e-3, e_pts
 
 
 def test_cfg4_slbfgs_one_epoch_full_size(ctx, pkg, O, mnist, cfg4_epoch):
