@@ -904,6 +904,110 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_group_ker
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Wave-split-K direct-load main loop for the 32 x 128 tile (round 5; profiles/micro/loop32.hip, results in
+// profiles/r05/c/). The LDS-DMA loop of this tile spends ~1.8k cycles per 32-deep k-tile against 1024 of MFMA
+// issue: its DMA writes and fragment reads contend for the LDS while each wave waits on its reads, and the
+// DMA pieces' issue cost sits in front of the MFMAs. Here no operand is shared between waves and nothing
+// goes through LDS until the end: the four waves split every 32-deep k-tile (wave w: k 8w .. 8w+7, lane half
+// h: the 4 consecutive k 8w+4h .. +3), each lane loads its A quad A[row][k..k+3] and, per k, one 16-B quad of
+// the B row (columns n0 + 4 li .. +3) straight into registers, WSK_PD k-tiles ahead. The quad's 4 columns feed
+// 4 accumulators (accumulator c holds columns n0 + 4 j + c), 16 v_mfma_f32_32x32x2_f32 per wave per k-tile on 4
+// independent chains. After the loop the four waves' partial tiles are summed in wave order through LDS into
+// the standard accumulator layout (wave w owns columns n0 + 32w .. +31), so the epilogues (bias + activation,
+// split-K slab, the fused output layer) are the LDS-DMA kernel's. Fixed order throughout: a re-evaluation is
+// bitwise identical. Requires K, lda, ldb, N, k_chunk % 4 == 0 and 16-B aligned A, B (wsk_ok).
+// ------------------------------------------------------------------------------------------------
+constexpr int WSK_PD = 3;
+constexpr int WSK_RED_F = 4 * 16 * 2 * 128; // four waves' partial tiles, [wave][r][h][128 columns]
+
+template <int EPI, bool GATHER>
+__global__ __launch_bounds__(256, 1) void gemm_wsk_kernel(const GemmK g) {
+  constexpr int BM = 32, BN = 128;
+  constexpr int HEAD_F = headc::smem_floats_epi(BN, headc::TB);
+  constexpr int LDS_F = HEAD_F > WSK_RED_F ? HEAD_F : WSK_RED_F;
+  __shared__ __attribute__((aligned(16))) float lds[LDS_F];
+  if (g.abort && *g.abort) return;
+  if (int(blockIdx.z) < g.side_planes) {
+    gemm_side_job(g, reinterpret_cast<double *>(lds));
+    return;
+  }
+  const int zsplit = int(blockIdx.z) - g.side_planes;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int m0 = int(blockIdx.y) * BM, n0 = int(blockIdx.x) * BN;
+  const int kb = zsplit * g.k_chunk;
+  const int ke = min(g.K, kb + g.k_chunk);
+  headc::EpiPrefetch<BN, BM, 256> hpre;
+  if constexpr (EPI == EPI_HEAD) {
+    hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
+    if (g.head_fold > 0) hpre.load_fold(g.A, g.lda, g.a_idx, g.head_fold_c0, g.head_fold, m0, g.M);
+  }
+  // rows past M and columns past N read row 0 / column n0 (finite data); the epilogues mask them
+  const int row = m0 + li;
+  long long grow = row < g.M ? row : 0;
+  if (GATHER && row < g.M) grow = g.a_idx[row];
+  const int k4 = 8 * wave + 4 * lh;
+  const int col = n0 + 4 * li;
+  const float *ap = g.A + grow * g.lda + kb + k4;
+  const float *bp = g.B + (long long)(kb + k4) * g.ldb + (col < g.N ? col : n0);
+  const int nk = kb < ke ? (ke - kb + 31) / 32 : 0;
+  f32x16 acc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[c][r] = 0.0f;
+  f32x4 ra[WSK_PD], rb[WSK_PD][4];
+  bool okm[WSK_PD];
+  // k-tile tt into register slot `slot`: clamped and unconditional (a k quad is all in or all out of
+  // [kb, ke): k4, kb, ke are multiples of 4); the mask is applied at the use
+  auto load = [&](int tt, int slot) {
+    const bool ok = kb + tt * 32 + k4 < ke;
+    const long long ko = ok ? (long long)tt * 32 : 0;
+    okm[slot] = ok;
+    ra[slot] = *reinterpret_cast<const f32x4 *>(ap + ko);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rb[slot][q] = *reinterpret_cast<const f32x4 *>(bp + (ko + q) * g.ldb);
+  };
+#pragma unroll
+  for (int p = 0; p < WSK_PD; ++p) load(p, p);
+  for (int i0 = 0; i0 < nk; i0 += WSK_PD) {
+#pragma unroll
+    for (int p = 0; p < WSK_PD; ++p) {
+      const int i = i0 + p;
+      if (i < nk) { // wave-uniform
+        f32x4 a = ra[p];
+        if (!okm[p]) a = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q], rb[p][q][c], acc[c], 0, 0, 0);
+      }
+      // the slot's next k-tile, issued after the MFMAs that read it (no register copy, so no wait for the new
+      // data in this iteration): WSK_PD - 1 k-tiles of MFMAs ahead of its use
+      __builtin_amdgcn_sched_barrier(0);
+      load(i + WSK_PD, p);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // the partial tiles, summed in wave order, into the standard layout (wave w: columns 32w + j)
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    *reinterpret_cast<f32x4 *>(&lds[((wave * 16 + r) * 2 + lh) * 128 + li * 4]) =
+        f32x4{acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
+  __syncthreads();
+  f32x16 out[1][1];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = lds[((0 * 16 + r) * 2 + lh) * 128 + 32 * wave + li];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) v += lds[((w * 16 + r) * 2 + lh) * 128 + 32 * wave + li];
+    out[0][0][r] = v;
+  }
+  __syncthreads(); // the LDS is the epilogue's now
+  gemm_epilogue<1, 4, 1, 1, EPI, 1>(g, out, lds, hpre, zsplit, m0, n0, 0, wave, li, lh, 0);
+}
+
 namespace {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -1017,13 +1121,33 @@ void launch(hipStream_t s, const GemmDesc &d, const GemmDesc *d2 = nullptr) {
   }
 }
 
+// gemm_wsk_kernel's conditions: forward operand layout, 16-B quads everywhere, no A-from-slabs prologue.
+// LBF_NO_WSK=1 keeps the LDS-DMA loop (A/B measurements).
+static bool wsk_ok(const GemmDesc &d) {
+  static const bool off = [] {
+    const char *e = std::getenv("LBF_NO_WSK");
+    return e && std::atoi(e) != 0;
+  }();
+  const int kc = d.splits > 1 ? d.k_chunk : d.K;
+  return !off && d.a_kc && !d.b_kc && !d.a_slab && d.K % 4 == 0 && d.lda % 4 == 0 && d.ldb % 4 == 0 && d.N % 4 == 0 &&
+         kc % 4 == 0 && aligned16(d.A) && aligned16(d.B) && (d.epi == EPI_FWD || d.epi == EPI_STORE || d.epi == EPI_HEAD);
+}
+
 template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const GemmDesc &d) {
   // LDS-DMA stages: as many tile buffers as fit two workgroups per CU (80 KB each); the register-staged
   // fallback (gathered mn-contiguous operands, odd shapes) keeps two k-tiles of loads in flight
-  if (d.tile == TILE_32x128) { // 32 x 128 (20 KB per stage), one 8-wave workgroup (two k-groups) per CU
-    // (six stages, a software-pipelined loop, dedicated loader waves and a direct-from-L2 operand path all
-    // measured no faster: profiles/r02/gemm_small_tiles.txt, profiles/r03/bench_7500_direct.json; these
-    // tiles are bound by the per-CU operand delivery rate, ~22 GB/s per CU)
+  if (d.tile == TILE_32x128) {
+    if constexpr (AKC && !BKC && EPI != EPI_DX) {
+      if (wsk_ok(d)) { // the wave-split-K direct-load loop (gemm_wsk_kernel)
+        GemmK k = make_gemmk<32, 128>(d);
+        const dim3 grid(unsigned(k.gx), unsigned(k.gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
+        if (d.a_idx) hipLaunchKernelGGL((gemm_wsk_kernel<EPI, true>), grid, dim3(256), 0, s, k);
+        else hipLaunchKernelGGL((gemm_wsk_kernel<EPI, false>), grid, dim3(256), 0, s, k);
+        return;
+      }
+    }
+    // 32 x 128 (20 KB per stage), one 8-wave workgroup (two k-groups) per CU: the LDS-DMA loop (A from the
+    // previous layer's slabs, dX, shapes the direct loop does not take)
     launch<1, 4, 1, 1, AKC, BKC, EPI, 2, 2, 4>(s, d);
   } else if (d.tile == TILE_64x128) { // 64 x 128 (24 KB per stage), two workgroups per CU
     launch<2, 2, 1, 2, AKC, BKC, EPI, 1, 2, 3>(s, d);
