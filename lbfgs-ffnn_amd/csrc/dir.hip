@@ -317,6 +317,10 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs 
   st.want_dir = a.want_dir;
   st.iter = a.iter;
   st.dsign = a.dsign;
+  if (a.kmat && a.g.policy == POL_SLBFGS && m <= DIR_MAXM) { // the pair update's coefficient map (hist_core)
+    st.kmat = a.kmat;
+    st.kscr = rhop + S_; // after SY, YY, rho (cols_fin_launch sizes it)
+  }
   if (fused) {
     st.ist = ist_l;
     st.rho = rhop;
@@ -358,33 +362,33 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_kernel(const DirArgs a) {
 }
 
 // The S-LBFGS direction step's coefficients and its combine in one launch (direction-only steps: has_g, no
-// pair, no reset; k <= KQ live pairs). Every block stages the ring header, the dots, SY, YY and rho (one
-// round trip, with its g and x quads), issues its quads of the live history vectors, and while they are in
-// flight wave 0 runs the two-loop recurrences (recur_fast, hist_core's fast path: bitwise the same
-// coefficients); then p = sum c_i basis_i and x_out = x_in + alpha p as combine_small computes them.
-// Block 0 also makes the step's global writes (g-dots rows, coefficients, scalars: hist_core's for this
-// step; no block of the launch reads any of them, and the ring header every block reads is not written),
-// so the state after the launch is what dir_cols_fin + combine leave. Replaces dir_cols_fin's serial step
-// and the combine's header round trip on the critical path.
+// pair, no reset; k <= KQ live pairs). Every block stages the ring header, the dots and the pairs' coefficient
+// map K (slbfgs_kmat, written by the last pair update: [cS; cY] = K [S^T g; Y^T g], one round trip with its g
+// and x quads), issues its quads of the live history vectors, and while they are in flight wave 0 computes
+// the 2k coefficients as one 2k x 2k mat-vec (the two-loop recursion of s_lbfgs.hpp:106-136 in compact form;
+// before round 5 each block ran the two k-step recurrences here); then p = sum c_i basis_i and
+// x_out = x + alpha p with combine_small's arithmetic. Block 0 also makes the step's global writes (g-dots,
+// coefficients, scalars: hist_core's for this step; no block of the launch reads any of them, and the ring
+// header every block reads is not written), so the state after the launch is what dir_cols_fin + combine
+// leave.
 template <int KQ>
 __global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const CombineArgs cb) {
   const HistView &h = a.g.h;
   if (h.abort && *h.abort) return;
-  constexpr int MM = DIR_MAXM, SS = DIR_MAXM + 1;
-  __shared__ double sSY[SS * SS], sYY[SS * SS], srho[SS];
-  __shared__ double sy[2 * MM * MM], yyl[MM * MM];
-  __shared__ double dl[6 * MM + 6], gS_l[MM], gY_l[MM], rho_l[MM], cf[2 * MM + 1];
+  constexpr int MM = DIR_MAXM;
+  __shared__ double sK[DIR_KS * DIR_KS];
+  __shared__ double dl[6 * MM + 6], cf[2 * MM + 1];
   __shared__ int Ls[MM];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int m = h.m, S_ = h.slots;
-  // ---- round trip 1: header, dots, Gram blocks, rho; this lane's g and x ----
+  // ---- round trip 1: header, dots, K and gamma; this lane's g and x ----
   const int k = __builtin_amdgcn_readfirstlane(h.ist[IST_COUNT]);
   if (t < m) Ls[t] = h.ist[IST_ORDER + t];
-  for (int i = t; i < S_ * S_; i += 256) {
-    sSY[i] = h.SY[i];
-    sYY[i] = h.YY[i];
+  for (int i = t; i < 4 * k * k; i += 256) { // rows and columns < 2k of the DIR_KS-stride map
+    const int r = i / (2 * k), c = i - r * (2 * k);
+    sK[r * DIR_KS + c] = a.kmat[r * DIR_KS + c];
   }
-  if (t < S_) srho[t] = h.rho[t];
+  const double gamma = k > 0 ? a.kmat[DIR_KS * DIR_KS] : 1.0;
   if (t < 6 * m + 6) dl[t] = a.dots[t];
   const long long n = h.n;
   const long long e = ((long long)blockIdx.x * 256 + t) * 4;
@@ -393,7 +397,7 @@ __global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const
   const f32x4 g4 = *reinterpret_cast<const f32x4 *>(cb.g + eq);
   const f32x4 x4 = *reinterpret_cast<const f32x4 *>((cb.x_out ? cb.x_in : cb.g) + eq);
   lds_barrier();
-  // ---- round trip 2: this lane's quads of the live history vectors, in flight through the recurrences ----
+  // ---- round trip 2: this lane's quads of the live history vectors, in flight through the mat-vec ----
   f32x4 sv[KQ], yv[KQ];
   if (k > 0)
 #pragma unroll
@@ -403,39 +407,25 @@ __global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const
       yv[i] = *reinterpret_cast<const f32x4 *>(h.Y + off);
     }
   if (wave == 0) {
-    // stage the live pairs' Gram entries in order (hist_core C1 with no pair: L = L0, the fresh dots' rows)
-    for (int q = lane; q < k * k; q += 64) {
-      const int i = q / k, j = q - i * k;
-      const double v = sSY[Ls[i] * S_ + Ls[j]];
-      sy[q] = v;
-      sy[k * k + j * k + i] = v; // transposed copy
-      yyl[q] = sYY[Ls[i] * S_ + Ls[j]];
-    }
-    if (lane < k) {
-      gS_l[lane] = dl[6 * lane + 4];
-      gY_l[lane] = dl[6 * lane + 5];
-      rho_l[lane] = srho[Ls[lane]];
-    }
-    const double gg = dl[6 * m + 5];
-    const double gamma = k > 0 ? slbfgs_gamma(sy[(k - 1) * k + (k - 1)], yyl[(k - 1) * k + (k - 1)]) : 1.0;
-    double al0 = 0.0, c0 = 0.0;
-    recur_fast(k, lane, rho_l, gS_l, gY_l, sy, sy + k * k, yyl, gamma, al0, c0);
+    // lane i < 2k: c_i = sum_j K[i][j] v_j, v = [S^T g ; Y^T g] (the fresh dots, logical order)
+    double c = 0.0;
+    if (lane < 2 * k)
+      for (int j = 0; j < 2 * k; ++j) c += sK[lane * DIR_KS + j] * (j < k ? dl[6 * j + 4] : dl[6 * (j - k) + 5]);
     const double ds = a.dsign;
-    if (lane < k) {
-      cf[lane] = ds * c0;
-      cf[MM + lane] = ds * (-gamma * al0);
-    }
+    const double gg = dl[6 * m + 5];
+    if (lane < k) cf[lane] = ds * c;
+    else if (lane < 2 * k) cf[MM + lane - k] = ds * c;
     if (lane == 0) cf[2 * MM] = ds * gamma;
     if (blockIdx.x == 0) { // hist_core's global writes for this step (FUSED, has_g, no pair, want_dir 1)
-      double part = 0.0;
-      if (lane < k) part += c0 * gS_l[lane] - gamma * al0 * gY_l[lane];
-      const double gTz = wave_sum_f64(part) + gamma * gg;
+      const double v = lane < k ? dl[6 * lane + 4] : (lane < 2 * k ? dl[6 * (lane - k) + 5] : 0.0);
+      const double gTz = wave_sum_f64(lane < 2 * k ? c * v : 0.0) + gamma * gg;
       if (lane < k) {
         const int j = Ls[lane];
-        h.gS[j] = gS_l[lane];
-        h.gY[j] = gY_l[lane];
-        h.coef[lane] = ds * c0;
-        h.coef[S_ + lane] = ds * (-gamma * al0);
+        h.gS[j] = dl[6 * lane + 4];
+        h.gY[j] = dl[6 * lane + 5];
+        h.coef[lane] = ds * c;
+      } else if (lane < 2 * k) {
+        h.coef[S_ + lane - k] = ds * c;
       }
       if (lane == 0) {
         h.coef[2 * S_] = ds * gamma;
@@ -536,7 +526,7 @@ static void cols_fin_launch(hipStream_t s, const DirArgs &a) {
   }();
   (void)attr_set;
   const int m = a.g.h.m, S_ = a.g.h.slots;
-  const size_t shmem = (size_t(3) * m * m + 2 * size_t(S_) * S_ + S_) * sizeof(double);
+  const size_t shmem = (size_t(3) * m * m + 2 * size_t(S_) * S_ + S_ + size_t(DIR_MAXM) * DIR_MAXM) * sizeof(double);
   hipLaunchKernelGGL(dir_cols_fin_kernel, dim3(unsigned(dir_ncols(m))), dim3(DF_THREADS), shmem, s, a);
   LBF_KERNEL_CHECK();
 }
@@ -546,7 +536,7 @@ void dir_fin(hipStream_t s, const DirArgs &a) { cols_fin_launch(s, a); }
 bool dir_combine_supported(const DirArgs &a, const CombineArgs &c) {
   const GramArgs &g = a.g;
   return a.want_dir == 1 && g.has_g && !g.has_pair && !g.reset && g.policy == POL_SLBFGS && g.h.m <= DIR_MAXM &&
-         !c.alpha_from_state && g.h.ld % 4 == 0;
+         !c.alpha_from_state && g.h.ld % 4 == 0 && a.kmat != nullptr;
 }
 
 void dir_cols_combine(hipStream_t s, const DirArgs &a, const CombineArgs &c) {

@@ -920,12 +920,20 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_group_ker
 // ------------------------------------------------------------------------------------------------
 constexpr int WSK_PD = 3;
 constexpr int WSK_RED_F = 4 * 16 * 2 * 128; // four waves' partial tiles, [wave][r][h][128 columns]
+constexpr int WSK_MAX_ASPLITS = 8;          // A-from-slabs: splits summed per quad (gemm_wsk_ok)
 
-template <int EPI, bool GATHER>
+// BKC: B stored k-contiguous (B[n*ldb + k]: the dX GEMM's W^T): a lane loads, per column block c, the quad
+// B[n0 + 32c + li][k..k+3], and accumulator c holds the standard columns n0 + 32c + j. Else (B n-contiguous)
+// the lane loads, per k, the quad B[k][n0 + 4li .. +3], and accumulator c holds columns n0 + 4j + c.
+// ASUM: the A quad is act(sum over the previous layer's forward split-K slabs in split order + bias) (the
+// LDS-DMA kernel's prologue and fwd_reduce_act's arithmetic), and the workgroups of column tile 0 store it to
+// a_out for the backward phase.
+template <int EPI, bool GATHER, bool BKC, bool ASUM>
 __global__ __launch_bounds__(256, 1) void gemm_wsk_kernel(const GemmK g) {
   constexpr int BM = 32, BN = 128;
   constexpr int HEAD_F = headc::smem_floats_epi(BN, headc::TB);
   constexpr int LDS_F = HEAD_F > WSK_RED_F ? HEAD_F : WSK_RED_F;
+  constexpr int NA = ASUM ? WSK_MAX_ASPLITS : 1; // A quads per k-tile
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
   if (g.abort && *g.abort) return;
   if (int(blockIdx.z) < g.side_planes) {
@@ -945,19 +953,29 @@ __global__ __launch_bounds__(256, 1) void gemm_wsk_kernel(const GemmK g) {
   }
   // rows past M and columns past N read row 0 / column n0 (finite data); the epilogues mask them
   const int row = m0 + li;
-  long long grow = row < g.M ? row : 0;
-  if (GATHER && row < g.M) grow = g.a_idx[row];
+  const bool rok = row < g.M;
+  long long grow = rok ? row : 0;
+  if (GATHER && rok) grow = g.a_idx[row];
   const int k4 = 8 * wave + 4 * lh;
-  const int col = n0 + 4 * li;
-  const float *ap = g.A + grow * g.lda + kb + k4;
-  const float *bp = g.B + (long long)(kb + k4) * g.ldb + (col < g.N ? col : n0);
+  const float *ap = (ASUM ? g.a_slab : g.A) + grow * g.lda + kb + k4;
+  const float *bp[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if constexpr (BKC) {
+      const int n = n0 + 32 * c + li;
+      bp[c] = g.B + (long long)(n < g.N ? n : n0) * g.ldb + kb + k4;
+    } else {
+      const int col = n0 + 4 * li;
+      bp[c] = g.B + (long long)(kb + k4 + c) * g.ldb + (col < g.N ? col : n0); // c: the k within the quad
+    }
+  }
   const int nk = kb < ke ? (ke - kb + 31) / 32 : 0;
   f32x16 acc[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[c][r] = 0.0f;
-  f32x4 ra[WSK_PD], rb[WSK_PD][4];
+  f32x4 ra[WSK_PD][NA], rb[WSK_PD][4], rbias[WSK_PD];
   bool okm[WSK_PD];
   // k-tile tt into register slot `slot`: clamped and unconditional (a k quad is all in or all out of
   // [kb, ke): k4, kb, ke are multiples of 4); the mask is applied at the use
@@ -965,9 +983,17 @@ __global__ __launch_bounds__(256, 1) void gemm_wsk_kernel(const GemmK g) {
     const bool ok = kb + tt * 32 + k4 < ke;
     const long long ko = ok ? (long long)tt * 32 : 0;
     okm[slot] = ok;
-    ra[slot] = *reinterpret_cast<const f32x4 *>(ap + ko);
+    if constexpr (ASUM) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) rb[slot][q] = *reinterpret_cast<const f32x4 *>(bp + (ko + q) * g.ldb);
+      for (int u = 0; u < NA; ++u) // every split's quad (clamped split; masked in the sum)
+        ra[slot][u] = *reinterpret_cast<const f32x4 *>(ap + (long long)min(u, g.a_splits - 1) * g.a_slab_stride + ko);
+      rbias[slot] = *reinterpret_cast<const f32x4 *>(g.a_bias + kb + k4 + ko);
+    } else {
+      ra[slot][0] = *reinterpret_cast<const f32x4 *>(ap + ko);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      rb[slot][c] = *reinterpret_cast<const f32x4 *>(bp[c] + (BKC ? ko : ko * g.ldb));
   };
 #pragma unroll
   for (int p = 0; p < WSK_PD; ++p) load(p, p);
@@ -976,12 +1002,25 @@ __global__ __launch_bounds__(256, 1) void gemm_wsk_kernel(const GemmK g) {
     for (int p = 0; p < WSK_PD; ++p) {
       const int i = i0 + p;
       if (i < nk) { // wave-uniform
-        f32x4 a = ra[p];
+        f32x4 a;
+        if constexpr (ASUM) {
+          f32x4 sum = ra[p][0];
+#pragma unroll
+          for (int u = 1; u < NA; ++u)
+            if (u < g.a_splits) sum += ra[p][u];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a[e] = act_rt(g.a_act, sum[e] + rbias[p][e]);
+          if (okm[p] && rok && n0 == 0) // column tile 0 stores the activations (bitwise fwd_reduce_act's)
+            *reinterpret_cast<f32x4 *>(g.a_out + (long long)row * g.lda + kb + k4 + (long long)i * 32) = a;
+        } else {
+          a = ra[p][0];
+        }
         if (!okm[p]) a = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q], rb[p][q][c], acc[c], 0, 0, 0);
+          for (int c = 0; c < 4; ++c)
+            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q], BKC ? rb[p][c][q] : rb[p][q][c], acc[c], 0, 0, 0);
       }
       // the slot's next k-tile, issued after the MFMAs that read it (no register copy, so no wait for the new
       // data in this iteration): WSK_PD - 1 k-tiles of MFMAs ahead of its use
@@ -992,9 +1031,15 @@ __global__ __launch_bounds__(256, 1) void gemm_wsk_kernel(const GemmK g) {
   }
   // the partial tiles, summed in wave order, into the standard layout (wave w: columns 32w + j)
 #pragma unroll
-  for (int r = 0; r < 16; ++r)
-    *reinterpret_cast<f32x4 *>(&lds[((wave * 16 + r) * 2 + lh) * 128 + li * 4]) =
-        f32x4{acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
+  for (int r = 0; r < 16; ++r) {
+    float *dst = &lds[((wave * 16 + r) * 2 + lh) * 128];
+    if constexpr (BKC) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[32 * c + li] = acc[c][r];
+    } else {
+      *reinterpret_cast<f32x4 *>(dst + li * 4) = f32x4{acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
+    }
+  }
   __syncthreads();
   f32x16 out[1][1];
 #pragma unroll
@@ -1129,20 +1174,33 @@ static bool wsk_ok(const GemmDesc &d) {
     return e && std::atoi(e) != 0;
   }();
   const int kc = d.splits > 1 ? d.k_chunk : d.K;
-  return !off && d.a_kc && !d.b_kc && !d.a_slab && d.K % 4 == 0 && d.lda % 4 == 0 && d.ldb % 4 == 0 && d.N % 4 == 0 &&
-         kc % 4 == 0 && aligned16(d.A) && aligned16(d.B) && (d.epi == EPI_FWD || d.epi == EPI_STORE || d.epi == EPI_HEAD);
+  const bool base = !off && d.a_kc && d.K % 4 == 0 && d.lda % 4 == 0 && d.ldb % 4 == 0 && kc % 4 == 0 &&
+                    aligned16(d.A) && aligned16(d.B);
+  if (!base) return false;
+  if (d.a_slab) // A from the previous layer's slabs: forward operand layout, split-K store or plain forward
+    return !d.b_kc && !d.a_idx && (d.epi == EPI_STORE || d.epi == EPI_FWD) && d.N % 4 == 0 && d.a_splits >= 1 &&
+           d.a_splits <= WSK_MAX_ASPLITS && d.a_slab_stride % 4 == 0 && aligned16(d.a_slab) && aligned16(d.a_bias) &&
+           aligned16(d.a_out);
+  if (d.b_kc) return d.epi == EPI_DX; // dX: B = W^T stored k-contiguous
+  return d.N % 4 == 0 && (d.epi == EPI_FWD || d.epi == EPI_STORE || d.epi == EPI_HEAD);
 }
 
 template <bool AKC, bool BKC, int EPI> void dispatch_tile(hipStream_t s, const GemmDesc &d) {
   // LDS-DMA stages: as many tile buffers as fit two workgroups per CU (80 KB each); the register-staged
   // fallback (gathered mn-contiguous operands, odd shapes) keeps two k-tiles of loads in flight
   if (d.tile == TILE_32x128) {
-    if constexpr (AKC && !BKC && EPI != EPI_DX) {
+    if constexpr (AKC) {
       if (wsk_ok(d)) { // the wave-split-K direct-load loop (gemm_wsk_kernel)
         GemmK k = make_gemmk<32, 128>(d);
         const dim3 grid(unsigned(k.gx), unsigned(k.gy), unsigned((d.splits > 1 ? d.splits : 1) + k.side_planes));
-        if (d.a_idx) hipLaunchKernelGGL((gemm_wsk_kernel<EPI, true>), grid, dim3(256), 0, s, k);
-        else hipLaunchKernelGGL((gemm_wsk_kernel<EPI, false>), grid, dim3(256), 0, s, k);
+        if (d.a_slab) {
+          if constexpr (!BKC && EPI != EPI_HEAD && EPI != EPI_DX)
+            hipLaunchKernelGGL((gemm_wsk_kernel<EPI, false, false, true>), grid, dim3(256), 0, s, k);
+        } else if (d.a_idx) {
+          hipLaunchKernelGGL((gemm_wsk_kernel<EPI, true, BKC, false>), grid, dim3(256), 0, s, k);
+        } else {
+          hipLaunchKernelGGL((gemm_wsk_kernel<EPI, false, BKC, false>), grid, dim3(256), 0, s, k);
+        }
         return;
       }
     }

@@ -28,6 +28,7 @@ namespace lbf {
 constexpr int COEF_MAXK = 128;
 
 struct HistSmem {
+  double cscr[(DIR_MAXM + 1) * DIR_MAXM + DIR_MAXM]; // compact_coef: R^-1 (row stride DIR_MAXM + 1), a vector
   double dots[6 * COEF_MAXK + 6];
   double gS_l[COEF_MAXK], gY_l[COEF_MAXK], rho_l[COEF_MAXK], alpha_l[COEF_MAXK], c_l[COEF_MAXK];
   int L0[COEF_MAXK + 1], L[COEF_MAXK + 1], inv0[COEF_MAXK + 1];
@@ -45,6 +46,10 @@ struct HistStep {
   // in LDS by the caller (the fused tail prefetches them with its first loads). Unused otherwise.
   const int *ist = nullptr;
   const double *rho = nullptr, *SY = nullptr, *YY = nullptr;
+  // S-LBFGS pair updates (dir_cols_fin, k <= DIR_MAXM): the live pairs' coefficient map K (slbfgs_kmat) into
+  // kmat (global, DIR_KMAT_N doubles), computed by wave 1 beside wave 0's recurrences; kscr: DIR_MAXM^2 doubles
+  // of LDS
+  double *kmat = nullptr, *kscr = nullptr;
 };
 
 // Ring slot the next pair is written to.
@@ -130,10 +135,141 @@ __device__ __forceinline__ void recur_fast(int k, int lane, const double *rho_l,
   }
 }
 
+// The two-loop coefficients of recur_fast (alpha = al0, alpha - beta = c0 for this lane's index) in compact form
+// (Byrd, Nocedal & Schnabel 1994; see slbfgs_kmat below for the algebra, exact for any rho): with R[i][j] =
+// s_i.y_j (i < j), R[i][i] = 1/rho_i, alpha = R^-1 gS (the backward recurrence) and alpha - beta =
+// R^-T (D alpha + gamma (YY alpha - gY)) (the forward one), D = diag(1/rho). Lane j computes column j of R^-1
+// by back substitution (no cross-lane dependency: the recurrences' k dependent v_readlane steps become
+// independent per-lane FMA chains), then three mat-vecs with one LDS exchange each. k <= KM; scr: (KM + 1) KM
+// + KM doubles of LDS; one wave.
+template <int KM>
+__device__ __forceinline__ void compact_coef(int k, int lane, const double *rho_l, const double *gS_l,
+                                             const double *gY_l, const double *sy, const double *yyl, double gamma,
+                                             double *scr, double &al0, double &c0) {
+  constexpr int LD = KM + 1; // odd stride: the row reads of R^-1 across lanes are conflict-free
+  double *rinv = scr, *vb = scr + KM * LD;
+  const int j = lane;
+  double x[KM]; // column j of R^-1
+#pragma unroll
+  for (int i = 0; i < KM; ++i) x[i] = 0.0;
+  if (j < k) {
+#pragma unroll
+    for (int i = KM - 1; i >= 0; --i) {
+      if (i == j) x[i] = rho_l[j];
+      if (i < j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int l = i + 1; l < KM; ++l)
+          if (l <= j) acc += sy[i * k + l] * x[l];
+        x[i] = -rho_l[i] * acc;
+      }
+    }
+  }
+  if (j < KM)
+#pragma unroll
+    for (int i = 0; i < KM; ++i) rinv[i * LD + j] = x[i];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  double p = 0.0; // alpha_lane = (R^-1 gS)_lane
+  if (lane < k)
+#pragma unroll
+    for (int jj = 0; jj < KM; ++jj)
+      if (jj < k) p += rinv[lane * LD + jj] * gS_l[jj];
+  al0 = p;
+  if (lane < KM) vb[lane] = p;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  double q = 0.0; // (D alpha + gamma (YY alpha - gY))_lane
+  if (lane < k) {
+    double acc = 0.0;
+#pragma unroll
+    for (int l = 0; l < KM; ++l)
+      if (l < k) acc += yyl[lane * k + l] * vb[l];
+    q = p / rho_l[lane] + gamma * (acc - gY_l[lane]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every lane has read vb
+  __builtin_amdgcn_wave_barrier();
+  if (lane < KM) vb[lane] = q;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  double c = 0.0; // (R^-T q)_lane = sum_l R^-1[l][lane] q_l: this lane's own column
+  if (lane < k)
+#pragma unroll
+    for (int l = 0; l < KM; ++l)
+      if (l < k) c += x[l] * vb[l];
+  c0 = c;
+}
+
 // The slbfgs gamma (s_lbfgs.hpp:119-126) from the newest pair's ys and yy.
 __device__ __forceinline__ double slbfgs_gamma(double ys, double yy) {
   const double g = fabs(yy) < 1e-12 ? 1.0 : ys / yy;
   return fmin(fmax(g, 1e-6), 1e6);
+}
+
+// The S-LBFGS direction's coefficient map (round 5). With R the k x k upper-triangular matrix R[i][j] = s_i.y_j
+// (i < j), R[i][i] = 1 / rho_i, the two-loop recursion of s_lbfgs.hpp:106-136 is, for ANY rho (checked in
+// numpy to 5e-16), H g = gamma g + S cS + Y cY with
+//   cY = -gamma R^-1 a,   cS = R^-T ((D + gamma YY) R^-1 a - gamma b),   a = S^T g, b = Y^T g, D = diag(1/rho)
+// (the compact form of Byrd, Nocedal & Schnabel 1994): the backward recurrence is R^-1 a, the forward one
+// R^-T q. So [cS; cY] = K [a; b] with K = [[R^-T M R^-1, -gamma R^-T], [-gamma R^-1, 0]], M = D + gamma YY,
+// and K depends only on the pairs, which change once every L inner steps: one wave computes it at each pair
+// update (lane j: column j of R^-1 by back substitution, then column j of M R^-1 and of R^-T M R^-1; no
+// cross-lane dependency), and every direction-only step's combine blocks do ONE 2k x 2k mat-vec instead of
+// the two k-step recurrences (dir_combine_kernel). Operands from LDS: sy = SY of the live pairs (k x k, row
+// stride k), yyl = YY, rho_l; rinv: DIR_MAXM^2 doubles of LDS; K: global, row stride DIR_KS, gamma after it.
+__device__ inline void slbfgs_kmat(int k, int lane, const double *rho_l, const double *sy, const double *yyl,
+                                   double *rinv, double *K) {
+  constexpr int KM = DIR_MAXM;
+  const double gamma = k > 0 ? slbfgs_gamma(sy[(k - 1) * k + (k - 1)], yyl[(k - 1) * k + (k - 1)]) : 1.0;
+  const int j = lane;
+  double x[KM];
+#pragma unroll
+  for (int i = 0; i < KM; ++i) x[i] = 0.0;
+  if (j < k) {
+#pragma unroll
+    for (int i = KM - 1; i >= 0; --i) { // back substitution for column j: R x = e_j
+      if (i == j) x[i] = rho_l[j];
+      if (i < j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int l = i + 1; l < KM; ++l)
+          if (l <= j) acc += sy[i * k + l] * x[l];
+        x[i] = -rho_l[i] * acc;
+      }
+    }
+  }
+  if (j < KM)
+#pragma unroll
+    for (int i = 0; i < KM; ++i) rinv[i * KM + j] = x[i];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // one wave: its own LDS writes are complete
+  __builtin_amdgcn_wave_barrier();
+  if (j < k) {
+    double tcol[KM]; // column j of M R^-1
+#pragma unroll
+    for (int i = 0; i < KM; ++i) {
+      tcol[i] = 0.0;
+      if (i < k) {
+        double acc = 0.0;
+#pragma unroll
+        for (int l = 0; l < KM; ++l)
+          if (l < k) acc += yyl[i * k + l] * x[l];
+        tcol[i] = x[i] / rho_l[i] + gamma * acc;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < KM; ++i)
+      if (i < k) {
+        double acc = 0.0; // (R^-T M R^-1)[i][j] = sum_l R^-1[l][i] (M R^-1)[l][j]
+#pragma unroll
+        for (int l = 0; l < KM; ++l)
+          if (l < k) acc += rinv[l * KM + i] * tcol[l];
+        K[i * DIR_KS + j] = acc;
+        K[i * DIR_KS + k + j] = -gamma * rinv[j * KM + i]; // -gamma R^-T
+        K[(k + i) * DIR_KS + j] = -gamma * x[i];           // -gamma R^-1
+        K[(k + i) * DIR_KS + k + j] = 0.0;
+      }
+  }
+  if (lane == 0) K[DIR_KS * DIR_KS] = gamma;
 }
 
 // Barriers here are LDS-only (wave.hpp lds_barrier): within a history step no thread reads global
@@ -350,6 +486,8 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
   lds_barrier();
   KTF(59);
   if (wave != 0) {
+    if (wave == 1 && a.kmat && a.policy == POL_SLBFGS && k <= DIR_MAXM && sy_t && yy_lds)
+      slbfgs_kmat(k, lane, sm.rho_l, sy, yyl, a.kscr, a.kmat); // beside wave 0's recurrences
     if constexpr (FUSED) { // the deferred writes of step B (the live count: wave 0, below)
       const int u = t - 64, nu = nt - 64;
       write_rows(u, nu);
@@ -391,7 +529,10 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
   if (k <= 64 && sy_t && yy_lds) {
     KTF(63);
     KTC(64);
-    recur_fast(k, lane, rho_l, gS_l, gY_l, sy, syT, yyl, gamma, al0, c0);
+    if (k <= DIR_MAXM && h.compact)
+      compact_coef<DIR_MAXM>(k, lane, rho_l, gS_l, gY_l, sy, yyl, gamma, sm.cscr, al0, c0);
+    else
+      recur_fast(k, lane, rho_l, gS_l, gY_l, sy, syT, yyl, gamma, al0, c0);
   } else if (big) {
     // Two indices per lane (l0 = lane, l1 = lane + 64); the LDS operands of 8 steps are loaded ahead
     // of them, so each step is VALU + v_readlane only (the k <= 64 fast path, widened).

@@ -328,6 +328,9 @@ struct HistView {
   double *coef = nullptr; // [2*slots + 1]: cs (logical), cy (logical), cg
   double *scal = nullptr; // SC_N
   const int *abort = nullptr; // speculative execution flag (nullable)
+  // two-loop coefficients for k <= DIR_MAXM live pairs in compact form (hist_core.hpp compact_coef) instead of
+  // the readlane recurrences; LBF_NO_COMPACT=1 clears it (A/B)
+  int compact = 1;
 };
 
 struct GramArgs {
@@ -400,6 +403,10 @@ int tail_vpw(int m);                                // vectors per wave of the G
 // against the live history (one block per 64*C columns, a partial row each, stored [nc][nb]), then one
 // block per Gram column whose last arrival runs the history step (hist_core.hpp) from the column sums.
 constexpr int DIR_MAXM = 16;
+// The S-LBFGS direction's coefficient map K ([cS; cY] = K [S^T g; Y^T g], hist_core.hpp slbfgs_kmat): row stride
+// DIR_KS, then gamma at [DIR_KS * DIR_KS]
+constexpr int DIR_KS = 2 * DIR_MAXM;
+constexpr int DIR_KMAT_N = DIR_KS * DIR_KS + 4;
 constexpr long long DIR_MAXN = 1LL << 22;
 struct CombineArgs {
   HistView h;
@@ -424,6 +431,9 @@ struct DirArgs {
   // instead of read; segments without splits (finished by the dW launch's side blocks) read gred.G
   RedAllArgs gred;
   int gred_on = 0;
+  // S-LBFGS (POL_SLBFGS, k <= DIR_MAXM): the coefficient map of the live pairs, written by every pair update
+  // (dir_fin) and read by the direction-only steps (dir_cols_combine); DIR_KMAT_N doubles
+  double *kmat = nullptr;
 };
 bool dir_supported(int m, long long n);
 int dir_cols_per_block(int m, long long n);

@@ -1064,6 +1064,7 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
   part_.resize(size_t(gram_nwg(n)) * gram_ncols(m));
   red_.resize(size_t(kGramFold) * gram_ncols(m));
   v_.m = m;
+  v_.compact = env_int("LBF_NO_COMPACT", 0) != 0 ? 0 : 1;
   v_.slots = slots;
   v_.n = n;
   v_.ld = ld;
@@ -1096,6 +1097,8 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
     const int nb = int(cdiv(n, dir_cols_per_block(m, n)));
     drows_.resize(size_t(dir_ncols(m)) * size_t(nb));
     ddots_.resize(size_t(dir_ncols(m)));
+    dkmat_.resize(size_t(DIR_KMAT_N));
+    LBF_HIP(hipMemsetAsync(dkmat_.get(), 0, dkmat_.size() * sizeof(double), ctx_->stream));
     dcount_.resize(1);
     LBF_HIP(hipMemsetAsync(dcount_.get(), 0, sizeof(unsigned), ctx_->stream));
   }
@@ -1148,6 +1151,7 @@ bool History::update_impl(const GramArgs &g0, int want_dir, int iter, double dsi
     d.dots = ddots_.get();
     d.nb = int(cdiv(v_.n, dir_cols_per_block(v_.m, v_.n)));
     d.cols_done = dcount_.get();
+    d.kmat = dkmat_.get();
     {
       ProfScope ps(ctx_, PK_GRAM);
       dir_sweep(s, d);

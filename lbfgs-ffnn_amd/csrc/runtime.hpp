@@ -251,7 +251,7 @@ private:
   DevBuf<int> ist_;
   DevBuf<double> dstate_, part_, red_;
   // two-launch S-LBFGS update (dir.hip): partial rows, column sums, arrival counter
-  DevBuf<double> drows_, ddots_;
+  DevBuf<double> drows_, ddots_, dkmat_;
   DevBuf<unsigned> dcount_;
   bool dir_on_ = false;
   // unfused path: Gram sweep (transposed partials in part_) + column sums whose last block runs the step

@@ -182,12 +182,15 @@ def test_cfg4_slbfgs_first_pair_full_size(mnist, cfg4_epoch):
     Against the fp64 oracle on the same RNG stream: the iterate w_t after the 20 steps and u within
     ||d||/||ref|| <= 1e-4; ||s|| (pair_trace row 0's s.s) within 1e-4; s itself, a difference of two averages
     10 steps apart (||s|| ~ 1e-3 ||u||, so the iterates' rounding-level differences are ~1e-3 of it), within
-    1e-2; y.s within 5e-3. The finite difference cancels: u +- 1e-4 s moves a typical parameter by a few fp32
-    ulps, so the rounding of the two evaluation points alone moves y by ~1e-2 (the reference runs it in
-    fp64; the oracle's own fp32 run lands 5x off here, at a ReLU kink). The device's y is therefore also
+    1e-2. The finite difference cancels: u +- 1e-4 s moves a typical parameter by a few fp32 ulps, and a
+    ReLU pre-activation within ~1e-6 of zero on one of the 128 Hessian rows changes sign between the two
+    points or not depending on how they round (the step-0.01 NaN): y against the fp64 oracle's
+    y (fp64 points) is a knife edge, not a tolerance (round 5: 1.2e-2 on one kernel build, a 4.6e3 vs 0.47
+    y.y kink spike on the next, with w_t and s closer to fp64 on the second). The device's y is therefore
     checked at ITS OWN fp32 evaluation points: the fp64 oracle's gradients at fl32(u +- eps s), differenced
     and scaled as the device does, must match the device y to 5e-3 (what remains: the two fp32 batch
-    gradients' own rounding, amplified by the difference)."""
+    gradients' own rounding, amplified by the difference), and the device's y.s (pair_trace row 0) the y.s
+    of those fp64 values to 1e-3. The fp64 oracle's own y.s is printed beside them."""
     _, _, X64, Y64, _, _ = mnist
     r = cfg4_epoch
     dev, o64, o32 = r["p0"], r["o64"], r["o32"]
@@ -212,13 +215,14 @@ def test_cfg4_slbfgs_first_pair_full_size(mnist, cfg4_epoch):
     print(f"first pair y.s device {row[2]:.9e} fp64 {row64[2]:.9e} fp32 {row32[2]:.9e}; ||s|| device {ns:.9e} "
           f"fp64 {ns64:.9e}; y.y device {row[4]:.9e} fp64 {row64[4]:.9e}; device y vs fp64 at its fp32 points "
           f"{e_pts:.2e}")
+    ys_pts = float(np.dot(y_pts, s))
     assert int(row[0]) == int(row64[0]) == 0 and int(row[1]) == int(row64[1]) == 20
     for k in ("w_t", "u"):
         assert errs[k] <= 1e-4, (k, errs[k])
     assert abs(ns - ns64) <= 1e-4 * ns64, (ns, ns64)
     assert errs["s"] <= 1e-2, errs["s"]
-    assert abs(row[2] - row64[2]) <= 5e-3 * abs(row64[2]), (row[2], row64[2])
     assert e_pts <= 5e-3, e_pts
+    assert abs(row[2] - ys_pts) <= 1e-3 * abs(ys_pts), (row[2], ys_pts)
 
 
 def test_cfg4_slbfgs_one_epoch_full_size(ctx, pkg, O, mnist, cfg4_epoch):
@@ -253,6 +257,36 @@ def test_cfg4_slbfgs_one_epoch_full_size(ctx, pkg, O, mnist, cfg4_epoch):
     assert int(hist["accepted"][0]) == int(rec[0, 3]) == 10   # M = 10 live pairs after 22 candidates
     assert len(dv) == len(o) == 22
     assert r["info"].n_evals >= 2 * 234
+
+
+def test_cfg4_tanh_slbfgs_epoch_full_size(ctx, pkg, O, mnist):
+    """The cfg-4 S-LBFGS epoch on the same shape with tanh hidden layers (784-512-256-10; the reference's
+    activations include tanh, src/layer.hpp): no kinks, so the finite-difference pairs are smooth functions of
+    the iterates and the 234-step chain is not a knife edge; the same kernels, split-K plans and solver run
+    (the activation is an epilogue parameter). Against the fp64 oracle: the epoch loss within 1e-3, the same
+    live-pair count, every one of the 22 curvature candidates' y.s within 5e-2 of the oracle's (the FD's fp32
+    cancellation, test_cfg4_slbfgs_first_pair_full_size) and ||s|| within 1e-2. This is the full-size check a
+    rounding-level chaos cannot absorb."""
+    _, _, X64, Y64, X, Y = mnist
+    dims, acts = [784, 512, 256, 10], ["tanh", "tanh", "linear"]
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    P0 = host(P)
+    hist, _ = pkg.slbfgs_solve(net, P, X, Y, max_epochs=1, tol=0.0, lam=1e-4, pair_trace=64, **CFG4_KW)
+    onet = O.Net(dims, acts)
+    _, rec, _, pairs64 = onet.slbfgs(P0, X64, Y64, epochs=1, tol=0.0, M=10, L=10, b=256, bH=128, step=0.005,
+                                     lam=1e-4, pair_trace=64)
+    dv = hist["pairs"]
+    r = abs(hist["loss"][0] - rec[0, 0]) / abs(rec[0, 0])
+    eys = np.abs(dv[:, 2] - pairs64[:, 2]) / np.abs(pairs64[:, 2])
+    ess = np.abs(np.sqrt(dv[:, 3]) - np.sqrt(pairs64[:, 3])) / np.sqrt(pairs64[:, 3])
+    print(f"cfg4 tanh epoch loss: device {hist['loss'][0]:.8f} oracle fp64 {rec[0, 0]:.8f}: {r:.2e}; "
+          f"pairs: y.s max rel {eys.max():.2e}, ||s|| max rel {ess.max():.2e}")
+    assert len(dv) == len(pairs64) == 22
+    assert r <= 1e-3, r
+    assert int(hist["accepted"][0]) == int(rec[0, 3])
+    assert eys.max() <= 5e-2, eys
+    assert ess.max() <= 1e-2, ess
 
 
 def test_fd_hvp_matches_oracle_cfg4(ctx, pkg, O, mnist):
