@@ -1166,12 +1166,13 @@ void launch(hipStream_t s, const GemmDesc &d, const GemmDesc *d2 = nullptr) {
   }
 }
 
-// gemm_wsk_kernel's conditions: forward operand layout, 16-B quads everywhere, no A-from-slabs prologue.
-// LBF_NO_WSK=1 keeps the LDS-DMA loop (A/B measurements).
+// gemm_wsk_kernel's conditions: 16-B quads everywhere. Opt-in (LBF_WSK=1): in the library's GEMMs it measured
+// no faster than the LDS-DMA loop at the 8-rank shard's fused-head forward and 10 % slower on config 4's
+// minibatch GEMMs (profiles/r05/g/), although its main loop alone is 28 % faster (profiles/r05/c/loop32.txt).
 static bool wsk_ok(const GemmDesc &d) {
   static const bool off = [] {
-    const char *e = std::getenv("LBF_NO_WSK");
-    return e && std::atoi(e) != 0;
+    const char *e = std::getenv("LBF_WSK");
+    return !(e && std::atoi(e) != 0);
   }();
   const int kc = d.splits > 1 ? d.k_chunk : d.K;
   const bool base = !off && d.a_kc && d.K % 4 == 0 && d.lda % 4 == 0 && d.ldb % 4 == 0 && kc % 4 == 0 &&

@@ -28,7 +28,6 @@ namespace lbf {
 constexpr int COEF_MAXK = 128;
 
 struct HistSmem {
-  double cscr[(DIR_MAXM + 1) * DIR_MAXM + DIR_MAXM]; // compact_coef: R^-1 (row stride DIR_MAXM + 1), a vector
   double dots[6 * COEF_MAXK + 6];
   double gS_l[COEF_MAXK], gY_l[COEF_MAXK], rho_l[COEF_MAXK], alpha_l[COEF_MAXK], c_l[COEF_MAXK];
   int L0[COEF_MAXK + 1], L[COEF_MAXK + 1], inv0[COEF_MAXK + 1];
@@ -133,71 +132,6 @@ __device__ __forceinline__ void recur_fast(int k, int lane, const double *rho_l,
       }
     }
   }
-}
-
-// The two-loop coefficients of recur_fast (alpha = al0, alpha - beta = c0 for this lane's index) in compact form
-// (Byrd, Nocedal & Schnabel 1994; see slbfgs_kmat below for the algebra, exact for any rho): with R[i][j] =
-// s_i.y_j (i < j), R[i][i] = 1/rho_i, alpha = R^-1 gS (the backward recurrence) and alpha - beta =
-// R^-T (D alpha + gamma (YY alpha - gY)) (the forward one), D = diag(1/rho). Lane j computes column j of R^-1
-// by back substitution (no cross-lane dependency: the recurrences' k dependent v_readlane steps become
-// independent per-lane FMA chains), then three mat-vecs with one LDS exchange each. k <= KM; scr: (KM + 1) KM
-// + KM doubles of LDS; one wave.
-template <int KM>
-__device__ __forceinline__ void compact_coef(int k, int lane, const double *rho_l, const double *gS_l,
-                                             const double *gY_l, const double *sy, const double *yyl, double gamma,
-                                             double *scr, double &al0, double &c0) {
-  constexpr int LD = KM + 1; // odd stride: the row reads of R^-1 across lanes are conflict-free
-  double *rinv = scr, *vb = scr + KM * LD;
-  const int j = lane;
-  double x[KM]; // column j of R^-1
-#pragma unroll
-  for (int i = 0; i < KM; ++i) x[i] = 0.0;
-  if (j < k) {
-#pragma unroll
-    for (int i = KM - 1; i >= 0; --i) {
-      if (i == j) x[i] = rho_l[j];
-      if (i < j) {
-        double acc = 0.0;
-#pragma unroll
-        for (int l = i + 1; l < KM; ++l)
-          if (l <= j) acc += sy[i * k + l] * x[l];
-        x[i] = -rho_l[i] * acc;
-      }
-    }
-  }
-  if (j < KM)
-#pragma unroll
-    for (int i = 0; i < KM; ++i) rinv[i * LD + j] = x[i];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  double p = 0.0; // alpha_lane = (R^-1 gS)_lane
-  if (lane < k)
-#pragma unroll
-    for (int jj = 0; jj < KM; ++jj)
-      if (jj < k) p += rinv[lane * LD + jj] * gS_l[jj];
-  al0 = p;
-  if (lane < KM) vb[lane] = p;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  double q = 0.0; // (D alpha + gamma (YY alpha - gY))_lane
-  if (lane < k) {
-    double acc = 0.0;
-#pragma unroll
-    for (int l = 0; l < KM; ++l)
-      if (l < k) acc += yyl[lane * k + l] * vb[l];
-    q = p / rho_l[lane] + gamma * (acc - gY_l[lane]);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every lane has read vb
-  __builtin_amdgcn_wave_barrier();
-  if (lane < KM) vb[lane] = q;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  double c = 0.0; // (R^-T q)_lane = sum_l R^-1[l][lane] q_l: this lane's own column
-  if (lane < k)
-#pragma unroll
-    for (int l = 0; l < KM; ++l)
-      if (l < k) c += x[l] * vb[l];
-  c0 = c;
 }
 
 // The slbfgs gamma (s_lbfgs.hpp:119-126) from the newest pair's ys and yy.
@@ -529,10 +463,9 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
   if (k <= 64 && sy_t && yy_lds) {
     KTF(63);
     KTC(64);
-    if (k <= DIR_MAXM && h.compact)
-      compact_coef<DIR_MAXM>(k, lane, rho_l, gS_l, gY_l, sy, yyl, gamma, sm.cscr, al0, c0);
-    else
-      recur_fast(k, lane, rho_l, gS_l, gY_l, sy, syT, yyl, gamma, al0, c0);
+    // (the compact form of slbfgs_kmat computed per step in this block, lane j inverting column j of R by
+    // back substitution, measured 1.5-2 % slower at cfg 2 than these recurrences: profiles/r05/g/)
+    recur_fast(k, lane, rho_l, gS_l, gY_l, sy, syT, yyl, gamma, al0, c0);
   } else if (big) {
     // Two indices per lane (l0 = lane, l1 = lane + 64); the LDS operands of 8 steps are loaded ahead
     // of them, so each step is VALU + v_readlane only (the k <= 64 fast path, widened).

@@ -328,9 +328,6 @@ struct HistView {
   double *coef = nullptr; // [2*slots + 1]: cs (logical), cy (logical), cg
   double *scal = nullptr; // SC_N
   const int *abort = nullptr; // speculative execution flag (nullable)
-  // two-loop coefficients for k <= DIR_MAXM live pairs in compact form (hist_core.hpp compact_coef) instead of
-  // the readlane recurrences; LBF_NO_COMPACT=1 clears it (A/B)
-  int compact = 1;
 };
 
 struct GramArgs {

@@ -1064,7 +1064,6 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
   part_.resize(size_t(gram_nwg(n)) * gram_ncols(m));
   red_.resize(size_t(kGramFold) * gram_ncols(m));
   v_.m = m;
-  v_.compact = env_int("LBF_NO_COMPACT", 0) != 0 ? 0 : 1;
   v_.slots = slots;
   v_.n = n;
   v_.ld = ld;
