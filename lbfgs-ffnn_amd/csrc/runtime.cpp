@@ -175,6 +175,8 @@ void Mlp::plan(long long B) {
       if (2 * tiles32 <= cus) {
         L.ftile = TILE_32x128;
         fs = std::max(2LL, std::min(cus / tiles32, cdiv(L.in, 64))); // splits of >= 2 k-tiles
+        static const int fs_cap = env_int("LBF_FSPLIT_CAP", 0); // A/B of the split count (slab bytes vs depth)
+        if (fs_cap > 0) fs = std::min<long long>(fs, fs_cap);
       } else {
         fs = std::min(cdiv(384, ftiles), (long long)L.in / 128);
       }
