@@ -186,12 +186,15 @@ def test_cfg4_slbfgs_first_pair_full_size(mnist, cfg4_epoch):
     ReLU pre-activation within ~1e-6 of zero on one of the 128 Hessian rows changes sign between the two
     points or not depending on how they round (the step-0.01 NaN): y against the fp64 oracle's
     y (fp64 points) is a knife edge, not a tolerance (round 5: 1.2e-2 on one kernel build, a 4.6e3 vs 0.47
-    y.y kink spike on the next, with w_t and s closer to fp64 on the second). The device's y is therefore
-    checked at ITS OWN fp32 evaluation points: the fp64 oracle's gradients at fl32(u +- eps s), differenced
-    and scaled as the device does, must match the device y to 5e-3 (what remains: the two fp32 batch
-    gradients' own rounding, amplified by the difference), and the device's y.s (pair_trace row 0) the y.s
-    of those fp64 values to 1e-3. The fp64 oracle's own y.s is printed beside them."""
-    _, _, X64, Y64, _, _ = mnist
+    y.y kink spike on the next, with w_t and s closer to fp64 on the second). Even at the device's OWN fp32
+    points fl32(u +- eps s) the fp64 oracle's differenced gradients sit 5e-3 .. 7e-3 from the device's y on
+    successive builds (a pre-activation within fp32 rounding of zero is on either side of the kink in fp32
+    and fp64 arithmetic). So y is checked in its two non-chaotic parts: (a) the device's batch gradient at
+    each of the two points against the fp64 oracle at the same points, 1e-4 as every full-size gradient test;
+    (b) the device's y equal to its own two gradients differenced and scaled in fp32 (the pair sweep's
+    arithmetic), and y.s (pair_trace row 0) to their y.s. The fp64-at-the-device's-points deviation and the
+    fp64 oracle's own y.s are printed, with a 5e-2 sanity bound on the former."""
+    _, _, X64, Y64, X, Y = mnist
     r = cfg4_epoch
     dev, o64, o32 = r["p0"], r["o64"], r["o32"]
     names = ["w_t", "u", "s", "y"]
@@ -215,14 +218,28 @@ def test_cfg4_slbfgs_first_pair_full_size(mnist, cfg4_epoch):
     print(f"first pair y.s device {row[2]:.9e} fp64 {row64[2]:.9e} fp32 {row32[2]:.9e}; ||s|| device {ns:.9e} "
           f"fp64 {ns64:.9e}; y.y device {row[4]:.9e} fp64 {row64[4]:.9e}; device y vs fp64 at its fp32 points "
           f"{e_pts:.2e}")
-    ys_pts = float(np.dot(y_pts, s))
+    # the device's own batch gradients at the two points (same 128-row batch, 1/b_H scale and lambda as the
+    # solver's FD evaluations: the same plan, so the same launches)
+    hbd = torch.from_numpy(hb.astype(np.int32)).cuda()
+    gd = []
+    for w in (wp, wm):
+        Pw = torch.from_numpy(w.astype(np.float32)).cuda()
+        gd.append(r["net"].loss_grad(Pw, X, Y, idx=hbd, inv_scale=1.0 / 128, l2=1e-4)[1].cpu().numpy())
+    eg = [rel(gd[0].astype(np.float64), gp), rel(gd[1].astype(np.float64), gm)]
+    y_own = (gd[0] - gd[1]) * np.float32(1.0 / (2.0 * eps))
+    e_own = rel(dev[3], y_own.astype(np.float64))
+    ys_own = float(np.dot(y_own.astype(np.float64), s))
+    print(f"first pair: device batch gradients at u +- eps s vs fp64 {eg[0]:.2e} / {eg[1]:.2e}; device y vs its "
+          f"own gradients differenced {e_own:.2e}; y.s {row[2]:.9e} vs {ys_own:.9e}")
     assert int(row[0]) == int(row64[0]) == 0 and int(row[1]) == int(row64[1]) == 20
     for k in ("w_t", "u"):
         assert errs[k] <= 1e-4, (k, errs[k])
     assert abs(ns - ns64) <= 1e-4 * ns64, (ns, ns64)
     assert errs["s"] <= 1e-2, errs["s"]
-    assert e_pts <= 5e-3, e_pts
-    assert abs(row[2] - ys_pts) <= 1e-3 * abs(ys_pts), (row[2], ys_pts)
+    assert max(eg) <= 1e-4, eg
+    assert e_own <= 1e-6, e_own
+    assert abs(row[2] - ys_own) <= 1e-5 * abs(ys_own), (row[2], ys_own)
+    assert e_pts <= 5e-2, e_pts
 
 
 def test_cfg4_slbfgs_one_epoch_full_size(ctx, pkg, O, mnist, cfg4_epoch):
