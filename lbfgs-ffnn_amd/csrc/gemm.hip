@@ -65,7 +65,24 @@ struct GemmK {
   float *a_out;
   int gx, gy;   // this problem's tile grid (the grouped launch's grid is the larger of two)
   int group_z;  // grouped launch: GEMM planes of the first problem (the second's follow)
+  int xcd_swz;  // split-K: deal each split's tiles to one XCD (xcd_tile below)
 };
+
+// XCD-aware placement of a split-K GEMM's blocks (cdna_hip_programming.md §5.5 T1, bijective form): blocks
+// b and b + 8 are dealt to the same XCD (its own L2), so the GEMM blocks whose index e (past the side
+// planes) is congruent mod 8 get one contiguous range of logical tiles, ordered split-major. The tiles of
+// one split then share an L2: its A panel (the rows' input columns) is read once instead of once per
+// column tile, its B panel (the rows' delta) once instead of once per row tile and XCD (784-128-10 at 7500
+// rows: 77 MB of L2 misses per dW launch for 27 MB of operands, profiles/r05/i/pmc_7500.txt; 32 MB with this
+// placement, dW 24.8 -> 23.4 us, profiles/r05/k/). Speed only: every logical tile is computed by exactly one
+// block whatever the placement, so results do not change.
+__device__ __forceinline__ void xcd_tile(int e, int n, int gx, int gy, int &z, int &bx, int &by) {
+  const int q = n >> 3, r = n & 7, x = e & 7;
+  const int l = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (e >> 3);
+  bx = l % gx;
+  by = (l / gx) % gy;
+  z = l / (gx * gy);
+}
 
 // Side job (see GemmDesc): one 256-column group (four per lane) x 4 split stripes per block, fp64 in
 // split order. Side blocks hold their slots for the whole launch, so a block takes many columns: 32
@@ -879,8 +896,13 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
     gemm_side_job(g, reinterpret_cast<double *>(lds));
     return;
   }
-  glds_body<WM, WN, TM, TN, AKC, BKC, EPI, GATHER, NS, KW, ASUM>(g, lds, int(blockIdx.z) - g.side_planes,
-                                                               int(blockIdx.x), int(blockIdx.y));
+  int z = int(blockIdx.z) - g.side_planes, bx = int(blockIdx.x), by = int(blockIdx.y);
+  if (g.xcd_swz) {
+    const int plane = int(gridDim.x * gridDim.y);
+    xcd_tile(z * plane + by * int(gridDim.x) + bx, (int(gridDim.z) - g.side_planes) * plane, int(gridDim.x),
+             int(gridDim.y), z, bx, by);
+  }
+  glds_body<WM, WN, TM, TN, AKC, BKC, EPI, GATHER, NS, KW, ASUM>(g, lds, z, bx, by);
 }
 
 // Two GEMMs of one shape in one launch (the S-LBFGS minibatch's dW GEMMs of adjacent layers): planes
@@ -1085,6 +1107,14 @@ template <int BM, int BN> GemmK make_gemmk(const GemmDesc &d) {
   k.gx = int(gx);
   k.gy = int(gy);
   k.group_z = 0;
+  static const bool xcd_off = [] { // A/B switch: LBF_NO_XCD=1 keeps the default block placement
+    const char *e = std::getenv("LBF_NO_XCD");
+    return e && std::atoi(e) != 0;
+  }();
+  // dW GEMMs only (A = activations^T, mn-contiguous). The split-K FORWARD of a minibatch (config 4's
+  // 256 x 784 -> 512, 32 x 128 tiles, 8 splits) measured slower with it: 12.3 -> 13.2-13.7 us per launch for
+  // 10.2 -> 7.9 MB of traffic (every CU of an XCD then streams the same W chunk at once); profiles/r05/k/.
+  k.xcd_swz = !xcd_off && d.epi == EPI_STORE && d.splits > 1 && !d.a_kc;
   k.side_planes = (d.side_slab && d.side_count > 0) ? int(cdiv(cdiv(d.side_count, SIDE_COLS), gx * gy)) : 0;
   k.side_slab = d.side_slab;
   k.side_splits = d.side_splits;
