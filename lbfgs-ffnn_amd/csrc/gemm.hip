@@ -281,19 +281,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
     // the head runs on them. n0 == 0 (N <= BN).
     constexpr int QM = headc::qstrips(BN);
     headc::Smem hs = headc::carve(lds, g.N);
-    // the head tile runs on TB-row halves: a 32-row GEMM tile's ys / xr rows [BM, TB) are zero (rows past
-    // the tile contribute nothing: their delta is zero, and zero times the LDS left by an earlier kernel
-    // could be NaN)
+    // the head tile runs on TBR-row parts: 64-row halves, or the whole of a 32-row GEMM tile (the head's
+    // products over samples then run half their steps)
+    constexpr int TBR = BM < headc::TB ? BM : headc::TB;
     constexpr int YRA = BM > headc::TB ? BM : headc::TB;
     hs.xr = hs.ys + YRA * 16;
     const bool fold = g.head_fold >= 0; // uniform
     hpre.store(hs);
     if (g.head_fold > 0) hpre.store_fold(hs);
-    if constexpr (YRA > BM) {
-      for (int e = threadIdx.x; e < (YRA - BM) * 16; e += 256 * KW) hs.ys[BM * 16 + e] = 0.0f;
-      if (g.head_fold > 0)
-        for (int e = threadIdx.x; e < (YRA - BM) * headc::XLD; e += 256 * KW) hs.xr[BM * headc::XLD + e] = 0.0f;
-    }
     KT(26);
     KTB(2);
     headc::f32x4 cw[QM];
@@ -316,15 +311,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
       fa.c[j] = (headc::f32x4){0.f, 0.f, 0.f, 0.f};
       fa.db[j] = 0.0f;
     }
-    for (int half = 0; half < (BM + headc::TB - 1) / headc::TB; ++half) {
-      const long long b0 = (long long)m0 + half * headc::TB;
-      const int rows_tile = min(headc::TB, BM - half * headc::TB);
+    for (int half = 0; half < (BM + TBR - 1) / TBR; ++half) {
+      const long long b0 = (long long)m0 + half * TBR;
+      const int rows_tile = min(TBR, BM - half * TBR);
       const int rows = int(min((long long)rows_tile, (long long)g.M - b0));
       if (rows <= 0) break;
-      ta.ys = hs.ys + half * headc::TB * 16;
-      ta.xr = hs.xr + half * headc::TB * headc::XLD;
+      ta.ys = hs.ys + half * TBR * 16;
+      ta.xr = hs.xr + half * TBR * headc::XLD;
       if (half == 0) lds_barrier(); // hb (read below) written by hpre.store
-      for (int e = threadIdx.x; e < (headc::TB - rows_tile) * hs.Hp; e += 256 * KW) { // rows the tile lacks
+      for (int e = threadIdx.x; e < (TBR - rows_tile) * hs.Hp; e += 256 * KW) { // rows the tile lacks
         const int r = rows_tile + e / hs.Hp, c = e % hs.Hp;
         hs.As[r * hs.LDA + c] = 0.0f;
       }
@@ -336,13 +331,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
           for (int tn = 0; tn < TN; ++tn) {
             const int col = wn * TN * 32 + tn * 32 + li;
             const int local0 = wm * TM * 32 + tm * 32;
-            if (kgrp == 0 && local0 / headc::TB == half && col < hs.Hp) { // the tile may be wider than Hp
+            if (kgrp == 0 && local0 / TBR == half && col < hs.Hp) { // the tile may be wider than Hp
               const float bn = hs.hb[col];
               const bool in = col < g.N;
 #pragma unroll
               for (int r = 0; r < 16; ++r) {
                 const int local = local0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                hs.As[(local % headc::TB) * hs.LDA + col] = in ? act_c<A>(acc[tm][tn][r] + bn) : 0.0f;
+                hs.As[(local % TBR) * hs.LDA + col] = in ? act_c<A>(acc[tm][tn][r] + bn) : 0.0f;
               }
             }
           }
@@ -355,8 +350,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
       lds_barrier();
       KT(28 + 2 * half);
       KTB(3 + 2 * half);
-      if (fold) headc::tile<(KW > 1), QM, true>(hs, ta, b0, rows, cw, sse, fa);
-      else headc::tile<(KW > 1), QM, false>(hs, ta, b0, rows, cw, sse, fa);
+      if (fold) headc::tile<(KW > 1), QM, true, TBR>(hs, ta, b0, rows, cw, sse, fa);
+      else headc::tile<(KW > 1), QM, false, TBR>(hs, ta, b0, rows, cw, sse, fa);
       KT(29 + 2 * half);
       KTB(4 + 2 * half);
     }

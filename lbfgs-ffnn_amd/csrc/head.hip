@@ -88,7 +88,7 @@ struct WRegs {
       if (e < n) {
         const int i = e / Out, o = e - i * Out;
         s.Wt[o * s.LDA + i] = w[j];
-        s.Wr[i * 16 + o] = w[j];
+        s.Wr[i * 16 + ocol(o)] = w[j];
       }
     }
     if (t < HMAX_OUT) s.bias[t] = t < Out ? bias : 0.0f;

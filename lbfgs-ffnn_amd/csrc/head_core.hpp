@@ -44,6 +44,12 @@ __device__ __forceinline__ int round64(int x) { return (x + 63) & ~63; }
 constexpr int XLD = 20;                    // folded input-column rows [yrows][XLD]: conflict-free b32 reads
 constexpr int FOLD_MAX = 16;               // input columns a GEMM epilogue can fold (one 16-wide strip)
 
+// Column order of the 16 (padded) outputs in Dz and Wr: output o sits at column ocol(o). A 16-B read of
+// columns 4g..4g+3 then gives lane group g the outputs 4kk + g (kk = 0..3), so step kk of the delta product's
+// MFMA chain consumes outputs 4kk .. 4kk+3 and the chain stops after ceil(Out / 4) steps (Out = 10: three of
+// four; the skipped steps multiplied zeros).
+__host__ __device__ constexpr int ocol(int o) { return (o & 3) * 4 + (o >> 2); }
+
 // LDS carve-up (floats): As [TB][LDA] | Wt [16][LDA] | Wr [Hp][16] | Dz [TB][LDZ] | bias [16] | red [8]
 // The GEMM epilogue appends hb [Hp] (the hidden layer's bias), ys [yrows][16] (the block's targets)
 // and xr [yrows][XLD] (the input columns folded into the epilogue, see TileArgs::fold).
@@ -86,7 +92,7 @@ __device__ inline void stage_w(const Smem &s, const float *P, int Out) {
     const int i = e / Out, o = e - i * Out;
     const float v = P[e];
     s.Wt[o * s.LDA + i] = v;
-    s.Wr[i * 16 + o] = v;
+    s.Wr[i * 16 + ocol(o)] = v;
   }
   if (t < HMAX_OUT) s.bias[t] = t < Out ? P[(long long)s.H * Out + t] : 0.0f;
   __syncthreads();
@@ -156,7 +162,7 @@ struct EpiPrefetch {
       const int e = t + j * NT, o = e / HN, i = e % HN;
       if (e < 16 * HN && i < s.Hp) {
         s.Wt[o * s.LDA + i] = w[j];
-        s.Wr[i * 16 + o] = w[j];
+        s.Wr[i * 16 + ocol(o)] = w[j];
       }
     }
     if (t < s.Hp) s.hb[t] = hb;
@@ -203,17 +209,22 @@ struct HRange {
 // QM: dW strips per wave (>= ceil(ceil((H+1)/16)/4)); strips past H are skipped (wave-uniform).
 // Barriers here only order LDS (lds_barrier): a __syncthreads would also wait for the delta stores.
 // FOLD: accumulate the fold (TileArgs::xr / nfold) into fa; needs H <= 128 (one pass of column strips).
-template <bool EXTRA_WAVES, int QM, bool FOLD> // EXTRA_WAVES: waves >= 4 only join barriers
+// TBR: samples the tile holds (64, or 32 for a 32-row GEMM tile: the products over samples then run half
+// their steps; rows >= TBR of As / Dz / ys / xr are neither read nor needed).
+template <bool EXTRA_WAVES, int QM, bool FOLD, int TBR = TB> // EXTRA_WAVES: waves >= 4 only join barriers
 __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int rows, f32x4 (&cw)[QM], double &sse,
                             FoldAcc &fa, const HRange &hr = HRange()) {
+  static_assert(TBR == 64 || TBR == 32, "head tile of 64 or 32 samples");
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int r0 = wave * 16, LDA = s.LDA, H = s.H;
   const bool active = !EXTRA_WAVES || wave < 4;
+  const bool zrows = active && wave < TBR / 16; // wave-uniform: this wave's 16 samples are in the tile
+  const int dzc = ocol(li);                      // this lane's output column in Dz (see ocol)
   KT(34);
   // ---- forward: Z strip (16 samples x 16 outputs) of this wave, two interleaved chains ----
   f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  for (int kc = 0; active && kc < s.Hp; kc += 32) { // 32 k per round: 8 steps, two chains
+  for (int kc = 0; zrows && kc < s.Hp; kc += 32) { // 32 k per round: 8 steps, two chains
     float af[8], bf[8];
     const int kh = kc & 63, k64 = kc & ~63; // lane group g consumes k = k64 + 16 g + s, s = kh/4 .. kh/4 + 7
     const float *pa = s.As + (r0 + li) * LDA + k64 + g * 16 + (kh >> 2);
@@ -237,7 +248,7 @@ __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int 
   acc += acc1;
   KT(35);
   // ---- loss and dZ (lane: samples r0 + g*4 + r, output o = li); targets loaded as one batch ----
-  if (active) {
+  if (zrows) {
     float yv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -260,7 +271,7 @@ __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int 
           sse += double(d) * double(d);
           dz = d * dact_c<A>(av) * a.sc;
         }
-        s.Dz[row * LDZ + li] = dz;
+        s.Dz[row * LDZ + dzc] = dz;
       }
     });
   }
@@ -270,23 +281,33 @@ __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int 
   // Step k of lane group g takes sample b = (k & 3) + 4g + 16(k >> 2): the four groups of a step read
   // rows 4 apart (bank offset 16 with LDA = 4 mod 64, 80 with LDZ = 20), so the reads are
   // conflict-free. Every LDS read is unconditional (clamped column) and all are issued before the
-  // MFMA chains; strips past the bias row are skipped wave-uniformly.
+  // MFMA chains; strips past the bias row are skipped wave-uniformly. A strip holding only the bias row
+  // (H % 16 == 0) is a column sum of dZ on the VALU: sixteen MFMAs for one useful row otherwise.
   if (active) {
 #pragma unroll
     for (int q = 0; q < QM; ++q) {
       const int st = hr.st0 + wave + 4 * q;
       if (st * 16 > H || st >= hr.st1) continue; // wave-uniform
+      if (st * 16 == H) { // db[o] += sum_b dZ[b][o]: lane group g sums samples b = g mod 4, then the groups
+        float d = 0.0f;
+#pragma unroll
+        for (int b = 0; b < TBR; b += 4) d += s.Dz[(b + g) * LDZ + dzc];
+        d += __shfl_xor(d, 16);
+        d += __shfl_xor(d, 32);
+        if (g == 0) cw[q][0] += d;
+        continue;
+      }
       const int ic = st * 16 + li;
       const int icc = ic < H ? ic : 0;
       const bool bias_strip = st * 16 + 15 >= H; // wave-uniform
       f32x4 c = cw[q];
 #pragma unroll 1
-      for (int k0 = 0; k0 < 16; k0 += 4) { // four steps of loads in flight, then their MFMAs
+      for (int k0 = 0; k0 < TBR / 4; k0 += 4) { // four steps of loads in flight, then their MFMAs
         float av[4], dz[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int b = k + 4 * g + k0 * 4; // (k & 3) + 4g + 16 (k >> 2) for step k0 + k
-          dz[k] = s.Dz[b * LDZ + li];
+          dz[k] = s.Dz[b * LDZ + dzc];
           av[k] = s.As[b * LDA + icc];
         }
 #pragma unroll
@@ -303,8 +324,10 @@ __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int 
   // Wave w takes the column strips 2w, 2w+1 (+8, +9, ... for H > 128) over all TB rows, one 16-row
   // strip at a time (two MFMA chains of 4 each). Lanes li of a row write 64 contiguous bytes.
   // Strip cb+1 may pass H: Wr's zero rows (Hp >= 16 (cb + 2)) make it zero and nothing is stored.
+  // The k = output dimension runs ceil(Out / 4) MFMA steps (Dz / Wr column order ocol).
   if (a.delta && active) {
     const int ncs = (H + 15) >> 4;
+    const int nks = (a.Out + 3) >> 2; // uniform
     with_act(a.act_prev, [&](auto AC) __attribute__((always_inline)) {
       constexpr int A = decltype(AC)::value;
       for (int cb = hr.cb0 + 2 * wave; cb < ncs && cb < hr.cb1; cb += 8) { // wave-uniform; one pass when H <= 128
@@ -312,7 +335,7 @@ __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int 
         const f32x4 wb1 = *reinterpret_cast<const f32x4 *>(s.Wr + ((cb + 1) * 16 + li) * 16 + g * 4);
         const int col = cb * 16 + li;
 #pragma unroll 1
-        for (int rs = 0; rs < 4; ++rs) {
+        for (int rs = 0; rs < TBR / 16; ++rs) {
           const f32x4 da = *reinterpret_cast<const f32x4 *>(s.Dz + (rs * 16 + li) * LDZ + g * 4);
           float ap0[4], ap1[4], xa[4];
 #pragma unroll
@@ -325,8 +348,10 @@ __device__ inline void tile(const Smem &s, const TileArgs &a, long long b0, int 
           f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(da[k], wb0[k], c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(da[k], wb1[k], c1, 0, 0, 0);
+            if (k < nks) { // uniform
+              c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(da[k], wb0[k], c0, 0, 0, 0);
+              c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(da[k], wb1[k], c1, 0, 0, 0);
+            }
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {

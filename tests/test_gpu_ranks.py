@@ -222,11 +222,11 @@ def test_ranks_empty_share_lbfgs(ctx, pkg):
 @pytest.mark.parametrize("world,kw", [
     (2, dict(M=5, L=4, b=32, b_H=16)),
     (3, dict(M=5, L=4, b=32, b_H=16)),
-    # b < world: one rank's slice of every minibatch and Hessian batch is empty (at 0.02, b = 1 diverges to
-    # NaN on both routes; one-row SVRG steps with FD pairs on one-row Hessian batches cross ReLU kinks at the
-    # rounding level: one epoch of 64 steps, tol 5 %; in a second epoch the routes part chaotically, 13.6 % on
-    # round 5's build against < 5 % on round 4's)
-    (2, dict(M=5, L=4, b=1, b_H=1, step=0.002, rtol=5e-2, max_epochs=1)),
+    # b < world: one rank's slice of every minibatch and Hessian batch is empty. With ReLU, one-row SVRG steps
+    # with FD pairs on one-row Hessian batches cross kinks at the rounding level and the two routes part
+    # chaotically (one epoch: < 5 % on round 4's build, 24.6 % on round 5's head epilogue, which only
+    # re-rounds); tanh has no kinks, so the same empty-slice code path is compared at a fixed bound
+    (2, dict(M=5, L=4, b=1, b_H=1, step=0.002, rtol=1e-2, max_epochs=1, acts=["tanh", "linear"])),
     (2, dict(M=5, L=4, b=32, b_H=1, hvp_exact=1)),  # exact HVP with b_H < world
     # replicated inner steps: identical chains on every rank, the full-batch gradient sharded
     (2, dict(M=5, L=4, b=32, b_H=16, dp_mode="replicated")),
@@ -234,10 +234,10 @@ def test_ranks_empty_share_lbfgs(ctx, pkg):
     (4, dict(M=5, L=4, b=32, b_H=1, hvp_exact=1, dp_mode="replicated")),
 ])
 def test_ranks_slbfgs_equals_single(ctx, pkg, world, kw):
-    dims, acts, N = [784, 16, 10], ["relu", "linear"], 512 if kw["b"] > 1 else 64
+    kw = dict(kw)
+    dims, acts, N = [784, 16, 10], kw.pop("acts", ["relu", "linear"]), 512 if kw["b"] > 1 else 64
     Xh, Yh = pkg.synth_mnist(N)
     X, Y = dev(Xh), dev(Yh)
-    kw = dict(kw)
     rtol = kw.pop("rtol", 1e-3)
     args = dict(step=0.02, max_epochs=2, tol=0.0, lam=1e-4, dp_mode="sliced")
     args.update(kw)
@@ -299,34 +299,74 @@ def test_ranks_cfg4_epoch(ctx, pkg, dp_mode):
     """BASELINE cfg 4 (784-512-256-10, N = 60000, b = 256, b_H = 128, L = M = 10) for one epoch at world 2
     against the single route. Sliced: the twin's anchor gradients ahead and ONE all-reduce per [g(w_t) | g(w)]
     block. Replicated: every rank runs the whole chain, the full-batch gradient at the anchor is sharded.
-    Same number of live curvature pairs, epoch loss within 5 % of the single route (the shard sums of the
-    full-batch gradient are added in another order, so the 234-step chain starts from a mu that differs at
-    the rounding level; tests/test_gpu_fullsize.py), ranks bitwise identical."""
+
+    The two routes add the full-batch gradient's shard sums (and, sliced, every minibatch gradient) in
+    another order, so they start apart at the rounding level; past the first finite-difference pairs the
+    ReLU epoch is chaotic at that level (tests/test_gpu_fullsize.py: re-rounding the head epilogue alone moved
+    the single route's epoch loss by 3.4 %, and this comparison from 0.9 % to 5.7 %). The fixed-bound checks
+    are therefore the non-chaotic window and the smooth network: the iterate after the first 20 (pure SVRG)
+    steps and their average u, the first pair's s (pair_trace snapshot), within 1e-4 / 1e-4 / 1e-2 of the
+    single route; the same live-pair count; ranks bitwise identical; and the same epoch with tanh hidden
+    layers within a fixed 2 % (test_ranks_cfg4_tanh_epoch). The ReLU epoch loss is printed beside them."""
     dims, acts, N, world = [784, 512, 256, 10], ["relu", "relu", "linear"], 60000, 2
     Xh, Yh = pkg.synth_mnist(N)
     X, Y = dev(Xh), dev(Yh)
-    args = dict(M=10, L=10, b=256, b_H=128, step=0.005, max_epochs=1, tol=0.0, lam=1e-4, dp_mode=dp_mode)
+    args = dict(M=10, L=10, b=256, b_H=128, step=0.005, tol=0.0, lam=1e-4, dp_mode=dp_mode)
     net1 = pkg.Mlp(ctx, dims, acts)
     P0 = net1.init_params(123, "cpu")
-    P1 = P0.clone()
-    h1, i1 = pkg.slbfgs_solve(net1, P1, X, Y, **args)
+    run1 = pkg.SlbfgsRun(net1, P0.clone(), X, Y, pair_trace=64, **args)
+    i1 = run1.iterate(1)
+    h1, p01 = run1.hist.as_dict(), [host(t) for t in run1.pair0()]
+    run1.close()
 
     def body(r, c):
         net = pkg.Mlp(c, dims, acts)
         P = P0.clone()
-        h, info = pkg.slbfgs_solve(net, P, X, Y, **args)
-        return h, P, info.n_rows
+        run = pkg.SlbfgsRun(net, P, X, Y, pair_trace=64, **args)
+        info = run.iterate(1)
+        out = run.hist.as_dict(), [host(t) for t in run.pair0()], info.n_rows, P
+        run.close()
+        return out
 
     res = run_ranks(pkg, world, body)
-    assert torch.equal(res[0][1], res[1][1])
-    h = res[0][0]
+    assert torch.equal(res[0][3], res[1][3])
+    h, p0 = res[0][0], res[0][1]
     assert np.isfinite(h["loss"][0])
     assert h["accepted"][0] == h1["accepted"][0]
+    e = [rel(p0[i], p01[i]) for i in range(3)]
     d = abs(h["loss"][0] - h1["loss"][0]) / abs(h1["loss"][0])
-    print(f"cfg4 epoch, world 2 {dp_mode}: loss {h['loss'][0]:.6f} single route {h1['loss'][0]:.6f}: {d:.4f}")
-    assert d <= 0.05, d
+    print(f"cfg4 epoch, world 2 {dp_mode}: first pair w_t {e[0]:.2e} u {e[1]:.2e} s {e[2]:.2e} from the single "
+          f"route; epoch loss {h['loss'][0]:.6f} single route {h1['loss'][0]:.6f}: {d:.4f}")
+    assert e[0] <= 1e-4 and e[1] <= 1e-4 and e[2] <= 1e-2, e
     if dp_mode == "sliced":
         assert res[0][2] + res[1][2] == i1.n_rows  # the ranks' slices partition the single route's rows
     else:  # every rank evaluates every minibatch row; the two full-batch evaluations are split
         full = 2 * N
         assert res[0][2] + res[1][2] == 2 * (i1.n_rows - full) + full
+
+
+@pytest.mark.parametrize("dp_mode", ["sliced", "replicated"])
+def test_ranks_cfg4_tanh_epoch(ctx, pkg, dp_mode):
+    """The cfg-4 epoch at world 2 on the smooth network (tanh hidden layers: no kinks for the finite
+    differences to cross): epoch loss within a fixed 2 % of the single route, the same live-pair count."""
+    dims, acts, N, world = [784, 512, 256, 10], ["tanh", "tanh", "linear"], 60000, 2
+    Xh, Yh = pkg.synth_mnist(N)
+    X, Y = dev(Xh), dev(Yh)
+    args = dict(M=10, L=10, b=256, b_H=128, step=0.005, max_epochs=1, tol=0.0, lam=1e-4, dp_mode=dp_mode)
+    net1 = pkg.Mlp(ctx, dims, acts)
+    P0 = net1.init_params(123, "cpu")
+    h1, _ = pkg.slbfgs_solve(net1, P0.clone(), X, Y, **args)
+
+    def body(r, c):
+        net = pkg.Mlp(c, dims, acts)
+        P = P0.clone()
+        h, _ = pkg.slbfgs_solve(net, P, X, Y, **args)
+        return h, P
+
+    res = run_ranks(pkg, world, body)
+    assert torch.equal(res[0][1], res[1][1])
+    h = res[0][0]
+    d = abs(h["loss"][0] - h1["loss"][0]) / abs(h1["loss"][0])
+    print(f"cfg4 tanh epoch, world 2 {dp_mode}: loss {h['loss'][0]:.8f} single route {h1['loss'][0]:.8f}: {d:.2e}")
+    assert h["accepted"][0] == h1["accepted"][0]
+    assert d <= 2e-2, d
