@@ -600,7 +600,44 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
     }
     const int dev = ctx_->device;
     tw_.reset(new TaskFifo([dev]() { LBF_HIP(hipSetDevice(dev)); }));
+    // the epoch-end full-batch evaluation ahead (see fnet_): single rank
+    if (!ctx_->dp() && env_int("LBF_NO_FULL_AHEAD", 0) == 0) {
+      fctx_.reset(new Ctx());
+      fctx_->device = ctx_->device;
+      fctx_->cus = ctx_->cus;
+      if (greatest < least) LBF_HIP(hipStreamCreateWithPriority(&fctx_->stream, hipStreamNonBlocking, least));
+      else LBF_HIP(hipStreamCreateWithFlags(&fctx_->stream, hipStreamNonBlocking));
+      fctx_->own_stream = true;
+      fctx_->prof.on = ctx_->prof.on;
+      fctx_->prof.only = ctx_->prof.only;
+      fctx_->prof.every = ctx_->prof.every;
+      fnet_.reset(new Mlp(fctx_.get(), int(acts.size()), dims.data(), acts.data()));
+      mu_next_.resize(ng);
+      fscal_.resize(SC_N);
+      LBF_HIP(hipMemsetAsync(fscal_.get(), 0, SC_N * sizeof(double), ctx_->stream));
+      LBF_HIP(hipEventCreateWithFlags(&ev_anchor_, hipEventDisableTiming | event_release_flags()));
+      LBF_HIP(hipEventCreateWithFlags(&ev_full_, hipEventDisableTiming | event_release_flags()));
+    }
   }
+}
+
+int SlbfgsSolver::full_ahead_step(const EpochDraw &d) const {
+  if (!fnet_ || d.pick < 0) return -2;
+  // w_history at the epoch's end holds iterates w_{m+1-W} .. w_m (w_0: the anchor copy, w_{t+1}: after step t),
+  // W = min(m + 1, L + 1) entries, the same count draw_epoch drew the pick over (s_lbfgs.hpp:265-266)
+  const int m_inner = int(std::max(1LL, N_ / prm_.b));
+  const int W = std::min(m_inner + 1, prm_.L + 1);
+  const int j = m_inner + 1 - W + d.pick;
+  return j - 1;
+}
+
+void SlbfgsSolver::post_full(const float *anchor) {
+  hipStream_t s = ctx_->stream;
+  LBF_HIP(hipEventRecord(ev_anchor_, s));
+  LBF_HIP(hipStreamWaitEvent(fctx_->stream, ev_anchor_, 0));
+  fnet_->loss_grad(anchor, mu_next_.get(), X_, Y_, nullptr, N_, 1.0 / double(N_), prm_.lambda, nullptr, fscal_.get());
+  LBF_HIP(hipEventRecord(ev_full_, fctx_->stream));
+  full_posted_ = true;
 }
 
 long long SlbfgsSolver::twin_post(std::function<void()> f) {
@@ -624,6 +661,9 @@ SlbfgsSolver::~SlbfgsSolver() {
     if (ev_g2_[i]) (void)hipEventDestroy(ev_g2_[i]);
     if (ev_free_[i]) (void)hipEventDestroy(ev_free_[i]);
   }
+  if (fctx_) (void)hipStreamSynchronize(fctx_->stream);
+  if (ev_anchor_) (void)hipEventDestroy(ev_anchor_);
+  if (ev_full_) (void)hipEventDestroy(ev_full_);
 }
 
 void SlbfgsSolver::reduce_pair(const float *wa, const float *wb, float *gab, double inv_scale) {
@@ -750,10 +790,12 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
   LBF_HIP(hipMemcpyAsync(wt_.get(), w_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
   wh_head_ = 0;
   wh_count_ = 0;
+  const int full_at = full_ahead_step(d);
   {
     const int slot = wh_push_slot();
     LBF_HIP(hipMemcpyAsync(wh_.get() + slot * ld, wt_.get(), size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice,
                            s));
+    if (full_at == -1) post_full(wh_.get() + slot * ld);
   }
   // The minibatch gradients at the anchor w (fixed for the epoch, and independent of the iterates) run one
   // step ahead on the twin stream: step t's evaluation at w_t and its direction on the context stream then
@@ -873,6 +915,7 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
     h0 = tick();
     if (!twin_free) LBF_HIP(hipEventRecord(ev_free_[t & 1], ctx_->stream)); // block t & 1 read (v formed)
     tock(2, h0);
+    if (t == full_at) post_full(wh_.get() + slot * ld); // the picked iterate w_{t+1} now exists
     h0 = tick();
     if (t > 0 && t % L == 0) {
       int slots[64];
@@ -923,11 +966,12 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
   const long long ld = round4(n_);
   const int nr = ctx_->nranks, rk = ctx_->rank;
   const int m_inner = int(std::max(1LL, N_ / prm_.b));
-  if (tctx_) { // the benchmark's section timing covers the twin's launches too (settings may change per call)
-    tctx_->prof.on = ctx_->prof.on;
-    tctx_->prof.only = ctx_->prof.only;
-    if (tctx_->prof.every != ctx_->prof.every) tctx_->prof.seen = 0;
-    tctx_->prof.every = ctx_->prof.every;
+  for (Ctx *c : {tctx_.get(), fctx_.get()}) { // the benchmark's section timing covers the side streams' launches
+    if (!c) continue;                          // too (settings may change per call)
+    c->prof.on = ctx_->prof.on;
+    c->prof.only = ctx_->prof.only;
+    if (c->prof.every != ctx_->prof.every) c->prof.seen = 0;
+    c->prof.every = ctx_->prof.every;
   }
   if (!started_) {
     LBF_HIP(hipMemcpyAsync(w_.get(), user_params_, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -1007,7 +1051,16 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
     LBF_HIP(hipMemcpyAsync(w_.get(), anchor, size_t(n_) * sizeof(float), hipMemcpyDeviceToDevice, s));
     if (repl_ && nr > 1) replica_fingerprints(); // compared after read(): no extra host wait
     // recorder (s_lbfgs.hpp:274-284): full loss and gradient at the new anchor == next epoch's mu
-    eval_full(w_.get(), mu_.get());
+    if (full_posted_) { // evaluated ahead on the third stream (fnet_): join, take its gradient and status words
+      LBF_HIP(hipStreamWaitEvent(s, ev_full_, 0));
+      std::swap(mu_, mu_next_);
+      double *hsc = hist_.scal();
+      LBF_HIP(hipMemcpyAsync(hsc + SC_LOSS, fscal_.get() + SC_LOSS, 2 * sizeof(double), hipMemcpyDeviceToDevice, s));
+      LBF_HIP(hipMemcpyAsync(hsc + SC_WW, fscal_.get() + SC_WW, 2 * sizeof(double), hipMemcpyDeviceToDevice, s));
+      full_posted_ = false;
+    } else {
+      eval_full(w_.get(), mu_.get());
+    }
     read();
     if (repl_ && nr > 1) replica_check();
     mu_valid_ = true;
@@ -1030,6 +1083,10 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
   if (tctx_) {
     LBF_HIP(hipStreamSynchronize(tctx_->stream));
     tctx_->prof.merge_into(ctx_->prof);
+  }
+  if (fctx_) {
+    LBF_HIP(hipStreamSynchronize(fctx_->stream));
+    fctx_->prof.merge_into(ctx_->prof);
   }
   return iters_ - done0;
 }
@@ -1097,8 +1154,8 @@ void SlbfgsSolver::info(lbf_solve_info *out) const {
   if (!out) return;
   std::memset(out, 0, sizeof(*out));
   out->iterations = iters_;
-  out->n_evals = net_->evals() - evals0_ + (tnet_ ? tnet_->evals() : 0);
-  out->n_rows = net_->rows() - rows0_ + (tnet_ ? tnet_->rows() : 0);
+  out->n_evals = net_->evals() - evals0_ + (tnet_ ? tnet_->evals() : 0) + (fnet_ ? fnet_->evals() : 0);
+  out->n_rows = net_->rows() - rows0_ + (tnet_ ? tnet_->rows() : 0) + (fnet_ ? fnet_->rows() : 0);
   out->final_loss = last_loss_;
   out->final_grad_norm = last_gnorm_;
 }

@@ -270,6 +270,22 @@ private:
   DevBuf<float> ganc_;
   std::vector<hipEvent_t> ev_anc_;
   hipEvent_t ev_g2_[2] = {nullptr, nullptr}, ev_free_[2] = {nullptr, nullptr}; // anchor gradients ahead (twin)
+  // The epoch-end full-batch evaluation at the next anchor (s_lbfgs.hpp:265-284: the recorder's loss and
+  // gradient, which are the next epoch's mu) started as soon as the picked iterate exists: the pick is drawn
+  // with the epoch's index lists, before the epoch runs, and the picked entry of w_history stays in its ring
+  // slot to the end. A third workspace of the network on its own stream evaluates it beside the epoch's last
+  // inner steps into mu_next_ and its own status block; the context stream joins it where the ordered route
+  // evaluated. Same launches on the same inputs: bitwise the ordered route. Single rank only (data parallel
+  // keeps the ordered, sharded evaluation and its fingerprint check); LBF_NO_FULL_AHEAD=1 turns it off.
+  std::unique_ptr<Ctx> fctx_;
+  std::unique_ptr<Mlp> fnet_;
+  DevBuf<float> mu_next_;
+  DevBuf<double> fscal_;
+  hipEvent_t ev_anchor_ = nullptr, ev_full_ = nullptr;
+  bool full_posted_ = false;
+  // inner step after whose combine the picked iterate exists (-1: the epoch's start, -2: no pick)
+  int full_ahead_step(const EpochDraw &d) const;
+  void post_full(const float *anchor);
 };
 
 // CudaGD / CudaSGD (src/cuda/gd.cuh:38-106, sgd.cuh:50-153) on the MLP; return the iterations done.

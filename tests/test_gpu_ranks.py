@@ -222,11 +222,12 @@ def test_ranks_empty_share_lbfgs(ctx, pkg):
 @pytest.mark.parametrize("world,kw", [
     (2, dict(M=5, L=4, b=32, b_H=16)),
     (3, dict(M=5, L=4, b=32, b_H=16)),
-    # b < world: one rank's slice of every minibatch and Hessian batch is empty. With ReLU, one-row SVRG steps
-    # with FD pairs on one-row Hessian batches cross kinks at the rounding level and the two routes part
-    # chaotically (one epoch: < 5 % on round 4's build, 24.6 % on round 5's head epilogue, which only
-    # re-rounds); tanh has no kinks, so the same empty-slice code path is compared at a fixed bound
-    (2, dict(M=5, L=4, b=1, b_H=1, step=0.002, rtol=1e-2, max_epochs=1, acts=["tanh", "linear"])),
+    # b < world: one rank's slice of every minibatch and Hessian batch is empty. The finite-difference pair of
+    # a one-row Hessian batch amplifies the two routes' rounding-level differences by ~1/(2 eps) (with ReLU
+    # kinks, chaotically: one epoch < 5 % apart on round 4's build, 24.6 % on round 5's re-rounded head; with
+    # tanh still 2.5 %), so the empty-slice path is compared on the smooth network with the exact HVP pairs,
+    # at the default fixed bound
+    (2, dict(M=5, L=4, b=1, b_H=1, step=0.002, hvp_exact=1, acts=["tanh", "linear"])),
     (2, dict(M=5, L=4, b=32, b_H=1, hvp_exact=1)),  # exact HVP with b_H < world
     # replicated inner steps: identical chains on every rank, the full-batch gradient sharded
     (2, dict(M=5, L=4, b=32, b_H=16, dp_mode="replicated")),

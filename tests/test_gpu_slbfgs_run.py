@@ -89,3 +89,28 @@ def test_profiler_times_sampled_launches(ctx, pkg):
     # per epoch: 2 minibatch evaluations per inner step (w_t and the anchor on the twin), the FD pairs, the
     # full-batch gradient; 1024 / 64 = 16 inner steps
     assert 2 * 2 * 16 <= n <= 2 * (2 * 16 + 2 * 4 + 2), n
+
+
+@pytest.mark.parametrize("L,N", [(4, 1024), (10, 640)])
+def test_full_ahead_equals_ordered(ctx, pkg, monkeypatch, L, N):
+    """The epoch-end full-batch evaluation at the picked anchor, started on a third stream once that iterate
+    exists (SlbfgsSolver::post_full), is bitwise the ordered evaluation after the last inner step
+    (LBF_NO_FULL_AHEAD=1): losses, gradient norms, live pairs and parameters over several epochs, picks early
+    and late in the ring (N = 640, b = 64: 10 inner steps, the whole epoch fits the L + 1 = 11 ring, so a pick
+    of entry 0 is the epoch's own anchor, posted before the first step)."""
+    Xh, Yh = pkg.synth_mnist(N)
+    X, Y = dev(Xh), dev(Yh)
+    kw = dict(KW, L=L)
+    out = []
+    for off in ("0", "1"):
+        monkeypatch.setenv("LBF_NO_FULL_AHEAD", off)
+        net = pkg.Mlp(ctx, DIMS, ACTS)
+        P = net.init_params(123, "cpu")
+        hist, info = pkg.slbfgs_solve(net, P, X, Y, max_epochs=6, **kw)
+        out.append((host(P), hist, info))
+    (P0, h0, i0), (P1, h1, i1) = out
+    assert np.array_equal(P0, P1)
+    for k in ("loss", "grad_norm", "accepted"):
+        assert np.array_equal(h0[k], h1[k]), k
+    assert i0.n_evals == i1.n_evals and i0.n_rows == i1.n_rows
+    assert np.all(np.isfinite(h0["loss"]))
