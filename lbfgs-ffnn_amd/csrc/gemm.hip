@@ -542,6 +542,7 @@ __global__ __launch_bounds__(256 * KW, 2) void gemm_kernel(const GemmK g) {
 
   if (EPI == EPI_HEAD) KT(0);
   if (EPI == EPI_HEAD) KTB(0);
+  if (EPI == EPI_HEAD) KTHW();
   // EPI_HEAD: the head's HBM inputs (W, biases, targets) are loaded while the last k-tile computes
   headc::EpiPrefetch<BN, BM, 256 * KW> hpre;
   if (kb < ke) {
@@ -800,6 +801,7 @@ __device__ __forceinline__ void glds_body(const GemmK &g, float *lds, int zsplit
   if (EPI == EPI_HEAD) KT(0);
   if (EPI == EPI_HEAD) KTC(40);
   if (EPI == EPI_HEAD) KTB(0);
+  if (EPI == EPI_HEAD) KTHW();
   headc::EpiPrefetch<BN, BM, 256 * KW> hpre;
   if constexpr (EPI == EPI_HEAD) {
     hpre.load(g.head_P, g.N, g.head_out, g.bias, g.head_Y, g.head_idx, m0, g.M);
@@ -1333,5 +1335,8 @@ extern "C" int lbf_dbg_ktrace_gemm(unsigned long long *host, int n) {
 }
 extern "C" int lbf_dbg_ktrace_gemm_blk(unsigned long long *host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(lbf::lbf_kt_blk), sizeof(lbf::lbf_kt_blk)) == hipSuccess ? 0 : 1;
+}
+extern "C" int lbf_dbg_ktrace_gemm_hw(unsigned long long *host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(lbf::lbf_kt_hw), sizeof(lbf::lbf_kt_hw)) == hipSuccess ? 0 : 1;
 }
 #endif

@@ -124,7 +124,22 @@ static __device__ unsigned long long lbf_kt_blk[8 * 1024];
     const unsigned lin_ = blockIdx.y * gridDim.x + blockIdx.x;                                          \
     if (threadIdx.x == 0 && blockIdx.z == 0 && lin_ < 1024) lbf_kt_blk[(slot) * 1024 + lin_] = wall_clock64(); \
   } while (0)
+// KTHW(): where the block runs (XCC id << 32 | HW_ID: CU, shader array, SE, SIMD), for the per-block stamps
+static __device__ unsigned long long lbf_kt_hw[1024];
+#define KTHW()                                                                                          \
+  do {                                                                                                  \
+    const unsigned lin_ = blockIdx.y * gridDim.x + blockIdx.x;                                          \
+    if (threadIdx.x == 0 && blockIdx.z == 0 && lin_ < 1024) {                                           \
+      unsigned xcc_, hw_;                                                                               \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                                \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                                  \
+      lbf_kt_hw[lin_] = ((unsigned long long)xcc_ << 32) | hw_;                                         \
+    }                                                                                                   \
+  } while (0)
 #else
+#define KTHW()                                                                                          \
+  do {                                                                                                  \
+  } while (0)
 #define KTF(slot)                                                                                       \
   do {                                                                                                  \
   } while (0)

@@ -600,8 +600,8 @@ SlbfgsSolver::SlbfgsSolver(Mlp *net, const lbf_slbfgs_params &prm, float *d_para
     }
     const int dev = ctx_->device;
     tw_.reset(new TaskFifo([dev]() { LBF_HIP(hipSetDevice(dev)); }));
-    // the epoch-end full-batch evaluation ahead (see fnet_): single rank
-    if (!ctx_->dp() && env_int("LBF_NO_FULL_AHEAD", 0) == 0) {
+    // the epoch-end full-batch evaluation ahead (see fnet_): single rank, opt-in (LBF_FULL_AHEAD=1)
+    if (!ctx_->dp() && env_int("LBF_FULL_AHEAD", 0) != 0) {
       fctx_.reset(new Ctx());
       fctx_->device = ctx_->device;
       fctx_->cus = ctx_->cus;

@@ -276,7 +276,10 @@ private:
   // slot to the end. A third workspace of the network on its own stream evaluates it beside the epoch's last
   // inner steps into mu_next_ and its own status block; the context stream joins it where the ordered route
   // evaluated. Same launches on the same inputs: bitwise the ordered route. Single rank only (data parallel
-  // keeps the ordered, sharded evaluation and its fingerprint check); LBF_NO_FULL_AHEAD=1 turns it off.
+  // keeps the ordered, sharded evaluation and its fingerprint check). Opt-in (LBF_FULL_AHEAD=1): measured
+  // slower at cfg 4, 35.27-35.59 against 35.88-36.16 epochs/s interleaved (profiles/r05/n/): the full-batch
+  // GEMMs occupy the chip for ~1.2 ms and the latency-bound inner steps beside them slow down by more than
+  // the evaluation's ~0.6 ms average window (the pick lands mid-ring) saves.
   std::unique_ptr<Ctx> fctx_;
   std::unique_ptr<Mlp> fnet_;
   DevBuf<float> mu_next_;

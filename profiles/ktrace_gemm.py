@@ -55,6 +55,28 @@ def main():
         print(f"N={N} blocks={nb} (min/med/max us): " + "  ".join(line) + f"  end {min(ends):.2f}/{q(ends):.2f}/{max(ends):.2f}")
         late = sorted(range(nb), key=lambda i: starts[i])[-8:]
         print(f"N={N} latest starters:", " ".join(f"{i}:{starts[i]:.1f}" for i in late))
+        # placement (lbf_kt_hw: XCC id, HW_ID): main loop and end by XCD and by blocks sharing the CU
+        hw = (C.c_ulonglong * 1024)()
+        if hasattr(L, "lbf_dbg_ktrace_gemm_hw"):
+            L.lbf_dbg_ktrace_gemm_hw.argtypes = [C.c_void_p]
+            assert L.lbf_dbg_ktrace_gemm_hw(hw) == 0
+            key = []
+            for i in range(nb):
+                h = hw[i] & 0xffffffff
+                key.append((hw[i] >> 32, (h >> 13) & 7, (h >> 12) & 1, (h >> 8) & 15))
+            share = {k: key.count(k) for k in set(key)}
+            ml = [(S[1][i] - S[0][i]) / 100 for i in range(nb)]
+            en = [(S[7][i] - t0) / 100 for i in range(nb)]
+            for name, grp in (("xcc", lambda i: key[i][0]), ("blocks on the CU", lambda i: share[key[i]])):
+                g = {}
+                for i in range(nb):
+                    g.setdefault(grp(i), []).append(i)
+                print(f"N={N} by {name}: " + "  ".join(
+                    f"{k}: n={len(v)} loop {q([ml[i] for i in v]):.1f}/{max(ml[i] for i in v):.1f} end "
+                    f"{q([en[i] for i in v]):.1f}/{max(en[i] for i in v):.1f}" for k, v in sorted(g.items())))
+            slow = sorted(range(nb), key=lambda i: -ml[i])[:12]
+            print(f"N={N} slowest main loops (block: us xcc/se/sh/cu, blocks on the CU):",
+                  " ".join(f"{i}:{ml[i]:.1f} {key[i][0]}/{key[i][1]}/{key[i][2]}/{key[i][3]},{share[key[i]]}" for i in slow))
 
 
 if __name__ == "__main__":

@@ -94,16 +94,16 @@ def test_profiler_times_sampled_launches(ctx, pkg):
 @pytest.mark.parametrize("L,N", [(4, 1024), (10, 640)])
 def test_full_ahead_equals_ordered(ctx, pkg, monkeypatch, L, N):
     """The epoch-end full-batch evaluation at the picked anchor, started on a third stream once that iterate
-    exists (SlbfgsSolver::post_full), is bitwise the ordered evaluation after the last inner step
-    (LBF_NO_FULL_AHEAD=1): losses, gradient norms, live pairs and parameters over several epochs, picks early
+    exists (SlbfgsSolver::post_full, opt-in LBF_FULL_AHEAD=1), is bitwise the ordered evaluation after the last
+    inner step: losses, gradient norms, live pairs and parameters over several epochs, picks early
     and late in the ring (N = 640, b = 64: 10 inner steps, the whole epoch fits the L + 1 = 11 ring, so a pick
     of entry 0 is the epoch's own anchor, posted before the first step)."""
     Xh, Yh = pkg.synth_mnist(N)
     X, Y = dev(Xh), dev(Yh)
     kw = dict(KW, L=L)
     out = []
-    for off in ("0", "1"):
-        monkeypatch.setenv("LBF_NO_FULL_AHEAD", off)
+    for on in ("1", "0"):
+        monkeypatch.setenv("LBF_FULL_AHEAD", on)
         net = pkg.Mlp(ctx, DIMS, ACTS)
         P = net.init_params(123, "cpu")
         hist, info = pkg.slbfgs_solve(net, P, X, Y, max_epochs=6, **kw)
