@@ -521,7 +521,10 @@ def run_rank(a, world, rank, local, pkg):
     ctx.prof_enable(False)
     if not a.breakdown_last:
         run.iterate(a.warmup)
-    dominant = max(breakdown.items(), key=lambda kv: kv[1][0])[0]
+    # the section with the largest total time among those that run at least once per iteration (a section of
+    # the occasional non-speculative start can win the breakdown when a profiler serialises the launches)
+    regular = {k: v for k, v in breakdown.items() if v[1] >= bd_steps} or breakdown
+    dominant = max(regular.items(), key=lambda kv: kv[1][0])[0]
     if world > 1:  # every rank must time the same section (identical launch sequences)
         obj = [dominant]
         torch.distributed.broadcast_object_list(obj, src=0)
@@ -572,6 +575,8 @@ def run_rank(a, world, rank, local, pkg):
         fwd_passes = evals - gal + lonly
         gflops = (fwd_passes * Ffwd + evals * (F - Ffwd)) / elapsed / 1e9
         # dominant kernel: largest total time in the timed region (HIP events on the library stream)
+        if dominant not in prof:
+            raise SystemExit(f"bench.py: the dominant section {dominant} did not run in the timed region")
         name, (ms, cnt) = dominant, prof[dominant]
         avg_s = ms / 1e3 / cnt
         kind, layer = name.split("[")[0], int(name.split("[")[1].rstrip("]"))

@@ -74,6 +74,13 @@ def main():
                 print(f"N={N} by {name}: " + "  ".join(
                     f"{k}: n={len(v)} loop {q([ml[i] for i in v]):.1f}/{max(ml[i] for i in v):.1f} end "
                     f"{q([en[i] for i in v]):.1f}/{max(en[i] for i in v):.1f}" for k, v in sorted(g.items())))
+            raw = os.environ.get("KT_RAW")
+            if raw:  # per block: id, start, main-loop end, end (us from the first start), xcc, se, sh, cu
+                with open(f"{raw}_{N}.csv", "w") as fh:
+                    fh.write("block,start_us,loop_end_us,end_us,xcc,se,sh,cu,blocks_on_cu\n")
+                    for i in range(nb):
+                        fh.write(f"{i},{(S[0][i] - t0) / 100:.2f},{(S[1][i] - t0) / 100:.2f},{en[i]:.2f},"
+                                 f"{key[i][0]},{key[i][1]},{key[i][2]},{key[i][3]},{share[key[i]]}\n")
             slow = sorted(range(nb), key=lambda i: -ml[i])[:12]
             print(f"N={N} slowest main loops (block: us xcc/se/sh/cu, blocks on the CU):",
                   " ".join(f"{i}:{ml[i]:.1f} {key[i][0]}/{key[i][1]}/{key[i][2]}/{key[i][3]},{share[key[i]]}" for i in slow))
