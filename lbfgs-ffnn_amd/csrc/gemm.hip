@@ -924,8 +924,8 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_group_ker
 }
 
 // ------------------------------------------------------------------------------------------------
-// Wave-split-K direct-load main loop for the 32 x 128 tile (round 5; profiles/micro/loop32.hip, results in
-// profiles/r05/c/). The LDS-DMA loop of this tile spends ~1.8k cycles per 32-deep k-tile against 1024 of MFMA
+// Wave-split-K direct-load main loop for the 32 x 128 tile (round 5; microbenchmark profiles/micro/loop32.hip,
+// whose results were lost with the session that ran it; library A/B in profiles/r05/g/, n/). The LDS-DMA loop of this tile spends ~1.8k cycles per 32-deep k-tile against 1024 of MFMA
 // issue: its DMA writes and fragment reads contend for the LDS while each wave waits on its reads, and the
 // DMA pieces' issue cost sits in front of the MFMAs. Here no operand is shared between waves and nothing
 // goes through LDS until the end: the four waves split every 32-deep k-tile (wave w: k 8w .. 8w+7, lane half
@@ -1195,7 +1195,7 @@ void launch(hipStream_t s, const GemmDesc &d, const GemmDesc *d2 = nullptr) {
 
 // gemm_wsk_kernel's conditions: 16-B quads everywhere. Opt-in (LBF_WSK=1): in the library's GEMMs it measured
 // no faster than the LDS-DMA loop at the 8-rank shard's fused-head forward and 10 % slower on config 4's
-// minibatch GEMMs (profiles/r05/g/), although its main loop alone is 28 % faster (profiles/r05/c/loop32.txt).
+// minibatch GEMMs (profiles/r05/g/), although its main loop alone measured 28 % faster (profiles/micro/loop32.hip).
 static bool wsk_ok(const GemmDesc &d) {
   static const bool off = [] {
     const char *e = std::getenv("LBF_WSK");
