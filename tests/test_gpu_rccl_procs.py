@@ -125,21 +125,23 @@ def test_rccl_against_single_route(ctx, pkg, rccl2):
     assert np.max(np.abs(a["wolfe_loss"] - h1["loss"]) / np.abs(h1["loss"])) <= 1e-5
 
 
-@pytest.mark.parametrize("solver", ["lbfgs", "slbfgs"])
-def test_bench_two_ranks_one_gpu(solver, tmp_path):
-    """bench.py as the driver runs it at N = 2 (WORLD_SIZE set, one process per rank, the RCCL id through
-    gloo, the barrier + max-over-ranks clock), both ranks on GPU 0: one JSON line from rank 0 with
-    n_gpus 2 / dp2 and a finite value. The timing of two ranks sharing one GPU over sockets is not a result."""
-    world, port = 2, free_port()
-    args = ["--gpus", "2", "--steps", "3" if solver == "slbfgs" else "10", "--warmup", "1", "--no-cpu-baseline",
+@pytest.mark.parametrize("solver,world", [("lbfgs", 2), ("slbfgs", 2), ("lbfgs", 4)])
+def test_bench_two_ranks_one_gpu(solver, world, tmp_path):
+    """bench.py as the driver runs it at N = 2 and 4 (WORLD_SIZE set, one process per rank, the RCCL id through
+    gloo, the barrier + max-over-ranks clock; at 4 ranks also shard offsets past the second rank), every rank
+    on GPU 0: one JSON line from rank 0 with n_gpus N / dpN and a finite value. The timing of ranks sharing one
+    GPU over sockets is not a result."""
+    port = free_port()
+    args = ["--gpus", str(world), "--steps", "3" if solver == "slbfgs" else "10", "--warmup", "1", "--no-cpu-baseline",
             "--device-warmup", "0", "--solver", solver]
     outs = run_procs([([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + args, rank_env(r, world, port))
                       for r in range(world)], timeout=300)
     lines = [ln for ln in outs[0].splitlines() if ln.startswith("{")]
     assert len(lines) == 1, outs[0][-3000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"].startswith("dp2")
+    assert d["n_gpus"] == world and d["config"]["parallelism"].startswith(f"dp{world}")
     assert np.isfinite(d["value"]) and d["value"] > 0
-    assert not any(ln.startswith("{") for ln in outs[1].splitlines())
+    for o in outs[1:]:
+        assert not any(ln.startswith("{") for ln in o.splitlines())
     (tmp_path / "bench.json").write_text(lines[0])
-    print(f"bench --gpus 2 ({solver}) on one GPU over sockets: {d['value']} {d['unit']}")
+    print(f"bench --gpus {world} ({solver}) on one GPU over sockets: {d['value']} {d['unit']}")
