@@ -275,16 +275,21 @@ def main_slbfgs(a, pkg, ctx, world, rank):
     breakdown = ctx.prof_read()
     ctx.prof_enable(False)
     wep = 1
-    dominant = max(breakdown.items(), key=lambda kv: kv[1][0])[0]
+    # the dominant GEMM section (the roofline is a GEMM's); at many ranks the epoch's all-reduce can take longer,
+    # but it runs once or twice per epoch, too rarely to sample
+    gemms = {k: v for k, v in breakdown.items() if k.split("[")[0] in ("gemm_fwd", "gemm_dw", "gemm_dx")}
+    dominant = max((gemms or breakdown).items(), key=lambda kv: kv[1][0])[0]
     if world > 1:
         obj = [dominant]
         torch.distributed.broadcast_object_list(obj, src=0)
         dominant = obj[0]
     # timed region: only the dominant section carries events, on every PROF_EVERY-th launch (an event pair
-    # costs ~10 us of GPU time, and this section runs ~2x per inner step); the rows of every timed launch
-    # are counted (lbf_prof_read_work), so the sampled flops are exact whatever the batch sizes
+    # costs ~10 us of GPU time, and this section runs ~2x per inner step) while that still times
+    # PROF_MIN_LAUNCHES of them; the rows of every timed launch are counted (lbf_prof_read_work), so the
+    # sampled flops are exact whatever the batch sizes
+    every = max(1, min(PROF_EVERY, int(breakdown[dominant][1] * max(a.steps, 1) // PROF_MIN_LAUNCHES)))
     ctx.prof_select(dominant)
-    ctx.prof_sample(PROF_EVERY)
+    ctx.prof_sample(every)
     ctx.prof_enable(True)
     run.iterate(a.warmup)
     ctx.prof_enable(True)          # clears the warmup's timings
@@ -313,6 +318,8 @@ def main_slbfgs(a, pkg, ctx, world, rank):
     if rank == 0:
         epochs = int(info.iterations) - ep0
         F = pkg.grad_flops_per_sample(dims)
+        if dominant not in prof:
+            raise SystemExit(f"bench.py: the dominant section {dominant} did not run in the timed region")
         name, (ms, launches) = dominant, prof[dominant]
         kind, layer = name.split("[")[0], int(name.split("[")[1].rstrip("]"))
         roof = dict(bound="mfma", achieved=None, peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s", frac=None)
@@ -323,7 +330,7 @@ def main_slbfgs(a, pkg, ctx, world, rank):
             roof["achieved"] = round(flops / (ms / 1e3) / 1e12, 3)
             roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
         roof.update(kernel=name, avg_launch_us=round(ms * 1e3 / launches, 2), timed_launches=launches,
-                    sampled_every=PROF_EVERY, avg_rows_per_timed_launch=round(work.get(dominant, 0.0) / launches, 1),
+                    sampled_every=every, avg_rows_per_timed_launch=round(work.get(dominant, 0.0) / launches, 1),
                     traffic=pmc_traffic(a.pmc_json, name, f"{','.join(str(d) for d in dims)}:{a.samples}:{world}"))
         # (traffic: the median over the section's minibatch launches, the PMC pass's most frequent size)
         out = {
