@@ -531,7 +531,9 @@ def run_rank(a, world, rank, local, pkg):
     # the section with the largest total time among those that run at least once per iteration (a section of
     # the occasional non-speculative start can win the breakdown when a profiler serialises the launches)
     regular = {k: v for k, v in breakdown.items() if v[1] >= bd_steps} or breakdown
-    dominant = max(regular.items(), key=lambda kv: kv[1][0])[0]
+    # the roofline is a GEMM's: at many ranks the all-reduce section can take longer than any GEMM
+    gemms = {k: v for k, v in regular.items() if k.split("[")[0] in ("gemm_fwd", "gemm_dw", "gemm_dx")}
+    dominant = max((gemms or regular).items(), key=lambda kv: kv[1][0])[0]
     if world > 1:  # every rank must time the same section (identical launch sequences)
         obj = [dominant]
         torch.distributed.broadcast_object_list(obj, src=0)
