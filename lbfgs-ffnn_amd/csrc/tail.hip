@@ -44,7 +44,9 @@ template <int VPW>
 __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   constexpr int TC = TAIL_COLS, C = TAIL_COLS / 64;
   const RedAllArgs &ra = a.ra;
-  if (ra.abort && *ra.abort) return;
+  // the speculative chain's abort flag: requested with the ring header (one round trip for both) and tested
+  // before the block's history and slab loads, so an aborted launch exits after that round trip
+  const int abf = abort_flag(ra.abort);
   __shared__ double part[4][TC];
   __shared__ float xs[2 * TAIL_MAXM][TC]; // this group's values of the live history vectors
   __shared__ float ops[5][TC];            // s, y, g, p, w
@@ -60,11 +62,11 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   // the ring header in one round trip (count, free slot, order)
   if (t < IST_ORDER + h.m) ist[t] = h.ist[t];
   lds_barrier();
+  if (aborted(abf)) return; // uniform for the launch: no store, no arrival
   KTB(1);
   // wave-uniform scalars (SGPRs): the loads below then need no per-lane select or branch
   const int count0 = __builtin_amdgcn_readfirstlane(ist[IST_COUNT]);
   const int w = __builtin_amdgcn_readfirstlane(hist_write_slot(ist, h.m, a.policy, 0));
-  if (blockIdx.x == 0 && t == 0) h.ist[IST_WSLOT] = w;
   const int nvec = 2 * count0;
   const int cg = blockIdx.x;
   int si = 0;
@@ -130,6 +132,7 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
           if (k + 4 * u < S.splits) acc[c] += double(x[u][c]);
     }
   }
+  if (blockIdx.x == 0 && t == 0) h.ist[IST_WSLOT] = w;
   KT(50);
 #pragma unroll
   for (int c = 0; c < C; ++c) part[stripe][lane + 64 * c] = acc[c];
@@ -218,10 +221,11 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
 // transposed ([nc][nb]), so each block reads one contiguous column. The sum is
 // stored write-through (agent-scope relaxed store = sc1) and waited for, so the arrival counter's add
 // publishes it without a release fence (MI355X_MICROARCH.md hand-off table, first row).
-__device__ __forceinline__ void tail_cols_body(const TailArgs &a) {
+__device__ __forceinline__ void tail_cols_body(const TailArgs &a, int abf) {
   __shared__ double ws[4];
   const int c = blockIdx.x, t = threadIdx.x;
-  const int count0 = a.h.ist[IST_COUNT];
+  const int count0 = a.h.ist[IST_COUNT]; // in flight with the caller's abort flag
+  if (aborted(abf)) return;
   // only the columns in use (live pairs and the self block)
   if (c < 6 * a.h.m && c >= 6 * count0) return;
   const double *colp = a.rows + (long long)c * a.nb;
@@ -381,9 +385,10 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
 // each block's column sum is an sc1 (write-through) store waited for with vmcnt(0) before the same lane's
 // agent-scope add; the block whose add returns the last count reads the sums with sc1 loads.
 __global__ __launch_bounds__(TF_THREADS) void tail_cols_fin_kernel(const TailArgs a) {
-  if (a.ra.abort && *a.ra.abort) return; // uniform for the launch: nobody arrives, the counter stays 0
+  const int abf = abort_flag(a.ra.abort);
   KT(39);
-  tail_cols_body(a);
+  tail_cols_body(a, abf);
+  if (aborted(abf)) return; // uniform for the launch: nobody arrives, the counter stays 0
   __shared__ int s_last;
   if (threadIdx.x == 0)
     s_last = __hip_atomic_fetch_add(a.cols_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;

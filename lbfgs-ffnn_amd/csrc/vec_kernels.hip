@@ -1292,7 +1292,9 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
 // round trip for the header, one for the data.
 template <int KMAX>
 __global__ __launch_bounds__(256) void combine_small_kernel(const CombineArgs a) {
-  if (a.h.abort && *a.h.abort) return;
+  // the speculative chain's abort flag: requested with the header, g and x (one round trip for all) and
+  // tested before the history loads, so an aborted launch exits after that round trip
+  const int abf = abort_flag(a.h.abort);
   const HistView &h = a.h;
   const int S_ = h.slots, lane = threadIdx.x & 63;
   const long long e0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1307,6 +1309,7 @@ __global__ __launch_bounds__(256) void combine_small_kernel(const CombineArgs a)
   const double csr = h.coef[lk], cyr = h.coef[S_ + lk];
   const double cg = h.coef[2 * S_];
   const double alpha = a.alpha_from_state ? h.scal[SC_ALPHA0] : a.alpha;
+  if (aborted(abf)) return; // uniform for the launch
   float sv[KMAX], yv[KMAX];
   if (k > 0) {
 #pragma unroll

@@ -40,4 +40,13 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // it by another thread of the block, the LDS wait is all the barrier has to order.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// The speculative chain's abort flag (null: never aborted), requested as a vector load (an agent-scope
+// relaxed atomic load is a global_load, counted by vmcnt). A kernel that tests it only once its first loads
+// are in flight then does not wait for it in front of them; a scalar load of the flag would be covered by the
+// kernel's first lgkmcnt wait for its arguments. Test it wave-uniformly: aborted(flag).
+__device__ __forceinline__ int abort_flag(const int *p) {
+  return p ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+}
+__device__ __forceinline__ bool aborted(int flag) { return __builtin_amdgcn_readfirstlane(flag) != 0; }
+
 } // namespace lbf
