@@ -341,8 +341,9 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_kernel(const DirArgs a) {
   if (h.abort && *h.abort) return;
   __shared__ double ws[4];
   const int c = blockIdx.x, t = threadIdx.x;
+  // The column's loads go out with the live count (one round trip for both): a column not in use (a pair slot
+  // not yet live) sums whatever its rows hold and stores nothing.
   const int count0 = h.ist[IST_COUNT];
-  if (c < 6 * h.m && c >= 6 * count0) return; // only the columns in use (live pairs and the self block)
   const double *colp = a.rows + (long long)c * a.nb;
   double v[8];
   double s = 0.0;
@@ -358,6 +359,7 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_kernel(const DirArgs a) {
   s = wave_sum_f64(s);
   if ((t & 63) == 0) ws[t >> 6] = s;
   lds_barrier();
+  if (c < 6 * h.m && c >= 6 * count0) return; // only the columns in use (live pairs and the self block)
   if (t == 0) a.dots[c] = ((ws[0] + ws[1]) + ws[2]) + ws[3]; // dir_cols_fin's order
 }
 
@@ -382,10 +384,12 @@ __global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int m = h.m, S_ = h.slots;
   // ---- round trip 1: header, dots, K and gamma; this lane's g and x ----
+  // (K is staged for rows and columns < 2m, not < 2k: its loads then need no live count first, one round trip
+  // for all; the rows and columns past 2k are not read)
   const int k = __builtin_amdgcn_readfirstlane(h.ist[IST_COUNT]);
   if (t < m) Ls[t] = h.ist[IST_ORDER + t];
-  for (int i = t; i < 4 * k * k; i += 256) { // rows and columns < 2k of the DIR_KS-stride map
-    const int r = i / (2 * k), c = i - r * (2 * k);
+  for (int i = t; i < 4 * m * m; i += 256) { // rows and columns < 2m of the DIR_KS-stride map
+    const int r = i / (2 * m), c = i - r * (2 * m);
     sK[r * DIR_KS + c] = a.kmat[r * DIR_KS + c];
   }
   const double gamma = k > 0 ? a.kmat[DIR_KS * DIR_KS] : 1.0;
