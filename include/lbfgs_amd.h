@@ -107,7 +107,10 @@ int lbf_mlp_loss_grad(lbf_mlp *net, const float *d_params, float *d_grad, const 
 /* ---- two-loop recursion (src/minimizer/lbfgs.hpp:106-139 / s_lbfgs.hpp:106-136 /
  * lbfgs.cuh:206-261) on an explicit history given in logical order (oldest first):
  * d_S, d_Y are k x n row-major, h_rho[k]. mode: 0 = CPU (returns -Hg), 1 = S-LBFGS (returns +Hg,
- * gamma guarded and clamped), 2 = CUDA (returns -Hg, gamma guarded). */
+ * gamma guarded and clamped), 2 = CUDA (returns -Hg, gamma guarded), 3 = S-LBFGS as the S-LBFGS solver computes
+ * it: each pair offered through the solver's pair update (kept when |y.s| > 1e-10, rho = 1 / y.s on the device,
+ * h_rho ignored; s_lbfgs.hpp:245-256), then one direction-only step (the coefficients from the pairs' map K;
+ * k <= 16, n % 4 == 0). */
 /* Exact Hessian-vector product of the batch loss of lbf_mlp_loss_grad (same inv_scale / l2 / d_idx
  * meaning): d_hv = H(params) d_v, computed with Pearlmutter's R-operator on the device (one forward
  * and backward R-pass; no finite differences). With a communicator the shards' products are summed.
@@ -269,6 +272,17 @@ int lbf_slbfgs_end(lbf_slbfgs *s);
  * the iterate average u, s = u - u_prev and the y stored for it (s_lbfgs.hpp:236-256), n floats each into
  * device buffers (any may be NULL). LBF_ERR_INVALID until a candidate has been traced. */
 int lbf_slbfgs_pair0(lbf_slbfgs *s, float *d_wt, float *d_u, float *d_s, float *d_y);
+/* Diagnostics, teacher forcing of the curvature pairs (set before the first iterate; a new function, so no struct
+ * of ABI 3 changes). A curvature event is every inner step t > 0 with t % L == 0 (s_lbfgs.hpp:236-261), the
+ * first, which only pushes u, included; with ld = (n + 3) & ~3, event e (counted over epochs, e < cap):
+ *   d_rec   (nullable) receives [w_{t+1} | u | g(u + eps s) | g(u - eps s)] at d_rec + 4 e ld (ld floats each;
+ *           the two gradients of the batch loss + lambda w, zero at the first event; with hvp_exact the second
+ *           is zero and the first is H(u) s);
+ *   d_force (nullable, same layout, e.g. another run's d_rec) replaces u before s = u - u_prev and the two
+ *           gradients before y = (g+ - g-) / (2 eps) is stored, so the ring receives the other run's pairs
+ *           while the iterates w_t stay this run's own. Two routes forced with one run's record then compare
+ *           non-chaotically: the gradients at the same points, and the iterates under the same history. */
+int lbf_slbfgs_pair_io(lbf_slbfgs *s, int cap, float *d_rec, const float *d_force);
 
 /* ---- profiling: HIP-event timing of every kernel class on the context stream (benchmark use).
  * Section id = kind*16 + layer; kinds: 0 fwd GEMM, 1 dW GEMM, 2 dX GEMM, 3 loss, 4 split-K reduce,

@@ -404,12 +404,15 @@ inline void write_hip_history_csv(const std::string &filename, const IterationRe
     f << i << "," << l[i] << "," << g[i] << "," << t[i] << "\n";
 }
 
-/// UnifiedOptimizer<HipBackend> (unified_optimization.hpp:420-439). Device data are raw fp32 pointers
-/// (rows of In / Out floats per sample == the reference's column-major matrices).
+/// UnifiedOptimizer<HipBackend> (unified_optimization.hpp:420-439): the reference strategy's parameter list,
+/// (handle, net, host_data, d_train_x, d_train_y, config), so a strategy written against
+/// UnifiedOptimizer<CudaBackend>::optimize overrides this one with its backend types renamed. host_data is the
+/// host dataset (for dimensions: n_train = host_data.train_x.cols()); the device data are fp32 rows of In / Out
+/// floats per sample (== the reference's column-major matrices).
 template <> class UnifiedOptimizer<HipBackend> {
 public:
   virtual ~UnifiedOptimizer() = default;
-  virtual void optimize(hip_mlp::HipHandle &handle, NetworkWrapper<HipBackend> &net, long n_train,
+  virtual void optimize(hip_mlp::HipHandle &handle, NetworkWrapper<HipBackend> &net, const UnifiedDataset &host_data,
                         hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &d_train_x,
                         hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &d_train_y, const UnifiedConfig &config) = 0;
   IterationRecorder<HipBackend> recorder;
@@ -420,9 +423,10 @@ public:
 /// all on the device (no per-evaluation callback or D2D gradient copy, cf. :483-491).
 class UnifiedLBFGS_HIP : public UnifiedOptimizer<HipBackend> {
 public:
-  void optimize(hip_mlp::HipHandle &, NetworkWrapper<HipBackend> &net, long n_train,
+  void optimize(hip_mlp::HipHandle &, NetworkWrapper<HipBackend> &net, const UnifiedDataset &host_data,
                 hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dx, hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dy,
                 const UnifiedConfig &c) override {
+    const long n_train = long(host_data.train_x.cols());
     auto &nw = net.getInternal();
     lbf_lbfgs_params prm;
     lbf_lbfgs_default_params(&prm, line_search);
@@ -443,9 +447,10 @@ public:
 /// S-LBFGS on the device (the reference's is CPU-only: unified_optimization.hpp:306-408, 688-696).
 class UnifiedSLBFGS_HIP : public UnifiedOptimizer<HipBackend> {
 public:
-  void optimize(hip_mlp::HipHandle &, NetworkWrapper<HipBackend> &net, long n_train,
+  void optimize(hip_mlp::HipHandle &, NetworkWrapper<HipBackend> &net, const UnifiedDataset &host_data,
                 hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dx, hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dy,
                 const UnifiedConfig &c) override {
+    const long n_train = long(host_data.train_x.cols());
     auto &nw = net.getInternal();
     lbf_slbfgs_params prm;
     lbf_slbfgs_default_params(&prm);
@@ -470,9 +475,10 @@ public:
 /// max_iters, tolerance from the config (gd.cuh:38-106), on the device.
 class UnifiedGD_HIP : public UnifiedOptimizer<HipBackend> {
 public:
-  void optimize(hip_mlp::HipHandle &, NetworkWrapper<HipBackend> &net, long n_train,
+  void optimize(hip_mlp::HipHandle &, NetworkWrapper<HipBackend> &net, const UnifiedDataset &host_data,
                 hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dx, hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dy,
                 const UnifiedConfig &c) override {
+    const long n_train = long(host_data.train_x.cols());
     auto &nw = net.getInternal();
     lbf_gd_params prm;
     lbf_gd_default_params(&prm);
@@ -496,9 +502,10 @@ public:
 /// (sgd.cuh:50-153; the reference does not pass the tolerance, so CudaSGD keeps its 1e-6).
 class UnifiedSGD_HIP : public UnifiedOptimizer<HipBackend> {
 public:
-  void optimize(hip_mlp::HipHandle &, NetworkWrapper<HipBackend> &net, long n_train,
+  void optimize(hip_mlp::HipHandle &, NetworkWrapper<HipBackend> &net, const UnifiedDataset &host_data,
                 hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dx, hip_mlp::DeviceBuffer<hip_mlp::HipScalar> &dy,
                 const UnifiedConfig &c) override {
+    const long n_train = long(host_data.train_x.cols());
     auto &nw = net.getInternal();
     lbf_sgd_params prm;
     lbf_sgd_default_params(&prm);
@@ -527,22 +534,24 @@ public:
   template <int In, int Out, typename Activation> void addLayer() { net_wrapper_.addLayer<In, Out, Activation>(); }
   void buildNetwork() { net_wrapper_.bindParams(); }
 
-  /// Host -> device upload with the fp64 -> fp32 conversion of unified_launcher.hpp:105-128.
+  /// Host -> device upload with the fp64 -> fp32 conversion of unified_launcher.hpp:105-128; like the reference
+  /// it keeps a copy of the dataset, which train() hands to the strategy as host_data.
   /// Works with the reference's Eigen-based UnifiedDataset and with the standalone HostMatrix one.
-  template <typename Dataset> void setData(const Dataset &data) {
-    upload(data.train_x, d_train_x_, train_x_);
-    upload(data.train_y, d_train_y_, train_y_);
-    upload(data.test_x, d_test_x_, test_x_);
-    upload(data.test_y, d_test_y_, test_y_);
-    n_train_ = long(data.train_x.cols());
-    n_test_ = long(data.test_x.cols());
+  void setData(const UnifiedDataset &data) {
+    dataset_ = data;
+    upload(dataset_.train_x, d_train_x_, train_x_);
+    upload(dataset_.train_y, d_train_y_, train_y_);
+    upload(dataset_.test_x, d_test_x_, test_x_);
+    upload(dataset_.test_y, d_test_y_, test_y_);
+    n_train_ = long(dataset_.train_x.cols());
+    n_test_ = long(dataset_.test_x.cols());
     std::cout << "Data Uploaded to GPU. Train: " << n_train_ << " samples." << std::endl;
   }
 
   void train(UnifiedOptimizer<HipBackend> &optimizer, const UnifiedConfig &config) {
     std::cout << ">>> Running HIP Experiment: " << config.name << std::endl;
     if (config.reset_params) net_wrapper_.bindParams(config.seed);
-    optimizer.optimize(handle_, net_wrapper_, n_train_, d_train_x_, d_train_y_, config);
+    optimizer.optimize(handle_, net_wrapper_, dataset_, d_train_x_, d_train_y_, config);
     last_train_ = evaluate(train_y_, d_train_x_, n_train_, "Training Results");
   }
   void test() { last_test_ = evaluate(test_y_, d_test_x_, n_test_, "Test Results"); }
@@ -593,6 +602,7 @@ private:
 
   hip_mlp::HipHandle handle_;
   NetworkWrapper<HipBackend> net_wrapper_;
+  UnifiedDataset dataset_;
   hip_mlp::DeviceBuffer<hip_mlp::HipScalar> d_train_x_, d_train_y_, d_test_x_, d_test_y_;
   std::vector<double> train_x_, train_y_, test_x_, test_y_;
   std::vector<long> rows_;

@@ -119,6 +119,7 @@ def lib():
         "lbf_slbfgs_iterate": (C.c_int, [_vp, C.c_int, C.POINTER(Record), C.POINTER(SolveInfo)]),
         "lbf_slbfgs_end": (C.c_int, [_vp]),
         "lbf_slbfgs_pair0": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+        "lbf_slbfgs_pair_io": (C.c_int, [_vp, C.c_int, _vp, _vp]),
         "lbf_prof_enable": (C.c_int, [_vp, C.c_int]),
         "lbf_prof_select": (C.c_int, [_vp, C.c_int]),
         "lbf_prof_sample": (C.c_int, [_vp, C.c_int]),
@@ -154,7 +155,7 @@ EXPORTS = ("lbf_last_error lbf_version lbf_abi_version lbf_ctx_create lbf_ctx_de
            "lbf_comm_unique_id lbf_comm_init lbf_comm_init_local lbf_comm_rank lbf_allreduce_sum lbf_mlp_create lbf_mlp_destroy "
            "lbf_mlp_param_count lbf_mlp_init_params lbf_init_params_host lbf_mlp_forward lbf_mlp_loss_grad lbf_mlp_batch_grads lbf_two_loop lbf_dot "
            "lbf_nrm2 lbf_axpy lbf_scal lbf_lbfgs_default_params lbf_slbfgs_default_params lbf_lbfgs_solve "
-           "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_slbfgs_begin lbf_slbfgs_iterate lbf_slbfgs_end lbf_slbfgs_pair0 lbf_prof_enable lbf_prof_select lbf_prof_sample lbf_prof_read lbf_prof_read_work lbf_synth_mnist "
+           "lbf_lbfgs_begin lbf_lbfgs_iterate lbf_lbfgs_end lbf_lbfgs_solve_fn lbf_device_alloc lbf_device_free lbf_memcpy lbf_slbfgs_solve lbf_slbfgs_begin lbf_slbfgs_iterate lbf_slbfgs_end lbf_slbfgs_pair0 lbf_slbfgs_pair_io lbf_prof_enable lbf_prof_select lbf_prof_sample lbf_prof_read lbf_prof_read_work lbf_synth_mnist "
            "lbf_sample_indices lbf_synth_regression lbf_gd_default_params lbf_sgd_default_params lbf_gd_solve "
            "lbf_sgd_solve lbf_idx_read_images lbf_idx_read_labels lbf_mlp_hvp lbf_mlp_fd_hvp lbf_mlp_loss").split()
 

@@ -55,7 +55,7 @@ void check_comm(ncclResult_t r, const char *what) {
 extern "C" {
 
 const char *lbf_last_error(void) { return g_err.c_str(); }
-const char *lbf_version(void) { return "lbfgs_amd 0.3 (gfx950, abi 2)"; }
+const char *lbf_version(void) { return "lbfgs_amd 0.4 (gfx950, abi 3)"; }
 int lbf_abi_version(void) { return LBF_ABI_VERSION; }
 
 int lbf_ctx_create(int device, void *stream, lbf_ctx **out) {
@@ -303,14 +303,42 @@ int lbf_two_loop(lbf_ctx *ctx, long long n, int k, const float *d_S, const float
   return guard([&] {
     LBF_REQUIRE(ctx && d_g && d_dir && n > 0 && k >= 0 && k <= 128, "bad argument");
     LBF_REQUIRE(k == 0 || (d_S && d_Y && h_rho), "history pointers");
-    LBF_REQUIRE(mode >= 0 && mode <= 2, "mode");
+    LBF_REQUIRE(mode >= 0 && mode <= 3, "mode");
     ctx->c.set_device();
     hipStream_t s = ctx->c.stream;
-    const int policy = mode == 0 ? POL_CPU : (mode == 1 ? POL_SLBFGS : POL_CUDA);
-    const double dsign = mode == 1 ? 1.0 : -1.0;
+    const int policy = mode == 0 ? POL_CPU : (mode == 1 || mode == 3 ? POL_SLBFGS : POL_CUDA);
+    const double dsign = mode == 1 || mode == 3 ? 1.0 : -1.0;
     History h(&ctx->c, k, n);
     DevBuf<float> zero{size_t(n)};
     LBF_HIP(hipMemsetAsync(zero.get(), 0, size_t(n) * sizeof(float), s));
+    if (mode == 3) { // the S-LBFGS solver's own route (SlbfgsSolver::epoch_steps)
+      LBF_REQUIRE(k <= DIR_MAXM && n % 4 == 0 && dir_supported(k, n) &&
+                      (reinterpret_cast<uintptr_t>(d_g) & 15u) == 0 && (k == 0 || ((reinterpret_cast<uintptr_t>(d_S) |
+                      reinterpret_cast<uintptr_t>(d_Y)) & 15u) == 0),
+                  "mode 3: k <= 16, n % 4 == 0, 16-B aligned vectors");
+      for (int i = 0; i < k; ++i) { // pair updates: |y.s| > 1e-10, rho = 1 / y.s and the map K on the device
+        GramArgs ga;
+        ga.policy = policy;
+        ga.has_pair = 1;
+        ga.sa = d_S + size_t(i) * n;
+        ga.sb = zero.get();
+        ga.ya = d_Y + size_t(i) * n;
+        ga.yb = zero.get();
+        h.update(ga, 0, 1, dsign);
+      }
+      DevBuf<float> v{size_t(n)};
+      GramArgs gg; // a direction-only step: dir_cols_combine, x_out = 0 + 1 * (+H g)
+      gg.policy = policy;
+      gg.has_g = 1;
+      gg.ga = d_g;
+      gg.g_out = v.get();
+      h.update_combine(gg, 1, dsign, zero.get(), d_dir, nullptr, 1.0);
+      ctx->c.host.ensure(1);
+      LBF_HIP(hipMemcpyAsync(ctx->c.host.get(), h.view().scal + SC_KERR, sizeof(double), hipMemcpyDeviceToHost, s));
+      LBF_HIP(hipStreamSynchronize(s));
+      LBF_REQUIRE(ctx->c.host[0] == 0.0, "mode 3: the coefficient map K is out of step with the ring");
+      return;
+    }
     for (int i = 0; i < k; ++i) {
       GramArgs ga;
       ga.policy = policy;
@@ -585,6 +613,13 @@ int lbf_slbfgs_pair0(lbf_slbfgs *s, float *d_wt, float *d_u, float *d_s, float *
   return guard([&] {
     LBF_REQUIRE(s, "null argument");
     LBF_REQUIRE(s->s->pair0(d_wt, d_u, d_s, d_y), "no curvature-pair candidate traced (pair_trace off, or none yet)");
+  });
+}
+
+int lbf_slbfgs_pair_io(lbf_slbfgs *s, int cap, float *d_rec, const float *d_force) {
+  return guard([&] {
+    LBF_REQUIRE(s && cap >= 0, "bad argument");
+    s->s->pair_io(cap, d_rec, d_force);
   });
 }
 

@@ -393,6 +393,7 @@ __global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const
     sK[r * DIR_KS + c] = a.kmat[r * DIR_KS + c];
   }
   const double gamma = k > 0 ? a.kmat[DIR_KS * DIR_KS] : 1.0;
+  const double kbuilt = a.kmat[DIR_KS * DIR_KS + 1]; // the live count K was built for (slbfgs_kmat)
   if (t < 6 * m + 6) dl[t] = a.dots[t];
   const long long n = h.n;
   const long long e = ((long long)blockIdx.x * 256 + t) * 4;
@@ -401,6 +402,11 @@ __global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const
   const f32x4 g4 = *reinterpret_cast<const f32x4 *>(cb.g + eq);
   const f32x4 x4 = *reinterpret_cast<const f32x4 *>((cb.x_out ? cb.x_in : cb.g) + eq);
   lds_barrier();
+  // K's layout depends on the count it was built for: a map out of step with the ring (no pair update since the
+  // count changed, which the solver's order rules out) must not be applied. The step then writes NaN (x_out, dir)
+  // and block 0 raises SC_KERR, which the solver checks at the epoch's end and fails on.
+  const bool kbad = k > 0 && kbuilt != double(k);
+  if (kbad && blockIdx.x == 0 && t == 0) h.scal[SC_KERR] = 1.0;
   // ---- round trip 2: this lane's quads of the live history vectors, in flight through the mat-vec ----
   f32x4 sv[KQ], yv[KQ];
   if (k > 0)
@@ -446,7 +452,7 @@ __global__ __launch_bounds__(256) void dir_combine_kernel(const DirArgs a, const
   }
   lds_barrier();
   // ---- combine (combine_small's arithmetic per element) ----
-  const double cg = cf[2 * MM];
+  const double cg = kbad ? __builtin_nan("") : cf[2 * MM];
   const double alpha = cb.alpha;
   if (full) {
     f32x4 d4, o4;

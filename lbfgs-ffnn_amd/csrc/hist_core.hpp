@@ -150,7 +150,7 @@ __device__ __forceinline__ double slbfgs_gamma(double ys, double yy) {
 // update (lane j: column j of R^-1 by back substitution, then column j of M R^-1 and of R^-T M R^-1; no
 // cross-lane dependency), and every direction-only step's combine blocks do ONE 2k x 2k mat-vec instead of
 // the two k-step recurrences (dir_combine_kernel). Operands from LDS: sy = SY of the live pairs (k x k, row
-// stride k), yyl = YY, rho_l; rinv: DIR_MAXM^2 doubles of LDS; K: global, row stride DIR_KS, gamma after it.
+// stride k), yyl = YY, rho_l; rinv: DIR_MAXM^2 doubles of LDS; K: global, row stride DIR_KS, then gamma and k.
 __device__ inline void slbfgs_kmat(int k, int lane, const double *rho_l, const double *sy, const double *yyl,
                                    double *rinv, double *K) {
   constexpr int KM = DIR_MAXM;
@@ -203,7 +203,10 @@ __device__ inline void slbfgs_kmat(int k, int lane, const double *rho_l, const d
         K[(k + i) * DIR_KS + k + j] = 0.0;
       }
   }
-  if (lane == 0) K[DIR_KS * DIR_KS] = gamma;
+  if (lane == 0) {
+    K[DIR_KS * DIR_KS] = gamma;
+    K[DIR_KS * DIR_KS + 1] = double(k); // the layout depends on k: dir_combine checks it against the ring's count
+  }
 }
 
 // Barriers here are LDS-only (wave.hpp lds_barrier): within a history step no thread reads global

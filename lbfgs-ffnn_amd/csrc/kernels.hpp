@@ -288,6 +288,7 @@ enum {
   SC_SSE = 12,    //                  local sum of squared errors (before reduction over ranks)
   SC_FOLD = 13,   // speculative line search: loss of the last accepted iterate (fp64, Wolfe)
   SC_FOLDF = 14,  //                          same, as the fp32 value the Armijo test uses
+  SC_KERR = 15,   // S-LBFGS: a direction step found the coefficient map K built for another live count (sticky)
   SC_N = 16
 };
 
@@ -401,7 +402,7 @@ int tail_vpw(int m);                                // vectors per wave of the G
 // block per Gram column whose last arrival runs the history step (hist_core.hpp) from the column sums.
 constexpr int DIR_MAXM = 16;
 // The S-LBFGS direction's coefficient map K ([cS; cY] = K [S^T g; Y^T g], hist_core.hpp slbfgs_kmat): row stride
-// DIR_KS, then gamma at [DIR_KS * DIR_KS]
+// DIR_KS, then gamma at [DIR_KS * DIR_KS] and the live count k it was built for at [DIR_KS * DIR_KS + 1]
 constexpr int DIR_KS = 2 * DIR_MAXM;
 constexpr int DIR_KMAT_N = DIR_KS * DIR_KS + 4;
 constexpr long long DIR_MAXN = 1LL << 22;

@@ -921,6 +921,17 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
       int slots[64];
       for (int i = 0; i < wh_count_; ++i) slots[i] = wh_slot(i);
       average_slots(s, n_, wh_.get(), ld, slots, wh_count_, u_.get());
+      // diagnostics (lbf_slbfgs_pair_io): this event's record [w_{t+1} | u | g+ | g-] and forced inputs
+      const int ev = nev_++;
+      float *pr = pio_rec_ && ev < pio_cap_ ? pio_rec_ + size_t(ev) * 4 * size_t(ld) : nullptr;
+      const float *pf = pio_force_ && ev < pio_cap_ ? pio_force_ + size_t(ev) * 4 * size_t(ld) : nullptr;
+      const size_t nb = size_t(n_) * sizeof(float);
+      if (pr) {
+        LBF_HIP(hipMemcpyAsync(pr, wt_.get(), nb, hipMemcpyDeviceToDevice, s));
+        LBF_HIP(hipMemcpyAsync(pr + ld, u_.get(), nb, hipMemcpyDeviceToDevice, s));
+        LBF_HIP(hipMemsetAsync(pr + 2 * ld, 0, 2 * nb + 2 * (size_t(ld) - size_t(n_)) * sizeof(float), s));
+      }
+      if (pf) LBF_HIP(hipMemcpyAsync(u_.get(), pf + ld, nb, hipMemcpyDeviceToDevice, s));
       if (have_u_) {
         const Slice &hs = hb[t];
         const double eps = prm_.fd_eps;
@@ -941,6 +952,14 @@ void SlbfgsSolver::epoch_steps(const EpochDraw &d) {
           lincomb(s, n_, u_.get(), -eps, s_.get(), wm_.get());
           eval_pair(wp_.get(), wm_.get(), fdpair_.get(), hs.off, hs.cnt, 1.0 / double(hs.total));
           pa.yscale = 1.0 / (2.0 * eps);
+        }
+        if (pr) {
+          LBF_HIP(hipMemcpyAsync(pr + 2 * ld, gp, nb, hipMemcpyDeviceToDevice, s));
+          LBF_HIP(hipMemcpyAsync(pr + 3 * ld, gm, nb, hipMemcpyDeviceToDevice, s));
+        }
+        if (pf) {
+          LBF_HIP(hipMemcpyAsync(gp, pf + 2 * ld, nb, hipMemcpyDeviceToDevice, s));
+          LBF_HIP(hipMemcpyAsync(gm, pf + 3 * ld, nb, hipMemcpyDeviceToDevice, s));
         }
         pa.ya = gp;
         pa.yb = gm;
@@ -1063,6 +1082,9 @@ int SlbfgsSolver::iterate(int epochs, lbf_record *rec) {
     }
     read();
     if (repl_ && nr > 1) replica_check();
+    if (hs_[SC_KERR] != 0.0) // dir_combine_kernel's check of the coefficient map against the ring's live count
+      throw Error(LBF_ERR_STATE, "S-LBFGS: a direction step found the coefficient map K out of step with the "
+                                 "history ring's live count (epoch " + std::to_string(iters_) + ")");
     mu_valid_ = true;
     last_loss_ = hs_[SC_LOSS];
     last_gnorm_ = std::sqrt(hs_[SC_TGG]);

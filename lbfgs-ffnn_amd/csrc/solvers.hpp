@@ -180,8 +180,19 @@ public:
   // copies the first traced curvature-pair candidate's iterate w_t, average u, s and y (n floats each);
   // false when no candidate was traced yet
   bool pair0(float *wt, float *u, float *s, float *y) const;
+  // Diagnostics (lbf_slbfgs_pair_io): at curvature event e (each inner step t > 0 with t % L == 0, the first,
+  // which offers no pair, included) record [w_{t+1} | u | g(u + eps s) | g(u - eps s)] into rec + 4 e ld, and
+  // force u, g(u + eps s), g(u - eps s) to force + 4 e ld's before use (ld = round4(n); NULL: off)
+  void pair_io(int cap, float *rec, const float *force) {
+    pio_cap_ = cap;
+    pio_rec_ = rec;
+    pio_force_ = force;
+  }
 
 private:
+  int pio_cap_ = 0, nev_ = 0;
+  float *pio_rec_ = nullptr;
+  const float *pio_force_ = nullptr;
   struct Slice {
     long long off = 0, cnt = 0, total = 0; // offset / count in this rank's flat list, whole batch size
   };

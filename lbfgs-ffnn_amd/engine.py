@@ -74,7 +74,8 @@ class Context:
     def two_loop(self, S: Optional[torch.Tensor], Y: Optional[torch.Tensor], rho: Sequence[float],
                  g: torch.Tensor, mode: int = 0) -> torch.Tensor:
         """Two-loop recursion on an explicit history (logical order, oldest first).
-        mode 0: CPU semantics (returns -Hg), 1: S-LBFGS (+Hg), 2: CUDA (-Hg)."""
+        mode 0: CPU semantics (returns -Hg), 1: S-LBFGS (+Hg), 2: CUDA (-Hg), 3: S-LBFGS through the solver's pair
+        updates and direction-only step (rho computed on the device, `rho` ignored)."""
         k = 0 if S is None else int(S.shape[0])
         out = torch.empty_like(g)
         rho_arr = (C.c_double * max(k, 1))(*[float(r) for r in rho]) if k else None
@@ -407,6 +408,21 @@ class SlbfgsRun:
         out = [torch.empty(n, dtype=torch.float32, device=self._keep[1].device) for _ in range(4)]
         check(lib().lbf_slbfgs_pair0(self.h, *[ptr(t) for t in out]), "lbf_slbfgs_pair0")
         return out
+
+    def pair_io(self, cap: int, record: bool = True, force: Optional[torch.Tensor] = None):
+        """Teacher forcing of the curvature pairs (lbf_slbfgs_pair_io; call before iterate). Returns the record
+        tensor [cap, 4, ld] ([w_{t+1} | u | g(u + eps s) | g(u - eps s)] per curvature event) or None; `force`
+        (same shape, e.g. another run's record) replaces u and the two gradients of each event."""
+        n = int(self._keep[1].numel())
+        ld = (n + 3) & ~3
+        dev = self._keep[1].device
+        rec = torch.zeros((int(cap), 4, ld), dtype=torch.float32, device=dev) if record else None
+        if force is not None:
+            if tuple(force.shape) != (int(cap), 4, ld):
+                raise LbfError(f"force: expected shape {(int(cap), 4, ld)}, got {tuple(force.shape)}")
+        self._pio = (rec, force)  # kept alive while the solver may write / read them
+        check(lib().lbf_slbfgs_pair_io(self.h, int(cap), ptr(rec), ptr(force)), "lbf_slbfgs_pair_io")
+        return rec
 
     def close(self):
         if self.h:

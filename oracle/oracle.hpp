@@ -622,9 +622,10 @@ inline std::vector<size_t> sample_minibatch_indices(size_t N, size_t b, std::mt1
 
 // finite_difference_hvp_batch (s_lbfgs.hpp:88-101): y = (g_S(w + eps v) - g_S(w - eps v)) / (2 eps) on the
 // Hessian batch S, eps = 1e-4 (:90).
-template <class T, class BG>
+// hook(gp, gm) (diagnostics, PairIO below) may read or replace the two gradients before the difference.
+template <class T, class BG, class Hook>
 Vec<T> finite_difference_hvp_batch(BG &&batch_g, const Vec<T> &w, const Vec<T> &v, const std::vector<size_t> &S,
-                                   double eps) {
+                                   double eps, Hook &&hook) {
   const size_t n = w.size();
   Vec<T> wp(n), wm(n), gp(n, T(0)), gm(n, T(0)), y(n);
   for (size_t j = 0; j < n; ++j) {
@@ -633,9 +634,24 @@ Vec<T> finite_difference_hvp_batch(BG &&batch_g, const Vec<T> &w, const Vec<T> &
   }
   batch_g(wp, S, gp);
   batch_g(wm, S, gm);
+  hook(gp, gm);
   for (size_t j = 0; j < n; ++j) y[j] = (gp[j] - gm[j]) / T(2.0 * eps);
   return y;
 }
+template <class T, class BG>
+Vec<T> finite_difference_hvp_batch(BG &&batch_g, const Vec<T> &w, const Vec<T> &v, const std::vector<size_t> &S,
+                                   double eps) {
+  return finite_difference_hvp_batch<T>(batch_g, w, v, S, eps, [](Vec<T> &, Vec<T> &) {});
+}
+
+// Diagnostics (test only; the device's lbf_slbfgs_pair_io): at curvature event e (each t > 0 with t % L == 0, the
+// first included) record [w_{t+1} | u | g(u + eps s) | g(u - eps s)] (n doubles each, the gradients zero at the
+// first event) into rec + 4 e n, and replace u and the two gradients by force + 4 e n's before use.
+struct PairIO {
+  double *rec = nullptr;
+  const double *force = nullptr;
+  int cap = 0;
+};
 
 struct SlbfgsParams {
   int max_iters = 1000; // epochs
@@ -651,7 +667,9 @@ struct SlbfgsParams {
 template <class T, class BG, class BF>
 Vec<T> slbfgs(Vec<T> weights, BG &&batch_g, BF &&batch_f, const SlbfgsParams &prm, std::vector<IterRecord> *rec,
               int *iters_out, std::vector<std::vector<size_t>> *sampled = nullptr,
-              std::vector<std::array<double, 8>> *pairs = nullptr, std::vector<double> *pair0_us = nullptr) {
+              std::vector<std::array<double, 8>> *pairs = nullptr, std::vector<double> *pair0_us = nullptr,
+              const PairIO *pio = nullptr) {
+  int nev = 0;
   const size_t n = weights.size();
   const int M = prm.M;
   Ring<Vec<T>> u_list(M > 0 ? M + 1 : 0), s_list(M > 0 ? M : 0), y_list(M > 0 ? M : 0);
@@ -686,13 +704,37 @@ Vec<T> slbfgs(Vec<T> weights, BG &&batch_g, BF &&batch_f, const SlbfgsParams &pr
           for (size_t j = 0; j < n; ++j) u[j] += w_hist[i][j];
         if (nw > 0)
           for (size_t j = 0; j < n; ++j) u[j] /= T(nw);
+        const int ev = nev++;
+        double *pr = pio && pio->rec && ev < pio->cap ? pio->rec + size_t(ev) * 4 * n : nullptr;
+        const double *pf = pio && pio->force && ev < pio->cap ? pio->force + size_t(ev) * 4 * n : nullptr;
+        if (pr) {
+          for (size_t j = 0; j < n; ++j) {
+            pr[j] = double(wt[j]);
+            pr[n + j] = double(u[j]);
+            pr[2 * n + j] = pr[3 * n + j] = 0.0;
+          }
+        }
+        if (pf)
+          for (size_t j = 0; j < n; ++j) u[j] = T(pf[n + j]);
         if (!u_list.empty()) {
           const Vec<T> &up = u_list.back();
           Vec<T> s(n);
           for (size_t j = 0; j < n; ++j) s[j] = u[j] - up[j];
           auto hb = sample_minibatch_indices(size_t(prm.N), size_t(prm.b_H), rng);
           if (sampled) sampled->push_back(hb);
-          Vec<T> y = finite_difference_hvp_batch<T>(batch_g, u, s, hb, 1e-4);
+          Vec<T> y = (pr || pf) ? finite_difference_hvp_batch<T>(batch_g, u, s, hb, 1e-4, [&](Vec<T> &gp, Vec<T> &gm) {
+            for (size_t j = 0; j < n; ++j) {
+              if (pr) {
+                pr[2 * n + j] = double(gp[j]);
+                pr[3 * n + j] = double(gm[j]);
+              }
+              if (pf) {
+                gp[j] = T(pf[2 * n + j]);
+                gm[j] = T(pf[3 * n + j]);
+              }
+            }
+          })
+                                           : finite_difference_hvp_batch<T>(batch_g, u, s, hb, 1e-4);
           if (pair0_us && pair0_us->empty()) { // diagnostics: the first candidate's w_t, u, s, y (fp64 copies)
             pair0_us->assign(wt.begin(), wt.end());
             pair0_us->insert(pair0_us->end(), u.begin(), u.end());

@@ -63,7 +63,7 @@ def lib():
         L.oracle_slbfgs_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_int, C.c_double,
                                         C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, _dp,
                                         C.POINTER(C.c_int), C.c_void_p, C.c_longlong, C.c_void_p, C.c_int,
-                                        C.POINTER(C.c_int), C.c_void_p]
+                                        C.POINTER(C.c_int), C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_gd_mlp.restype = C.c_int
         L.oracle_gd_mlp.argtypes = [C.c_int, _ip, _ip, _dp, _dp, _dp, C.c_longlong, C.c_double, C.c_double, C.c_int,
                                     C.c_double, C.c_int, _dp]
@@ -192,11 +192,13 @@ class Net:
         return P, rec[:n]
 
     def slbfgs(self, P, X, Y, epochs=2, tol=0.0, M=10, L=10, b=32, bH=16, step=0.02, lam=1e-4, fp32=False,
-               want_idx=False, pair_trace=0, pair0=None):
+               want_idx=False, pair_trace=0, pair0=None, pio_rec=None, pio_force=None):
         """Returns (params, rec, idx) or, with pair_trace > 0, (params, rec, idx, pairs): one row per curvature
         pair candidate (epoch, t, y.s, s.s, y.y, accepted, live pairs, 0), as the device's pair trace.
         pair0: an fp64 array of 4 * nparams receiving the first candidate's iterate w_t (after step t), the
-        iterate average u, s = u - u_prev and y (diagnostics; lbf_slbfgs_pair0 on the device)."""
+        iterate average u, s = u - u_prev and y (diagnostics; lbf_slbfgs_pair0 on the device).
+        pio_rec / pio_force: fp64 arrays [cap, 4, nparams], the curvature events' record [w_{t+1} | u | g+ | g-] and
+        the teacher forcing of u, g+, g- (PairIO in oracle.hpp; lbf_slbfgs_pair_io on the device)."""
         P = np.array(P, np.float64, copy=True)
         rec = np.zeros((epochs, 6), np.float64)
         it = C.c_int(0)
@@ -209,11 +211,18 @@ class Net:
             idx = np.full(cap, -1, np.int64)
         pairs = np.zeros((max(int(pair_trace), 1), 8), np.float64)
         npairs = C.c_int(0)
+        cap_io = 0
+        for a in (pio_rec, pio_force):
+            if a is not None:
+                assert a.dtype == np.float64 and a.flags.c_contiguous and a.ndim == 3 and a.shape[1:] == (4, P.size)
+                cap_io = a.shape[0] if cap_io == 0 else min(cap_io, a.shape[0])
         lib().oracle_slbfgs_mlp(self.nl, self.dims, self.acts, P, np.ascontiguousarray(X, np.float64),
                                 np.ascontiguousarray(Y, np.float64), N, epochs, tol, M, L, b, bH, step, lam, int(fp32),
                                 rec, C.byref(it), idx.ctypes.data if want_idx else None, cap,
                                 pairs.ctypes.data if pair_trace > 0 else None, int(pair_trace), C.byref(npairs),
-                                pair0.ctypes.data if pair0 is not None else None)
+                                pair0.ctypes.data if pair0 is not None else None, cap_io,
+                                pio_rec.ctypes.data if pio_rec is not None else None,
+                                pio_force.ctypes.data if pio_force is not None else None)
         if want_idx:
             idx = idx[idx >= 0]
         if pair_trace > 0:

@@ -131,7 +131,7 @@ template <class T>
 int run_slbfgs_mlp(const Net &net, double *params, const double *X, const double *Y, int64_t N, int epochs,
                    double tol, int M, int L, int b, int bH, double step, double lambda, double *rec_out, int *iters,
                    int64_t *idx_out, int64_t idx_cap, double *pair_out, int pair_cap, int *npairs,
-                   double *pair0_us) {
+                   double *pair0_us, const PairIO *pio) {
   std::vector<T> Xt = to_vec<T>(X, size_t(N) * net.dims[0]);
   std::vector<T> Yt = to_vec<T>(Y, size_t(N) * net.dims.back());
   MLPObjective<T> obj{&net, Xt.data(), Yt.data(), N, {}, 0, 0};
@@ -167,7 +167,7 @@ int run_slbfgs_mlp(const Net &net, double *params, const double *X, const double
   std::vector<std::array<double, 8>> pairs;
   std::vector<double> us;
   Vec<T> w = slbfgs<T>(to_vec<T>(params, net.nparams), bg, bf, prm, &rec, iters, idx_out ? &sampled : nullptr,
-                       pair_out ? &pairs : nullptr, pair0_us ? &us : nullptr);
+                       pair_out ? &pairs : nullptr, pair0_us ? &us : nullptr, pio);
   if (pair0_us && !us.empty()) std::copy(us.begin(), us.end(), pair0_us);
   if (pair_out) {
     int k = 0;
@@ -318,17 +318,26 @@ int oracle_lbfgs_armijo_mlp(int nl, const int *dims, const int *acts, double *pa
   return run_armijo_mlp<double>(net, params, X, Y, N, m, max_iters, tol, max_ls, c1, rho, rec, iters);
 }
 
-// S-LBFGS on the MLP (CPU semantics, fp64). idx_out (optional) receives every sampled index list in order.
+// S-LBFGS on the MLP (CPU semantics, fp64). idx_out (optional) receives every sampled index list in order;
+// pio_rec / pio_force (optional, pio_cap events of 4 x nparams doubles): the pair record / teacher forcing (PairIO).
 int oracle_slbfgs_mlp(int nl, const int *dims, const int *acts, double *params, const double *X, const double *Y,
                       long long N, int epochs, double tol, int M, int L, int b, int bH, double step, double lambda,
                       int fp32, double *rec, int *iters, long long *idx_out, long long idx_cap, double *pair_out,
-                      int pair_cap, int *npairs, double *pair0_us) {
+                      int pair_cap, int *npairs, double *pair0_us, int pio_cap, double *pio_rec,
+                      const double *pio_force) {
   Net net(dims, acts, nl);
+  PairIO pio;
+  pio.rec = pio_rec;
+  pio.force = pio_force;
+  pio.cap = pio_cap;
+  const PairIO *pp = (pio_rec || pio_force) ? &pio : nullptr;
   if (fp32)
     return run_slbfgs_mlp<float>(net, params, X, Y, N, epochs, tol, M, L, b, bH, step, lambda, rec, iters,
-                                 reinterpret_cast<int64_t *>(idx_out), idx_cap, pair_out, pair_cap, npairs, pair0_us);
+                                 reinterpret_cast<int64_t *>(idx_out), idx_cap, pair_out, pair_cap, npairs, pair0_us,
+                                 pp);
   return run_slbfgs_mlp<double>(net, params, X, Y, N, epochs, tol, M, L, b, bH, step, lambda, rec, iters,
-                                reinterpret_cast<int64_t *>(idx_out), idx_cap, pair_out, pair_cap, npairs, pair0_us);
+                                reinterpret_cast<int64_t *>(idx_out), idx_cap, pair_out, pair_cap, npairs, pair0_us,
+                                pp);
 }
 
 // GD (gd.cuh:38-106) / SGD (sgd.cuh:50-153) with momentum on the MLP. rec: 2 doubles per record.

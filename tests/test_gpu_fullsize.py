@@ -148,6 +148,7 @@ def test_cfg3_loss_grad_full_size(ctx, pkg, O, mnist, N):
 
 
 CFG4_KW = dict(M=10, L=10, b=256, b_H=128, step=0.005)
+N_EVENTS = 24  # curvature events of one cfg-4 epoch: t = 10, 20, ..., 230 (23), one spare row
 
 
 @pytest.fixture(scope="module")
@@ -160,9 +161,11 @@ def cfg4_epoch(ctx, pkg, O, mnist):
     P = net.init_params(123, "cpu")
     P0 = host(P)
     run = pkg.SlbfgsRun(net, P, X, Y, pair_trace=64, tol=0.0, lam=1e-4, **CFG4_KW)
+    pio = run.pair_io(N_EVENTS)  # record only: the run is bitwise the plain solve (checked below)
     info = run.iterate(1)
     hist, pairs = run.hist.as_dict(), run.pairs().copy()
     p0 = [host(t) for t in run.pair0()]
+    pio = pio[:, :, :P0.size].cpu().numpy()
     run.close()
     onet = O.Net(dims, acts)
     okw = dict(epochs=1, tol=0.0, M=10, L=10, b=256, bH=128, step=0.005, lam=1e-4, pair_trace=64)
@@ -171,7 +174,7 @@ def cfg4_epoch(ctx, pkg, O, mnist):
     _, rec32, _, pairs32 = onet.slbfgs(P0, X64, Y64, fp32=True, pair0=o32, **okw)
     return dict(net=net, P0=P0, P=P, hist=hist, info=info, pairs=pairs, p0=p0, rec=rec, rec32=rec32,
                 pairs64=pairs64, pairs32=pairs32, o64=o64.reshape(4, -1), o32=o32.reshape(4, -1),
-                l0=float(onet.loss(P0, X64, Y64)), onet=onet, idx64=idx64)
+                l0=float(onet.loss(P0, X64, Y64)), onet=onet, idx64=idx64, pio=pio)
 
 
 def test_cfg4_slbfgs_first_pair_full_size(mnist, cfg4_epoch):
@@ -332,3 +335,52 @@ def test_fd_hvp_matches_oracle_cfg4(ctx, pkg, O, mnist):
     # oracle's own fp64 quotient differs from H(u) s by ~30 % on this batch)
     # the device FD y is what the S-LBFGS pair sweep stores: y.s > 0 along a descent pair
     assert float((y.double() * s.double()).sum()) > 0
+
+
+def test_cfg4_slbfgs_epoch_forced_pairs_full_size(ctx, pkg, O, mnist, cfg4_epoch):
+    """The whole cfg-4 ReLU epoch against the fp64 oracle in a form rounding-level chaos cannot absorb (VERDICT r05
+    item 1). The epoch is chaotic only through its curvature pairs: y = (g(u + eps s) - g(u - eps s)) / (2 eps)
+    amplifies a rounding-level move of u across a ReLU kink by 1/(2 eps), and the ring passes that
+    on to every later direction. Teacher forcing (lbf_slbfgs_pair_io, oracle PairIO) takes that channel away: the
+    fp64 oracle runs the epoch with the device's u and the device's two FD gradients at each of the 23 curvature
+    events, so its ring holds the device's pairs while its iterates stay its own (s_lbfgs.hpp:218-262 unchanged).
+    Checked, all at fixed bounds:
+      (a) every pair's two batch gradients against the fp64 oracle AT THE SAME POINTS fl32(u +- eps s) on the same
+          128-row Hessian batch: 1e-4, as every full-size gradient test (22 pairs, not only the first);
+      (b) the device's iterate w_{t+1} at every event against the forced oracle's: 1e-4 (the SVRG chain itself,
+          234 steps of fp32 against fp64 under the same history);
+      (c) the recorded epoch loss at the picked anchor against the forced oracle's: 1e-4;
+      (d) the same live-pair count (the pairs' acceptance |y.s| > 1e-10, s_lbfgs.hpp:245-256, on fp32 vs fp64).
+    The unforced epoch (5 % bound, test_cfg4_slbfgs_one_epoch_full_size) stays beside it."""
+    _, _, X64, Y64, X, Y = mnist
+    r = cfg4_epoch
+    D = r["pio"].astype(np.float64)
+    ne = 23
+    assert not D[ne:].any() and D[:ne, 0].any()  # 23 events recorded, the spare row untouched
+    assert not D[0, 2:].any() and all(D[e, 2].any() for e in range(1, ne))  # the first event offers no pair
+    Ro = np.zeros_like(D)
+    _, rec_f, _ = r["onet"].slbfgs(r["P0"], X64, Y64, epochs=1, tol=0.0, M=10, L=10, b=256, bH=128, step=0.005,
+                                   lam=1e-4, pio_rec=Ro, pio_force=np.ascontiguousarray(D))
+    eps = 1e-4
+    f32 = lambda a: a.astype(np.float32).astype(np.float64)  # noqa: E731
+    eg, ew = [], []
+    for e in range(1, ne):
+        t = 10 * (e + 1)
+        u, up = D[e, 1], D[e - 1, 1]
+        s = f32(u - up)
+        hb = r["idx64"][256 * (t + 1) + 128 * (e - 1): 256 * (t + 1) + 128 * e]
+        _, gp = r["onet"].loss_grad(f32(u + eps * s), X64, Y64, idx=hb, lam=1e-4)
+        _, gm = r["onet"].loss_grad(f32(u - eps * s), X64, Y64, idx=hb, lam=1e-4)
+        eg.append(max(rel(D[e, 2], gp), rel(D[e, 3], gm)))
+    ew = [rel(D[e, 0], Ro[e, 0]) for e in range(ne)]
+    dl = abs(r["hist"]["loss"][0] - rec_f[0, 0]) / abs(rec_f[0, 0])
+    print("forced cfg-4 epoch: pair gradients at the same points vs fp64 max %.2e (per pair: %s)"
+          % (max(eg), " ".join(f"{x:.1e}" for x in eg)))
+    print("forced cfg-4 epoch: iterate w_t+1 vs the forced fp64 oracle max %.2e (per event: %s)"
+          % (max(ew), " ".join(f"{x:.1e}" for x in ew)))
+    print(f"forced cfg-4 epoch loss: device {r['hist']['loss'][0]:.9f} forced fp64 oracle {rec_f[0, 0]:.9f}: {dl:.2e}; "
+          f"unforced fp64 oracle {r['rec'][0, 0]:.9f}")
+    assert max(eg) <= 1e-4, eg
+    assert max(ew) <= 1e-4, ew
+    assert dl <= 1e-4, dl
+    assert int(r["hist"]["accepted"][0]) == int(rec_f[0, 3])

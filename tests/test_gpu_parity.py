@@ -167,6 +167,32 @@ def test_two_loop_matches_oracle(ctx, O, mode, k, n):
     assert rel(host(out), ref) <= DIR_RTOL
 
 
+@pytest.mark.parametrize("k", [1, 2, 5, 10, 16])
+@pytest.mark.parametrize("near", [False, True], ids=["plain", "ys_near_threshold"])
+def test_two_loop_kmat_route_matches_recurrences(ctx, O, k, near):
+    """The S-LBFGS solver's direction-only step takes its coefficients from the map K that the last pair update
+    built (compact form, an explicit R^-1; dir_combine_kernel), not from the two-loop recurrences. The same ring
+    through that route (lbf_two_loop mode 3: each pair offered through the solver's pair update, then one
+    direction-only step) against the recurrences (mode 1, dir_fin / hist_core) and the fp64 oracle's two-loop of
+    s_lbfgs.hpp:106-136, at every live count the route supports; `ys_near_threshold` makes one middle pair's
+    y.s = 3e-10, just above the acceptance threshold |y.s| > 1e-10 (s_lbfgs.hpp:245-256), so rho = 3.3e9 enters
+    R^-1. The route also checks that K was built for the ring's live count (SC_KERR)."""
+    n = 100000
+    S, Yv, rho, g = make_history(n, k, seed=3 * k + int(near))
+    if near:
+        j = k // 2
+        Yv[j] = (Yv[j] * (3e-10 / float(S[j] @ Yv[j]))).astype(np.float32).astype(np.float64)
+        rho = 1.0 / np.einsum("ij,ij->i", S, Yv)
+        assert 1e-10 < 1.0 / rho[j] < 1e-9
+    ref = O.two_loop(1, S, Yv, rho, g)
+    out1 = ctx.two_loop(dev(S), dev(Yv), rho, dev(g), mode=1)
+    out3 = ctx.two_loop(dev(S), dev(Yv), rho, dev(g), mode=3)
+    e31, e3, e1 = rel(host(out3), host(out1)), rel(host(out3), ref), rel(host(out1), ref)
+    print(f"k {k} near {near}: K route vs recurrences {e31:.2e}, vs oracle {e3:.2e} (recurrences {e1:.2e})")
+    assert e3 <= DIR_RTOL and e1 <= DIR_RTOL
+    assert e31 <= DIR_RTOL
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("k", [5, 48])
 def test_two_loop_large_n(ctx, O, mode, k):

@@ -371,3 +371,97 @@ def test_ranks_cfg4_tanh_epoch(ctx, pkg, dp_mode):
     print(f"cfg4 tanh epoch, world 2 {dp_mode}: loss {h['loss'][0]:.8f} single route {h1['loss'][0]:.8f}: {d:.2e}")
     assert h["accepted"][0] == h1["accepted"][0]
     assert d <= 2e-2, d
+
+
+def _forced_routes(ctx, pkg, dims, acts, X, Y, args, world, cap, seed=123):
+    """The single route records its curvature events (lbf_slbfgs_pair_io); then the world-`world` rank group runs
+    the same solve teacher-forced with that record (its ring receives the single route's pairs, its iterates and
+    its FD gradients at the forced points stay its own) and records too. Returns (single, ranks) as
+    (history, record [cap, 4, n] on the host, params)."""
+    net1 = pkg.Mlp(ctx, dims, acts)
+    P0 = net1.init_params(seed, "cpu")
+    n = P0.numel()
+    run1 = pkg.SlbfgsRun(net1, P0.clone(), X, Y, **args)
+    rec1 = run1.pair_io(cap)
+    run1.iterate(args.get("max_epochs", 1))
+    single = (run1.hist.as_dict(), rec1[:, :, :n].double().cpu().numpy(), run1._keep[1].clone())
+    run1.close()
+
+    def body(r, c):
+        net = pkg.Mlp(c, dims, acts)
+        P = P0.clone()
+        run = pkg.SlbfgsRun(net, P, X, Y, **args)
+        rec = run.pair_io(cap, force=rec1)
+        run.iterate(args.get("max_epochs", 1))
+        out = run.hist.as_dict(), rec[:, :, :n].double().cpu().numpy(), P
+        run.close()
+        return out
+
+    return single, run_ranks(pkg, world, body)
+
+
+@pytest.mark.parametrize("dp_mode", ["sliced", "replicated"])
+def test_ranks_cfg4_epoch_forced_pairs(ctx, pkg, dp_mode):
+    """The world-2 ReLU cfg-4 epoch (784-512-256-10, N = 60000, b = 256, b_H = 128, L = M = 10) against the single
+    route over the WHOLE epoch, in a form the FD pairs' kink chaos cannot absorb. The world-2
+    route is teacher-forced with the single route's curvature events (u and the two FD gradients of each of the 23
+    events, lbf_slbfgs_pair_io): its ring then holds the single route's 22 pairs, while each event's gradients are
+    still evaluated by the world-2 route at the (forced, so identical) points u +- eps s, and its iterates are its
+    own. Checked at fixed bounds:
+      - each pair's two FD gradients at the same points: sliced, the ranks' Hessian-batch slices summed by the
+        all-reduce, 1e-5 (the shard-sum tolerance); replicated, the pair evaluations run inside the rank-local
+        chain, so bitwise;
+      - the iterate w_{t+1} at every event and the own average u: 1e-4 of the single route (sliced: every
+        minibatch gradient summed across ranks; replicated: only the full-batch anchor gradient is);
+      - the epoch loss: 1e-4; the same live-pair count; ranks bitwise identical.
+    The unforced ReLU epoch's distance stays printed in test_ranks_cfg4_epoch."""
+    dims, acts, N, world = [784, 512, 256, 10], ["relu", "relu", "linear"], 60000, 2
+    Xh, Yh = pkg.synth_mnist(N)
+    X, Y = dev(Xh), dev(Yh)
+    args = dict(M=10, L=10, b=256, b_H=128, step=0.005, tol=0.0, lam=1e-4, dp_mode=dp_mode, max_epochs=1)
+    (h1, R1, _), res = _forced_routes(ctx, pkg, dims, acts, X, Y, args, world, 24)
+    assert torch.equal(res[0][2], res[1][2]) and np.array_equal(res[0][1], res[1][1])
+    h, R = res[0][0], res[0][1]
+    ne = 23
+    eg = [max(rel(R[e, 2], R1[e, 2]), rel(R[e, 3], R1[e, 3])) for e in range(1, ne)]
+    ew = [rel(R[e, 0], R1[e, 0]) for e in range(ne)]
+    eu = [rel(R[e, 1], R1[e, 1]) for e in range(ne)]
+    dl = abs(h["loss"][0] - h1["loss"][0]) / abs(h1["loss"][0])
+    print(f"forced cfg4 epoch, world 2 {dp_mode}: FD gradients at the same points max {max(eg):.2e}; iterate max "
+          f"{max(ew):.2e} (last {ew[-1]:.2e}); u max {max(eu):.2e}; epoch loss {h['loss'][0]:.9f} single "
+          f"{h1['loss'][0]:.9f}: {dl:.2e}")
+    if dp_mode == "replicated":
+        assert max(eg) == 0.0, eg
+    else:
+        assert max(eg) <= 1e-5, eg
+    assert max(ew) <= 1e-4 and max(eu) <= 1e-4, (ew, eu)
+    assert dl <= 1e-4, dl
+    assert h["accepted"][0] == h1["accepted"][0]
+
+
+@pytest.mark.parametrize("hvp_exact", [0, 1])
+def test_ranks_fd_pairs_empty_slice_forced(ctx, pkg, hvp_exact):
+    """b_H = 1 < world = 2, sliced: rank 1's slice of every Hessian batch is EMPTY, so each
+    curvature pair is one rank's one-row evaluation plus an empty one, summed by the all-reduce, with lambda w added
+    once after it. Teacher-forced with the single route's events, each pair's gradients (the reference's finite
+    difference, hvp_exact = 0; and the exact HVP) are compared with the single route's AT THE SAME POINTS, every pair
+    of two epochs: within 1e-6 (a sum with zeros in another order); the iterates under the same history within 1e-4."""
+    dims, acts, N, world = [784, 16, 10], ["relu", "linear"], 512, 2
+    Xh, Yh = pkg.synth_mnist(N)
+    X, Y = dev(Xh), dev(Yh)
+    args = dict(M=5, L=4, b=32, b_H=1, step=0.02, tol=0.0, lam=1e-4, dp_mode="sliced", max_epochs=2,
+                hvp_exact=hvp_exact)
+    cap = 2 * (N // 32 // 4) + 2
+    (h1, R1, _), res = _forced_routes(ctx, pkg, dims, acts, X, Y, args, world, cap)
+    assert torch.equal(res[0][2], res[1][2])
+    h, R = res[0][0], res[0][1]
+    ev = [e for e in range(cap) if R1[e, 2].any()]
+    assert len(ev) == 2 * (N // 32 // 4) - 1  # every event but the first offers a pair
+    eg = [max(rel(R[e, 2], R1[e, 2]), rel(R[e, 3], R1[e, 3]) if R1[e, 3].any() else 0.0) for e in ev]
+    ew = [rel(R[e, 0], R1[e, 0]) for e in ev]
+    print(f"b_H = 1 over 2 ranks (hvp_exact {hvp_exact}): pair gradients at the same points max {max(eg):.2e}; "
+          f"iterates max {max(ew):.2e}; losses {h['loss']} single {h1['loss']}")
+    assert max(eg) <= 1e-6, eg
+    assert max(ew) <= 1e-4, ew
+    assert np.array_equal(h["accepted"], h1["accepted"])
+    assert np.max(np.abs(h["loss"] - h1["loss"]) / np.abs(h1["loss"])) <= 1e-4

@@ -49,19 +49,36 @@ def rank_env(rank, world, port):
 
 
 def run_procs(cmds, timeout):
-    """Start one process per rank; kill every rank if one fails or the group overruns `timeout`."""
-    procs = [subprocess.Popen(c, env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, cwd=ROOT)
-             for c, e in cmds]
-    outs = []
-    try:
+    """Start one process per rank, each writing to its own file (no pipe can fill and block a rank); poll every
+    rank, and kill the others as soon as one exits non-zero (a rank left in a collective would wait for the
+    dead one until the time limit) or the group overruns `timeout`."""
+    import tempfile
+    import time
+
+    logs = [tempfile.TemporaryFile(mode="w+") for _ in cmds]
+    procs = [subprocess.Popen(c, env=e, stdout=f, stderr=subprocess.STDOUT, text=True, cwd=ROOT)
+             for (c, e), f in zip(cmds, logs)]
+    t_end = time.monotonic() + timeout
+    failed = None
+    while any(p.poll() is None for p in procs):
+        bad = [r for r, p in enumerate(procs) if p.poll() not in (None, 0)]
+        if bad or time.monotonic() > t_end:
+            failed = bad[0] if bad else -1
+            break
+        time.sleep(0.2)
+    if failed is not None:
         for p in procs:
-            outs.append(p.communicate(timeout=timeout)[0])
-    except subprocess.TimeoutExpired:
-        for p in procs:
-            p.kill()
+            if p.poll() is None:
+                p.kill()
         for p in procs:
             p.wait()
-        pytest.fail("a rank process overran its time limit")
+    outs = []
+    for f in logs:
+        f.seek(0)
+        outs.append(f.read())
+        f.close()
+    if failed == -1:
+        pytest.fail("a rank process overran its time limit:\n" + "\n".join(o[-2000:] for o in outs))
     for r, p in enumerate(procs):
         assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{outs[r][-4000:]}"
     return outs
