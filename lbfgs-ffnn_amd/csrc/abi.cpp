@@ -332,7 +332,8 @@ int lbf_two_loop(lbf_ctx *ctx, long long n, int k, const float *d_S, const float
       gg.has_g = 1;
       gg.ga = d_g;
       gg.g_out = v.get();
-      h.update_combine(gg, 1, dsign, zero.get(), d_dir, nullptr, 1.0);
+      LBF_REQUIRE(h.update_combine(gg, 1, dsign, zero.get(), d_dir, nullptr, 1.0),
+                  "mode 3: the direction-only step did not take the coefficient-map route");
       ctx->c.host.ensure(1);
       LBF_HIP(hipMemcpyAsync(ctx->c.host.get(), h.view().scal + SC_KERR, sizeof(double), hipMemcpyDeviceToHost, s));
       LBF_HIP(hipStreamSynchronize(s));

@@ -1216,7 +1216,7 @@ bool History::update_impl(const GramArgs &g0, int want_dir, int iter, double dsi
   return false;
 }
 
-void History::update_combine(const GramArgs &g0, int iter, double dsign, const float *x_in, float *x_out,
+bool History::update_combine(const GramArgs &g0, int iter, double dsign, const float *x_in, float *x_out,
                              float *x_out2, double alpha, const RedAllArgs *gred) {
   // (the combine inside the column-sum launch measured slower: its waiting blocks slowed the column sums
   // and the one-block step, profiles/r03b/README.md)
@@ -1229,8 +1229,9 @@ void History::update_combine(const GramArgs &g0, int iter, double dsign, const f
   c.x_out2 = x_out2;
   c.alpha_from_state = 0;
   c.alpha = alpha;
-  if (update_impl(g0, 1, iter, dsign, gred, &c)) return;
+  if (update_impl(g0, 1, iter, dsign, gred, &c)) return true; // dir_cols_combine ran (coefficients from K)
   combine(g0.g_out, nullptr, x_in, x_out, x_out2, false, alpha);
+  return false;
 }
 
 void History::combine(const float *g, float *dir, const float *x_in, float *x_out, float *x_out2,

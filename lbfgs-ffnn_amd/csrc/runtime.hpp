@@ -234,7 +234,7 @@ public:
   void combine(const float *g, float *dir, const float *x_in, float *x_out, float *x_out2, bool alpha_from_state,
                double alpha);
   // update(g, 1, iter, dsign) then combine(g.g_out, nullptr, x_in, x_out, x_out2, false, alpha)
-  void update_combine(const GramArgs &g, int iter, double dsign, const float *x_in, float *x_out, float *x_out2,
+  bool update_combine(const GramArgs &g, int iter, double dsign, const float *x_in, float *x_out, float *x_out2,
                       double alpha, const RedAllArgs *gred = nullptr);
   double *scal() const { return v_.scal; }
   int m() const { return v_.m; }

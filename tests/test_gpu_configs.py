@@ -96,6 +96,26 @@ def test_cfg5_loss_grad_matches_oracle(ctx, pkg, O):
     assert rel(host(g), g_ref) <= max(1e-4, 3.0 * rel(g32, g_ref))
 
 
+def test_cfg5_loss_grad_split_plan_matches_oracle(ctx, pkg, O):
+    """cfg 5 against the fp64 oracle where the N = 1,000,000 route engages: from ~8k rows the
+    two wide dW GEMMs run the 1M plan's 128 x 128 tiles with the same split counts (layer 0: 33 x 16 = 528 tiles
+    in 29 splits, layer 1: 17 x 8 in 15; LBF_SHOW_PLAN output in profiles/r06/), the forward GEMMs run unsplit
+    128-row tiles, and the last layer's 1024 x 1 dW is split many ways; below 2048 rows (the N <= 128 tests above)
+    every dW GEMM takes the small-batch 64 x 64 plan instead. Loss 1e-5, gradient 1e-4 (the full-size bounds)."""
+    dims, acts = CFG5
+    N = 8192
+    X, Y = pkg.synth_regression(ctx, N, dims[0])
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    loss, g = net.loss_grad(P, X, Y)
+    onet = O.Net(dims, acts)
+    l_ref, g_ref = onet.loss_grad(host(P), host(X), host(Y))
+    e = rel(host(g), g_ref)
+    print(f"cfg5 N = {N}: loss rel {abs(loss - l_ref) / abs(l_ref):.2e}, grad rel {e:.2e}")
+    assert abs(loss - l_ref) <= 1e-5 * abs(l_ref)
+    assert e <= 1e-4
+
+
 def test_cfg5_lbfgs_m50_trajectory(ctx, pkg, O):
     dims, acts = CFG5
     N = 128
