@@ -230,6 +230,29 @@ class Net:
         return P, rec[: it.value], idx
 
 
+def torch_loss_grad(dims, acts, P, X, Y, threads=None):
+    """The same MLP loss (0.5 * SSE / N) and gradient by torch CPU fp64 autograd on BLAS GEMMs: the pin of the C
+    restatement's loss_grad (tests/test_oracle.py, 1e-12), used where the restatement's loops are too slow (cfg 5
+    at tens of thousands of rows). P: the reference's flat layout, per layer W (Out x In column-major == [In][Out])
+    then b."""
+    import torch
+    if threads:
+        torch.set_num_threads(int(threads))
+    t = torch.tensor(np.asarray(P, np.float64), dtype=torch.float64, requires_grad=True)
+    a = torch.as_tensor(np.asarray(X, np.float64))
+    f = {"relu": torch.relu, "tanh": torch.tanh, "sigmoid": torch.sigmoid, "linear": lambda z: z}
+    off = 0
+    for li, act in enumerate(acts):
+        i, o = int(dims[li]), int(dims[li + 1])
+        W = t[off:off + i * o].view(i, o)
+        b = t[off + i * o: off + i * o + o]
+        off += (i + 1) * o
+        a = f[act](a @ W + b)
+    L = 0.5 * ((a - torch.as_tensor(np.asarray(Y, np.float64))) ** 2).sum() / a.shape[0]
+    L.backward()
+    return float(L.detach()), t.grad.numpy().copy()
+
+
 def two_loop(mode: int, S, Y, rho, g):
     S = np.ascontiguousarray(S, np.float64)
     Y = np.ascontiguousarray(Y, np.float64)

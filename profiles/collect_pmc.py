@@ -17,16 +17,22 @@ import os
 import statistics
 
 
-def per_dispatch(d, counter, kernel):
-    vals = []
+def per_dispatch(d, counter, kernel, largest_grid=False):
+    """Counter values of every dispatch whose name contains `kernel`; largest_grid: only the dispatches with the
+    largest grid among them (one instantiation serves several layers: e.g. cfg 5's dW GEMMs of layers 0 and 1,
+    whose largest grid is layer 0's)."""
+    rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
             if kernel not in r.get("Kernel_Name", ""):
                 continue
-            vals.append(float(r["Counter_Value"]))
-    return vals
+            rows.append((int(float(r.get("Grid_Size", 0) or 0)), float(r["Counter_Value"])))
+    if largest_grid and rows:
+        gmax = max(g for g, _ in rows)
+        rows = [x for x in rows if x[0] == gmax]
+    return [v for _, v in rows]
 
 
 def main():
@@ -37,9 +43,10 @@ def main():
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--config", required=True)
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "pmc_traffic.json"))
+    ap.add_argument("--largest-grid", action="store_true")
     a = ap.parse_args()
-    fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
-    write = per_dispatch(a.write_dir, "WRITE_SIZE", a.kernel)
+    fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel, a.largest_grid)
+    write = per_dispatch(a.write_dir, "WRITE_SIZE", a.kernel, a.largest_grid)
     if not fetch or not write:
         raise SystemExit(f"no samples: fetch={len(fetch)} write={len(write)}")
     f_kib, w_kib = statistics.median(fetch), statistics.median(write)

@@ -14,7 +14,7 @@ pkg = load_package()
 ctx = pkg.Context(0)
 net = pkg.Mlp(ctx, [4096, 2048, 1024, 1], ["relu", "relu", "linear"])
 P = net.init_params(123, "cpu")
-for N in (128, 2048, 4096, 8192, 16384, 40000, 1_000_000):
+for N in (128, 2048, 4096, 8192, 16384, 20000, 24576, 28672, 32768, 36864, 40000, 1_000_000):
     X = torch.zeros((N, 4096), device="cuda")
     Y = torch.zeros((N, 1), device="cuda")
     net.loss_grad(P, X, Y)

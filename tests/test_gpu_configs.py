@@ -116,6 +116,25 @@ def test_cfg5_loss_grad_split_plan_matches_oracle(ctx, pkg, O):
     assert e <= 1e-4
 
 
+def test_cfg5_loss_grad_1m_route_matches_fp64(ctx, pkg, O):
+    """cfg 5 at 32768 rows, the smallest N at which every GEMM of the N = 1,000,000 evaluation takes the 1M route's
+    tile and split plan (LBF_SHOW_PLAN, profiles/r06/: dW layer 0 128 x 128 in 29 splits, layer 1 in 47, the last
+    layer's forward on 128-row tiles; only the last layer's 1024 x 1 dW split count still grows with N). The fp64
+    reference is torch CPU autograd on BLAS (O.torch_loss_grad; the C restatement is pinned to it at 1e-12 in
+    tests/test_oracle.py and is too slow here). Loss 1e-5, gradient 1e-4."""
+    dims, acts = CFG5
+    N = 32768
+    X, Y = pkg.synth_regression(ctx, N, dims[0])
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(123, "cpu")
+    loss, g = net.loss_grad(P, X, Y)
+    l_ref, g_ref = O.torch_loss_grad(dims, acts, host(P), host(X), host(Y))
+    e = rel(host(g), g_ref)
+    print(f"cfg5 N = {N}: loss rel {abs(loss - l_ref) / abs(l_ref):.2e}, grad rel {e:.2e}")
+    assert abs(loss - l_ref) <= 1e-5 * abs(l_ref)
+    assert e <= 1e-4
+
+
 def test_cfg5_lbfgs_m50_trajectory(ctx, pkg, O):
     dims, acts = CFG5
     N = 128
