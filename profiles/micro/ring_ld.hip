@@ -1,0 +1,133 @@
+// History-ring layout micro-benchmark (gfx950): does the slot stride of the (s, y) ring change the rate of the
+// combine sweep's many-stream read (2k vectors, 16 B per lane of each, fp64 accumulate, grid-stride over the
+// resident grid, nontemporal loads: vec_kernels.hip combine_kernel<8, true>) and of the Gram sweep's pattern
+// (one wave per vector over a 4096-float chunk, 4 quads in flight)?
+//   hipcc --offload-arch=gfx950 -O3 ring_ld.hip -o ring_ld && ./ring_ld
+// n = 10,489,857 (cfg 5), k = 100 vectors (m = 50). Strides: round4(n) (the engine's), + 64 / 256 / 1024 / 4160
+// floats, and rounded up to 2 MiB (+ 4 KiB).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#define CK(x)                                                                                                \
+  do {                                                                                                       \
+    hipError_t e_ = (x);                                                                                     \
+    if (e_ != hipSuccess) {                                                                                  \
+      printf("%s line %d\n", hipGetErrorString(e_), __LINE__);                                               \
+      return 1;                                                                                              \
+    }                                                                                                        \
+  } while (0)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int U>
+__global__ __launch_bounds__(256) void comb_k(const float *H, long long ld, int k, const double *c, float *out,
+                                              long long n) {
+  __shared__ double cs[128];
+  for (int i = threadIdx.x; i < k; i += 256) cs[i] = c[i];
+  __syncthreads();
+  const long long stride = (long long)gridDim.x * 256 * 4;
+  for (long long e = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; e + 3 < n; e += stride) {
+    double acc[4] = {0, 0, 0, 0};
+    for (int i = 0; i + U <= k; i += U) {
+      f32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(H + (long long)(i + u) * ld + e));
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += cs[i + u] * double(v[u][j]);
+    }
+    f32x4 d;
+    for (int j = 0; j < 4; ++j) d[j] = float(acc[j]);
+    *reinterpret_cast<f32x4 *>(out + e) = d;
+  }
+}
+
+// Gram pattern: a workgroup of 8 waves owns a 4096-float chunk; wave w streams vectors w, w + 8, ... of it with
+// 4 quads per lane in flight, dots against one LDS vector, a DPP-free shuffle sum per vector.
+__global__ __launch_bounds__(512) void gram_k(const float *H, long long ld, int k, double *out, long long n) {
+  __shared__ float g[4096];
+  const long long e0 = (long long)blockIdx.x * 4096;
+  for (int i = threadIdx.x; i < 4096; i += 512) g[i] = 1.0f + 1e-3f * float(i);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int v = wave; v < k; v += 8) {
+    double s = 0.0;
+    const float *V = H + (long long)v * ld + e0;
+    for (int i0 = lane * 4; i0 < 4096; i0 += 1024) {
+      f32x4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long ee = e0 + i0 + 256 * u;
+        x[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(V + (ee + 3 < n ? i0 + 256 * u : 0)));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += double(x[u][j]) * double(g[i0 + 256 * u + j]);
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) out[(long long)blockIdx.x * 128 + v] = s;
+  }
+}
+
+int main() {
+  const long long n = 10489857, n4 = (n + 3) & ~3LL;
+  const int k = 100;
+  const long long pads[] = {0, 64, 256, 1024, 4160, -1, -2};
+  int dev = 0, cus = 0, per = 0;
+  CK(hipGetDevice(&dev));
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, comb_k<8>, 256, 0));
+  const long long maxld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4 + 1024;
+  float *H = nullptr, *out = nullptr, *flush = nullptr;
+  double *c = nullptr, *gout = nullptr;
+  CK(hipMalloc(&H, size_t(maxld) * k * 4));
+  CK(hipMalloc(&out, size_t(n4) * 4));
+  CK(hipMalloc(&flush, size_t(512) << 20));
+  CK(hipMalloc(&c, 128 * 8));
+  const int nch = int((n + 4095) / 4096);
+  CK(hipMalloc(&gout, size_t(nch) * 128 * 8));
+  CK(hipMemset(H, 0, size_t(maxld) * k * 4));
+  std::vector<double> hc(128, 0.01);
+  CK(hipMemcpy(c, hc.data(), 128 * 8, hipMemcpyHostToDevice));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  printf("n = %lld, k = %d, combine grid %d x 256 (%d per CU), gram %d chunks\n", n, k, cus * per, per, nch);
+  for (long long pad : pads) {
+    long long ld = n4 + (pad > 0 ? pad : 0);
+    if (pad == -1) ld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4;
+    if (pad == -2) ld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4 + 1024;
+    const double bytes = double(k) * n * 4;
+    for (int kind = 0; kind < 2; ++kind) {
+      float best = 1e30f, sum = 0.0f;
+      for (int it = 0; it < 6; ++it) {
+        CK(hipMemset(flush, it, size_t(512) << 20)); // evict the Infinity Cache between runs
+        CK(hipEventRecord(a));
+        if (kind == 0) hipLaunchKernelGGL(comb_k<8>, dim3(cus * per), dim3(256), 0, 0, H, ld, k, c, out, n);
+        else hipLaunchKernelGGL(gram_k, dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (it > 0) {
+          best = ms < best ? ms : best;
+          sum += ms;
+        }
+      }
+      printf("%-8s ld = n4 %+6lld floats (%s)  best %7.1f us %6.0f GB/s  avg %7.1f us %6.0f GB/s\n",
+             kind == 0 ? "combine" : "gram", ld - n4, pad == -1 ? "2 MiB" : (pad == -2 ? "2 MiB + 4 KiB" : "plain"),
+             best * 1e3, bytes / best / 1e6, sum / 5 * 1e3, bytes / (sum / 5) / 1e6);
+    }
+  }
+  CK(hipFree(H));
+  CK(hipFree(out));
+  CK(hipFree(flush));
+  CK(hipFree(c));
+  CK(hipFree(gout));
+  printf("done\n");
+  return 0;
+}
