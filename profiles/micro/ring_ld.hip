@@ -45,31 +45,45 @@ __global__ __launch_bounds__(256) void comb_k(const float *H, long long ld, int 
   }
 }
 
-// Gram pattern: a workgroup of 8 waves owns a 4096-float chunk; wave w streams vectors w, w + 8, ... of it with
-// 4 quads per lane in flight, dots against one LDS vector, a DPP-free shuffle sum per vector.
+// Gram pattern: a workgroup of 8 waves owns a 4096-float chunk; wave w streams vectors w, w + 8, ... of it, V vectors
+// at a time with U of each vector's 16 quads per lane in flight (the engine's gram_kernel: V = 1, U = 4), dots
+// against one LDS vector, a shuffle sum per vector.
+template <int U, int V>
 __global__ __launch_bounds__(512) void gram_k(const float *H, long long ld, int k, double *out, long long n) {
   __shared__ float g[4096];
   const long long e0 = (long long)blockIdx.x * 4096;
   for (int i = threadIdx.x; i < 4096; i += 512) g[i] = 1.0f + 1e-3f * float(i);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int v = wave; v < k; v += 8) {
-    double s = 0.0;
-    const float *V = H + (long long)v * ld + e0;
-    for (int i0 = lane * 4; i0 < 4096; i0 += 1024) {
-      f32x4 x[4];
+  for (int v0 = wave; v0 < k; v0 += 8 * V) {
+    double s[V];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const long long ee = e0 + i0 + 256 * u;
-        x[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(V + (ee + 3 < n ? i0 + 256 * u : 0)));
+    for (int q = 0; q < V; ++q) s[q] = 0.0;
+    for (int i0 = lane * 4; i0 < 4096; i0 += 256 * U) {
+      f32x4 x[V][U];
+#pragma unroll
+      for (int q = 0; q < V; ++q) {
+        const int v = min(v0 + 8 * q, k - 1);
+        const float *Vp = H + (long long)v * ld + e0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long ee = e0 + i0 + 256 * u;
+          x[q][u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(Vp + (ee + 3 < n ? i0 + 256 * u : 0)));
+        }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int q = 0; q < V; ++q)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s += double(x[u][j]) * double(g[i0 + 256 * u + j]);
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s[q] += double(x[q][u][j]) * double(g[i0 + 256 * u + j]);
     }
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (lane == 0) out[(long long)blockIdx.x * 128 + v] = s;
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      double t = s[q];
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+      if (lane == 0 && v0 + 8 * q < k) out[(long long)blockIdx.x * 128 + v0 + 8 * q] = t;
+    }
   }
 }
 
@@ -102,13 +116,18 @@ int main() {
     if (pad == -1) ld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4;
     if (pad == -2) ld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4 + 1024;
     const double bytes = double(k) * n * 4;
-    for (int kind = 0; kind < 2; ++kind) {
+    const char *names[] = {"combine", "gram_u4v1", "gram_u8v1", "gram_u16v1", "gram_u8v2"};
+    for (int kind = 0; kind < 5; ++kind) {
+      if (kind > 1 && pad != 0 && pad != -2) continue; // the in-flight variants at two strides only
       float best = 1e30f, sum = 0.0f;
       for (int it = 0; it < 6; ++it) {
         CK(hipMemset(flush, it, size_t(512) << 20)); // evict the Infinity Cache between runs
         CK(hipEventRecord(a));
         if (kind == 0) hipLaunchKernelGGL(comb_k<8>, dim3(cus * per), dim3(256), 0, 0, H, ld, k, c, out, n);
-        else hipLaunchKernelGGL(gram_k, dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else if (kind == 1) hipLaunchKernelGGL((gram_k<4, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else if (kind == 2) hipLaunchKernelGGL((gram_k<8, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else if (kind == 3) hipLaunchKernelGGL((gram_k<16, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else hipLaunchKernelGGL((gram_k<8, 2>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms = 0;
@@ -118,8 +137,8 @@ int main() {
           sum += ms;
         }
       }
-      printf("%-8s ld = n4 %+6lld floats (%s)  best %7.1f us %6.0f GB/s  avg %7.1f us %6.0f GB/s\n",
-             kind == 0 ? "combine" : "gram", ld - n4, pad == -1 ? "2 MiB" : (pad == -2 ? "2 MiB + 4 KiB" : "plain"),
+      printf("%-10s ld = n4 %+6lld floats (%s)  best %7.1f us %6.0f GB/s  avg %7.1f us %6.0f GB/s\n",
+             names[kind], ld - n4, pad == -1 ? "2 MiB" : (pad == -2 ? "2 MiB + 4 KiB" : "plain"),
              best * 1e3, bytes / best / 1e6, sum / 5 * 1e3, bytes / (sum / 5) / 1e6);
     }
   }
