@@ -66,13 +66,6 @@ struct GemmK {
   int gx, gy;   // this problem's tile grid (the grouped launch's grid is the larger of two)
   int group_z;  // grouped launch: GEMM planes of the first problem (the second's follow)
   int xcd_swz;  // split-K: deal each split's tiles to one XCD (xcd_tile below)
-  // stream-K forward (gemm_glds_sk_kernel): blocks < sk_dp run tile blockIdx.x whole; the rest split the k-tiles
-  // of tiles sk_dp .. gy-1 evenly, publishing partial accumulators to sk_part (3 slots per tile) and counting
-  // arrivals in sk_cnt (one per tile; the last arriver sums the parts in part order, runs the epilogue, and
-  // re-zeroes the counter)
-  int sk_dp;
-  float *sk_part;
-  int *sk_cnt;
 };
 
 // XCD-aware placement of a split-K GEMM's blocks (cdna_hip_programming.md §5.5 T1, bijective form): blocks
@@ -364,10 +357,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmK &g, f32x16 (&acc)[TM][
     }
     KT(32);
     const long long nf = fold ? (long long)(g.head_fold + 1) * g.N : 0; // fold rows in front of the head's
-    const int trow = m0 / BM; // the tile's row index (blockIdx.y, except in the stream-K launch)
-    float *slab = g.head_slab + (long long)trow * (nf + (long long)(g.N + 1) * g.head_out);
+    float *slab = g.head_slab + (long long)blockIdx.y * (nf + (long long)(g.N + 1) * g.head_out);
     if (fold) headc::write_fold(fa, g.N, g.head_fold, slab);
-    headc::write_partials(hs, g.head_out, cw, sse, slab + nf, g.head_sse + trow);
+    headc::write_partials(hs, g.head_out, cw, sse, slab + nf, g.head_sse + blockIdx.y);
     KT(33);
     KTB(7);
     return;
@@ -666,64 +658,8 @@ template <int WM, int WN, int TM, int TN, int EPI, int NS> struct GldsShape {
 };
 
 // One GEMM tile (bx, by) of split zsplit (the kernels below choose the problem and the tile).
-// Stream-K hand-off of one tile's partial accumulators (gemm_glds_sk_kernel): this block's part p of np is
-// stored write-through (agent-scope relaxed stores, sc1) and drained before the block's one arrival add; the
-// block whose add returns np - 1 reads the other parts with agent-scope loads and sums all parts in part order
-// ((p0 + p1) + p2, the same expression whichever block arrives last, so a re-evaluation is bitwise identical),
-// then returns true and runs the tile's epilogue. No block ever waits for another: no residency requirement.
-template <int TM, int TN>
-__device__ __forceinline__ bool sk_combine(const GemmK &g, f32x16 (&acc)[TM][TN], int trow, int p, int np,
-                                           int *s_flag) {
-  constexpr int NV = TM * TN * 16;
-  const int tid = threadIdx.x;
-  float *base = g.sk_part + (long long)(trow - g.sk_dp) * 3 * NV * 256;
-  float *mine = base + (long long)p * NV * 256;
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        __hip_atomic_store(mine + ((a * TN + b) * 16 + r) * 256 + tid, acc[a][b][r], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0)
-    *s_flag = __hip_atomic_fetch_add(g.sk_cnt + trow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == np - 1;
-  __syncthreads();
-  if (!*s_flag) return false;
-  if (tid == 0) g.sk_cnt[trow] = 0; // ready for the next launch (stream-ordered)
-  // the (at most two) other parts, o0 < o1 in part order, 16 values of one (a, b) accumulator at a time
-  const int o0 = p == 0 ? 1 : 0, o1 = p == 2 ? 1 : 2;
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      const long long off = (long long)(a * TN + b) * 16 * 256 + tid;
-      f32x16 v0, v1;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { // requested before the sum: one round trip per accumulator
-        v0[r] = __hip_atomic_load(base + (long long)o0 * NV * 256 + off + r * 256, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-        v1[r] = np > 2 ? __hip_atomic_load(base + (long long)o1 * NV * 256 + off + r * 256, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)
-                       : 0.0f;
-      }
-      const f32x16 m = acc[a][b];
-      f32x16 sum;
-      if (np == 2) sum = p == 0 ? m + v0 : v0 + m;                  // p0 + p1
-      else sum = p == 0 ? (m + v0) + v1 : (p == 1 ? (v0 + m) + v1 : (v0 + v1) + m); // (p0 + p1) + p2
-      acc[a][b] = sum;
-    }
-  return true;
-}
-
-// SKP: a stream-K part of tile (bx, by): k-tiles from k offset kb_sk to ke_sk, part sk_p of sk_np (sk_np == 1:
-// the whole tile, as without SK).
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW, bool ASUM,
-          bool SKP = false>
-__device__ __forceinline__ void glds_body(const GemmK &g, float *lds, int zsplit, int bx, int by, int kb_sk = 0,
-                                          int ke_sk = 0, int sk_p = 0, int sk_np = 1, int *sk_flag = nullptr) {
+template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW, bool ASUM>
+__device__ __forceinline__ void glds_body(const GemmK &g, float *lds, int zsplit, int bx, int by) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 32;
   constexpr int ASZ = BM * BK, STG = (BM + BN) * BK;
   constexpr int PA = BM / 8, P = (BM + BN) / 32; // A pieces per k-tile, pieces per wave per k-tile
@@ -738,8 +674,8 @@ __device__ __forceinline__ void glds_body(const GemmK &g, float *lds, int zsplit
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 31, lh = lane >> 5;
   const int n0 = bx * BN, m0 = by * BM;
-  const int kb = SKP ? kb_sk : zsplit * g.k_chunk;
-  const int ke = SKP ? ke_sk : min(g.K, kb + g.k_chunk);
+  const int kb = zsplit * g.k_chunk;
+  const int ke = min(g.K, kb + g.k_chunk);
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -946,10 +882,6 @@ __device__ __forceinline__ void glds_body(const GemmK &g, float *lds, int zsplit
       __syncthreads();
     }
   }
-  if constexpr (SKP) {
-    static_assert(KW == 1, "stream-K: one k-group");
-    if (sk_np > 1 && !sk_combine<TM, TN>(g, acc, by, sk_p, sk_np, sk_flag)) return; // another part finishes
-  }
   gemm_epilogue<WM, WN, TM, TN, EPI, KW>(g, acc, lds, hpre, zsplit, m0, n0, wm, wn, li, lh, kgrp);
 }
 
@@ -968,65 +900,6 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
              int(gridDim.y), z, bx, by);
   }
   glds_body<WM, WN, TM, TN, AKC, BKC, EPI, GATHER, NS, KW, ASUM>(g, lds, z, bx, by);
-}
-
-// Stream-K forward (one column tile, unsplit, single k-group): a launch of 2 x CUs blocks for CUs < tiles < 2 x CUs
-// row tiles, where the plain launch leaves tiles - CUs CUs with two blocks and the rest with one (cfg 2: 469 tiles
-// of 128 x 128 on 256 CUs, the 43 lone blocks idle for the launch's last ~50 us). Blocks
-// 0 .. sk_dp - 1 (dispatched first, one per CU) run tiles 0 .. sk_dp - 1 whole, exactly as the plain kernel; the
-// other sk_dp blocks share the k-tiles of the remaining tiles evenly (contiguous unit ranges, unit = one 32-deep
-// k-tile of one tile), so every CU gets the same MFMA work; a tile cut between two or three blocks is finished
-// by its last-arriving part (sk_combine). The whole-tile blocks keep their arbitration lead, so their epilogues
-// still overlap the partner blocks' main loops.
-template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int NS>
-__global__ __launch_bounds__(256, 2) void gemm_glds_sk_kernel(const GemmK g) {
-  __shared__ __attribute__((aligned(16))) float lds[GldsShape<WM, WN, TM, TN, EPI, NS>::LDS_F];
-  __shared__ int s_flag;
-  if (g.abort && *g.abort) return;
-  const int id = int(blockIdx.x);
-  const int KT = (g.K + 31) / 32;
-  // one call site of the body for both kinds of block: one inlined copy (a second one spilled the head's registers)
-  const bool whole = id < g.sk_dp;
-  const int nw = int(gridDim.x) - g.sk_dp, j = id - g.sk_dp;
-  const long long U = (long long)(g.gy - g.sk_dp) * KT;
-  auto bnd = [&](int w) { return U * w / nw; };     // first unit of stream-K block w
-  auto owner = [&](long long u) {                    // the stream-K block whose range holds unit u
-    int w = int(u * nw / U);
-    while (w + 1 < nw && bnd(w + 1) <= u) ++w;
-    while (w > 0 && bnd(w) > u) --w;
-    return w;
-  };
-  // A stream-K range is shorter than a tile (gemm_sk_ok), so it holds at most two parts: straight-line code for
-  // the two (a loop around the inlined body made the head epilogue's registers spill: 556 B per lane of scratch)
-  const long long u0 = whole ? 0 : bnd(j), u1 = whole ? KT : bnd(j + 1);
-  auto part = [&](long long u, int &tile, int &a, int &b, int &p, int &np) {
-    tile = id;
-    a = 0;
-    b = KT;
-    p = 0;
-    np = 1;
-    if (!whole) {
-      const int t = int(u / KT);
-      a = int(u - (long long)t * KT);
-      b = int(min((long long)KT, a + (u1 - u)));
-      const long long t0 = (long long)t * KT;
-      const int w0 = owner(t0);
-      tile = g.sk_dp + t;
-      p = j - w0;
-      np = owner(t0 + KT - 1) - w0 + 1;
-    }
-  };
-  int tile, a, b, p, np;
-  part(u0, tile, a, b, p, np);
-  const long long um = u0 + (b - a); // start of the second part (== u1: none)
-  glds_body<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, 1, false, true>(g, lds, 0, 0, tile, 32 * a, min(g.K, 32 * b), p,
-                                                                     np, &s_flag);
-  if (um < u1) {
-    __syncthreads(); // the second part's LDS-DMA stages reuse the first part's LDS
-    part(um, tile, a, b, p, np);
-    glds_body<WM, WN, TM, TN, AKC, BKC, EPI, false, NS, 1, false, true>(g, lds, 0, 0, tile, 32 * a, min(g.K, 32 * b),
-                                                                       p, np, &s_flag);
-  }
 }
 
 // Two GEMMs of one shape in one launch (the S-LBFGS minibatch's dW GEMMs of adjacent layers): planes
@@ -1203,19 +1076,6 @@ namespace {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// The stream-K forward's shape (Mlp::plan decides where it pays; kernels.hpp gemm_sk_rows): 128 x 128 tiles in one
-// column tile, no split, no gather / A-from-slabs, and at least 13 k-tiles per stream-K block, so a tile is cut
-// into at most three parts.
-bool gemm_sk_ok(const GemmDesc &d) {
-  if (d.sk_cus <= 0 || !d.sk_part || !d.sk_cnt || d.tile != TILE_AUTO || d.N > 128 || d.N <= 64 || d.splits > 1 ||
-      d.a_idx || d.a_slab || !d.a_kc || d.b_kc)
-    return false;
-  const long long gy = cdiv((long long)d.M, 128LL), KT = cdiv((long long)d.K, 32LL);
-  // ranges of >= 13 and < KT k-tiles: a range holds at most two parts and a tile at most three
-  const long long U = (gy - d.sk_cus) * KT;
-  return gy > d.sk_cus && gy < 2LL * d.sk_cus && U >= 13LL * d.sk_cus && U / d.sk_cus + 1 < KT;
-}
-
 template <int BM, int BN> GemmK make_gemmk(const GemmDesc &d) {
   GemmK k;
   k.M = d.M;
@@ -1275,9 +1135,6 @@ template <int BM, int BN> GemmK make_gemmk(const GemmDesc &d) {
   k.a_bias = d.a_bias;
   k.a_act = d.a_act;
   k.a_out = d.a_out;
-  k.sk_dp = 0;
-  k.sk_part = d.sk_part;
-  k.sk_cnt = d.sk_cnt;
   return k;
 }
 
@@ -1310,14 +1167,6 @@ void launch(hipStream_t s, const GemmDesc &d, const GemmDesc *d2 = nullptr) {
     throw std::runtime_error("gemm: grouped launch not supported for this tile");
   }
   if constexpr (NS > 0 && (AKC || BM >= 64) && (BKC || BN >= 64)) { // mn-contiguous swizzle: >= 64 columns
-    if constexpr (KW == 1 && AKC && !BKC && BM == 128 && BN == 128 && (EPI == EPI_FWD || EPI == EPI_HEAD)) {
-      if (fast && d.sk_part && gemm_sk_ok(d)) { // stream-K forward (gemm_sk_ok: one column tile, unsplit, plain A)
-        k.sk_dp = d.sk_cus;
-        hipLaunchKernelGGL((gemm_glds_sk_kernel<WM, WN, TM, TN, AKC, BKC, EPI, NS>), dim3(unsigned(2 * d.sk_cus)),
-                           dim3(256), 0, s, k);
-        return;
-      }
-    }
     if (fast && (AKC || !d.a_idx)) {
       const dim3 gb(256 * KW);
       if constexpr (AKC && BM == 32 && WN * TN == 4 && NS >= 2) {

@@ -52,11 +52,6 @@ struct GemmDesc {
   // workgroup forms its A tiles as act(sum_s a_slab[s * a_slab_stride + .] + a_bias) (fwd_reduce_act's
   // arithmetic, splits in order) in its prologue, and the workgroups of column tile 0 also write them to
   // a_out (row stride lda), which replaces the fwd_reduce_act launch of the previous layer.
-  // Stream-K forward (gemm.hip gemm_glds_sk_kernel; Mlp::plan sets these where the shape qualifies): sk_cus CUs,
-  // (tiles - sk_cus) x 3 partial tiles of 64 KB, one arrival counter per row tile (zero between launches).
-  float *sk_part = nullptr;
-  int *sk_cnt = nullptr;
-  int sk_cus = 0;
   const float *a_slab = nullptr;
   int a_splits = 0;
   long long a_slab_stride = 0;

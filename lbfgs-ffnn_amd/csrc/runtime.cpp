@@ -129,7 +129,7 @@ constexpr long long DW_SMALL_BATCH = 2048;
 // for batch B (workgroup-slot aware, split_factor), k chunks a multiple of the 32-deep LDS tile.
 void Mlp::plan(long long B) {
   if (planned_ == B) return;
-  size_t slab = 0, fslab = 0, skp = 0, skc = 0;
+  size_t slab = 0, fslab = 0;
   const int nl = int(layers_.size());
   const bool fused = nl >= 2 && head_supported(layers_[nl - 1].in, layers_[nl - 1].out);
   const long long slots = 2LL * ctx_->cus;
@@ -188,20 +188,6 @@ void Mlp::plan(long long B) {
         fslab = std::max(fslab, size_t(fs) * size_t(B) * L.out);
       }
     }
-    // Stream-K forward (gemm.hip gemm_glds_sk_kernel): 128 x 128 tiles in one column tile for CUs < row tiles <
-    // 2 x CUs, where the plain launch leaves (2 x CUs - tiles) CUs with one block, idle for the end of the launch
-    // (cfg 2: 469 tiles, 43 lone blocks done ~50 us before their paired neighbours); CUs blocks
-    // run tiles whole, CUs more share the rest's k-tiles evenly. LBF_FWD_SK=0: the plain launch.
-    static const int sk_on = env_int("LBF_FWD_SK", 1);
-    L.fsk = false;
-    if (sk_on && L.ftile == TILE_AUTO && L.fsplits == 1 && L.out > 64 && L.out <= 128) {
-      const long long gy = cdiv(B, 128LL), KT = cdiv((long long)L.in, 32LL);
-      if (gy > cus && gy < 2 * cus && (gy - cus) * KT >= 13 * cus) {
-        L.fsk = true;
-        skp = std::max(skp, size_t(gy - cus) * 3 * 128 * 128);
-        skc = std::max(skc, size_t(gy));
-      }
-    }
     // dW: 64x64 tiles over narrow outputs -> fewer, longer K splits (a third of the slab traffic)
     // (only for short K: at long K the 128x128 tile's reuse wins over the slab savings). Small batches
     // (S-LBFGS minibatches, K = 128 / 256 rows) take 64x64 tiles at any width: four times the tiles of
@@ -256,19 +242,11 @@ void Mlp::plan(long long B) {
   static const int show = env_int("LBF_SHOW_PLAN", 0);
   if (show) {
     for (int l = 0; l < nl; ++l)
-      std::fprintf(stderr, "[lbf plan] B=%lld layer %d: dW tile %d splits %d k_chunk %d | fwd tile %d splits %d sk %d\n",
-                   B, l, layers_[l].dtile, layers_[l].splits, layers_[l].k_chunk, layers_[l].ftile, layers_[l].fsplits,
-                   int(layers_[l].fsk));
+      std::fprintf(stderr, "[lbf plan] B=%lld layer %d: dW tile %d splits %d k_chunk %d | fwd tile %d splits %d\n", B,
+                   l, layers_[l].dtile, layers_[l].splits, layers_[l].k_chunk, layers_[l].ftile, layers_[l].fsplits);
     std::fprintf(stderr, "[lbf plan] B=%lld fold %d from column %d\n", B, fold_, fold_c0_);
   }
   slab_.ensure(slab);
-  if (skp) {
-    sk_part_.ensure(skp);
-    if (sk_cnt_.size() < skc) {
-      sk_cnt_.resize(skc);
-      LBF_HIP(hipMemsetAsync(sk_cnt_.get(), 0, skc * sizeof(int), ctx_->stream));
-    }
-  }
   fslab_.ensure(std::max<size_t>(fslab, 1));
   fslab2_.ensure(std::max<size_t>(fslab, 1)); // odd layers' slabs: the next layer may read the previous one's
   planned_ = B;
@@ -353,11 +331,6 @@ GemmDesc Mlp::fwd_desc(size_t l, const float *P, const float *in, const int *idx
   d.act = L.act;
   d.abort = ctx_->abort;
   d.tile = L.ftile;
-  if (L.fsk && !idx) {
-    d.sk_part = sk_part_.get();
-    d.sk_cnt = sk_cnt_.get();
-    d.sk_cus = ctx_->cus;
-  }
   return d;
 }
 
@@ -1083,7 +1056,12 @@ void Mlp::hvp(const float *P, const float *V, const float *X, const float *Y, co
 History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
   LBF_REQUIRE(m >= 0 && m <= 128, "history size m must be in [0, 128]");
   const int slots = m + 1;
-  const long long ld = cdiv(n, 4) * 4;
+  // Slot stride: n rounded to 4 floats; for the large-n sweeps (n >= 2^21: gram_kernel, combine) rounded up to
+  // 2 MiB, which the many-stream reads of the history prefer (profiles/micro/ring_ld.hip, profiles/r06/d/: the
+  // combine pattern 5.45 -> 5.88 TB/s, the Gram pattern 6.71 -> 6.91 TB/s at n = 10.49M, 100 vectors); at most
+  // 2 MiB more per slot. LBF_RING_PAD=0: the plain stride (A/B).
+  static const int ring_pad = env_int("LBF_RING_PAD", 1);
+  const long long ld = (ring_pad && n >= (1LL << 21)) ? cdiv(n, 1LL << 19) * (1LL << 19) : cdiv(n, 4) * 4;
   S_.resize(size_t(slots) * ld);
   Y_.resize(size_t(slots) * ld);
   ist_.resize(IST_ORDER + slots + 4);

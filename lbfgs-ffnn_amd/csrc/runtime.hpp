@@ -91,7 +91,6 @@ struct Layer {
   int fk_chunk = 0;
   int ftile = 0;       // forward GEMM tile (GemmTile)
   int dtile = 0;       // dW GEMM tile (GemmTile)
-  bool fsk = false;    // forward GEMM as the stream-K launch (gemm.hip gemm_glds_sk_kernel)
 };
 
 // RAII section: records an event pair around the enclosed launches when profiling is on.
@@ -197,8 +196,6 @@ private:
   long long cap_ = -1, planned_ = -1;
   std::vector<DevBuf<float>> A_, D_;
   DevBuf<float> slab_, head_slab_, fslab_, fslab2_;
-  DevBuf<float> sk_part_; // stream-K forward: partial tiles (Layer::fsk)
-  DevBuf<int> sk_cnt_;    // its arrival counters, one per row tile (zero between launches)
   float *fslab_buf(size_t l) const { return (l & 1) ? fslab2_.get() : fslab_.get(); } // forward slabs of layer l
   bool group_dw_ = true;      // dW of layers 1 and 0 in one launch (LBF_NO_GROUP=1: separate launches)
   bool fold_on_ = true;       // fold into the EPI_HEAD epilogue (LBF_NO_FOLD=1: the unfolded route, tests)

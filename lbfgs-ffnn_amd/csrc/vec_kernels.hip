@@ -1286,6 +1286,108 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
   }
 }
 
+// Large-n combine with the Gram sweep's access pattern (round 6). combine_kernel above reads, per wave-instruction,
+// 1 KB of one vector and per lane one quad of every live vector, the grid striding over the elements: the chip
+// then touches every vector at the same few offsets at once, a pattern that streams at 5.45 TB/s against 6.7 TB/s
+// for the Gram sweep's (each wave 4-16 KB contiguous of one vector; profiles/micro/ring_ld.hip, profiles/r06/d/).
+// Here a workgroup owns 4096-element chunks (grid-stride over the resident grid): wave w the 1024 elements
+// c0 + 1024 w .., lane l the quads 256 u + 4 l (u < 4), so each vector is read as 4 KB contiguous per wave and
+// 16 KB per workgroup, V vectors' quads (2 V x 4 loads) in flight per lane. Per element the same fp64 sum in the
+// same order as combine_kernel (cg g, then cs_i S_i + cy_i Y_i for i = 0 .. k - 1).
+template <int V, bool NT>
+__global__ __launch_bounds__(256) void combine_chunk_kernel(const CombineArgs a) {
+  if (a.h.abort && *a.h.abort) return;
+  __shared__ double cs[COEF_MAXK], cy[COEF_MAXK];
+  __shared__ int L[COEF_MAXK];
+  const HistView &h = a.h;
+  const int S_ = h.slots;
+  const int k = h.ist[IST_COUNT];
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    cs[i] = h.coef[i];
+    cy[i] = h.coef[S_ + i];
+    L[i] = h.ist[IST_ORDER + i];
+  }
+  __syncthreads();
+  const double cg = h.coef[2 * S_];
+  const double alpha = a.alpha_from_state ? h.scal[SC_ALPHA0] : a.alpha;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float *xsrc = a.x_out ? a.x_in : a.g;
+  for (long long c0 = (long long)blockIdx.x * 4096; c0 < h.n; c0 += (long long)gridDim.x * 4096) {
+    long long e[4], ec[4];
+    bool full[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      e[u] = c0 + wave * 1024 + u * 256 + 4 * lane;
+      full[u] = e[u] + 3 < h.n;
+      ec[u] = full[u] ? e[u] : 0; // clamped: loads unconditional, results masked
+    }
+    double acc[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 g4 = *reinterpret_cast<const f32x4 *>(a.g + ec[u]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[u][j] = cg * double(g4[j]);
+    }
+    int i = 0;
+    for (; i + V <= k; i += V) {
+      f32x4 s4[V][4], y4[V][4];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const long long sb = (long long)L[i + v] * h.ld;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s4[v][u] = hist_load<NT>(h.S + sb + ec[u]);
+          y4[v][u] = hist_load<NT>(h.Y + sb + ec[u]);
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[u][j] += cs[i + v] * double(s4[v][u][j]) + cy[i + v] * double(y4[v][u][j]);
+    }
+    for (; i < k; ++i) {
+      const long long sb = (long long)L[i] * h.ld;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 s4 = hist_load<NT>(h.S + sb + ec[u]);
+        const f32x4 y4 = hist_load<NT>(h.Y + sb + ec[u]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[u][j] += cs[i] * double(s4[j]) + cy[i] * double(y4[j]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (full[u]) {
+        f32x4 d4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d4[j] = float(acc[u][j]);
+        if (a.dir) *reinterpret_cast<f32x4 *>(a.dir + e[u]) = d4;
+        if (a.x_out) {
+          const f32x4 x4 = *reinterpret_cast<const f32x4 *>(xsrc + e[u]);
+          const f32x4 o4 = x4 + float(alpha) * d4;
+          *reinterpret_cast<f32x4 *>(a.x_out + e[u]) = o4;
+          if (a.x_out2) *reinterpret_cast<f32x4 *>(a.x_out2 + e[u]) = o4;
+        }
+      } else {
+        for (long long q = e[u]; q < h.n && q < e[u] + 4; ++q) { // the tail quad, element-wise (no read past n)
+          double ac = cg * double(a.g[q]);
+          for (int ii = 0; ii < k; ++ii)
+            ac += cs[ii] * double(h.S[(long long)L[ii] * h.ld + q]) + cy[ii] * double(h.Y[(long long)L[ii] * h.ld + q]);
+          const float d = float(ac);
+          if (a.dir) a.dir[q] = d;
+          if (a.x_out) {
+            const float o = a.x_in[q] + float(alpha) * d;
+            a.x_out[q] = o;
+            if (a.x_out2) a.x_out2[q] = o;
+          }
+        }
+      }
+    }
+  }
+}
+
 // Small-n form (the latency-bound regime: n up to a few million, k <= 32): one element per lane so
 // the grid covers every CU, the ring header and coefficients read lane-distributed (no LDS, no
 // barrier) and broadcast with v_readlane, and every history load of the lane issued at once: one
@@ -1341,6 +1443,24 @@ void hist_combine(hipStream_t s, const CombineArgs &a) {
       hipLaunchKernelGGL(combine_small_kernel<16>, g1, dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL(combine_small_kernel<32>, g1, dim3(256), 0, s, a);
+    LBF_KERNEL_CHECK();
+    return;
+  }
+  static const int chunked = env_int("LBF_COMBINE_CHUNK", 1); // A/B: 0 keeps combine_kernel
+  if (chunked) {
+    static const long long res_c = [] { // workgroups of combine_chunk_kernel the chip holds at once, once
+      int dev = 0, cus = 0, p1 = 0, p2 = 0;
+      LBF_HIP(hipGetDevice(&dev));
+      LBF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p1, combine_chunk_kernel<2, true>, 256, 0));
+      LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p2, combine_chunk_kernel<2, false>, 256, 0));
+      return (long long)std::max(1, cus) * std::max(1, std::min(p1, p2));
+    }();
+    const dim3 grid(unsigned(std::min(cdiv(a.h.n, 4096LL), res_c)));
+    if (hist_nt(a.h))
+      hipLaunchKernelGGL((combine_chunk_kernel<2, true>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((combine_chunk_kernel<2, false>), grid, dim3(256), 0, s, a);
     LBF_KERNEL_CHECK();
     return;
   }
