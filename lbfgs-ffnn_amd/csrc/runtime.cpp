@@ -1056,12 +1056,10 @@ void Mlp::hvp(const float *P, const float *V, const float *X, const float *Y, co
 History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
   LBF_REQUIRE(m >= 0 && m <= 128, "history size m must be in [0, 128]");
   const int slots = m + 1;
-  // Slot stride: n rounded to 4 floats; for the large-n sweeps (n >= 2^21: gram_kernel, combine) rounded up to
-  // 2 MiB, which the many-stream reads of the history prefer (profiles/micro/ring_ld.hip, profiles/r06/d/: the
-  // combine pattern 5.45 -> 5.88 TB/s, the Gram pattern 6.71 -> 6.91 TB/s at n = 10.49M, 100 vectors); at most
-  // 2 MiB more per slot. LBF_RING_PAD=0: the plain stride (A/B).
-  static const int ring_pad = env_int("LBF_RING_PAD", 1);
-  const long long ld = (ring_pad && n >= (1LL << 21)) ? cdiv(n, 1LL << 19) * (1LL << 19) : cdiv(n, 4) * 4;
+  // Slot stride n rounded to 4 floats. (Rounded up to 2 MiB, the many-stream reads of the old combine pattern went
+  // 5.45 -> 5.88 TB/s in profiles/micro/ring_ld.hip, but the Gram sweep slowed 5.43 -> 5.25 TB/s at n = 10.49M and the
+  // chunked combine below needs no help: 65.4-65.7 % against 65.9-66.0 % of HBM at m = 50, profiles/r06/f/.)
+  const long long ld = cdiv(n, 4) * 4;
   S_.resize(size_t(slots) * ld);
   Y_.resize(size_t(slots) * ld);
   ist_.resize(IST_ORDER + slots + 4);

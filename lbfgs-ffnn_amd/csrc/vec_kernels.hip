@@ -853,7 +853,8 @@ int gram_nwg(long long n) {
   // 2561 chunks of 4096 were 3.33 rounds of 768 resident workgroups, the last a third full; now 3072 of
   // 3416), chunks still <= 4096.
   const long long slots = gram_slots();
-  if (w > slots) w = cdiv(need, slots) * slots;
+  static const int whole_rounds = env_int("LBF_GRAM_ROUNDS", 1); // A/B: 0 keeps the 4096-element chunks
+  if (whole_rounds && w > slots) w = cdiv(need, slots) * slots;
   return int(w < 1 ? 1 : w);
 }
 static long long gram_chunk(long long n, int nwg) { return cdiv(cdiv(n, nwg), 4) * 4; }
@@ -889,6 +890,7 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
   KT(16);
   extern __shared__ __attribute__((aligned(16))) float sh[];
   __shared__ double scratch[6 * 16];
+  __shared__ int order[COEF_MAXK]; // the live slots in logical order, staged once: no global load per vector below
   float *ls = sh, *ly = sh + chunk, *lg = sh + 2 * chunk;
   const HistView &h = a.h;
   const int ncols = 6 * h.m + 6;
@@ -898,6 +900,7 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
   const int w = hist_write_slot(h.ist, h.m, a.policy, a.reset);
   const int count = a.reset ? 0 : h.ist[IST_COUNT];
   if (blockIdx.x == 0 && threadIdx.x == 0) h.ist[IST_WSLOT] = w;
+  for (int i = threadIdx.x; i < count; i += blockDim.x) order[i] = h.ist[IST_ORDER + i]; // visible after block_sum
 
   double self[6] = {0, 0, 0, 0, 0, 0};
   float *Sw = h.S + (long long)w * h.ld + e0;
@@ -975,7 +978,7 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int v = wave; v < 2 * count; v += nw) {
     const int li = v < count ? v : v - count;
-    const int slot = h.ist[IST_ORDER + li];
+    const int slot = order[li];
     if (a.has_pair && slot == w) { // overwritten in this sweep (CUDA full ring): dots from the self block
       if (lane == 0) {
         out[(6 * li + (v < count ? 0 : 1)) * rs] = 0.0;

@@ -87,6 +87,61 @@ __global__ __launch_bounds__(512) void gram_k(const float *H, long long ld, int 
   }
 }
 
+// The engine's Gram sweep arithmetic on the same pattern: three fp32 vectors (s, y, g) of the chunk in LDS (48 KB:
+// three workgroups per CU, as gram_kernel), three fp64 dots per history vector, V history vectors per pass sharing
+// each LDS read, U quads of each in flight.
+template <int U, int V>
+__global__ __launch_bounds__(512) void gram3_k(const float *H, long long ld, int k, double *out, long long n) {
+  __shared__ float ls[4096], ly[4096], lg[4096];
+  const long long e0 = (long long)blockIdx.x * 4096;
+  for (int i = threadIdx.x; i < 4096; i += 512) {
+    ls[i] = 1.0f + 1e-3f * float(i);
+    ly[i] = 2.0f - 1e-3f * float(i);
+    lg[i] = 0.5f + 1e-4f * float(i);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int v0 = wave; v0 < k; v0 += 8 * V) {
+    double ds[V], dy[V], dg[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) ds[q] = dy[q] = dg[q] = 0.0;
+    for (int i0 = lane * 4; i0 < 4096; i0 += 256 * U) {
+      f32x4 x[V][U];
+#pragma unroll
+      for (int q = 0; q < V; ++q) {
+        const int v = min(v0 + 8 * q, k - 1);
+        const float *Vp = H + (long long)v * ld + e0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long ee = e0 + i0 + 256 * u;
+          x[q][u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(Vp + (ee + 3 < n ? i0 + 256 * u : 0)));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const f32x4 s4 = *reinterpret_cast<const f32x4 *>(ls + i0 + 256 * u);
+        const f32x4 y4 = *reinterpret_cast<const f32x4 *>(ly + i0 + 256 * u);
+        const f32x4 g4 = *reinterpret_cast<const f32x4 *>(lg + i0 + 256 * u);
+#pragma unroll
+        for (int q = 0; q < V; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const double xv = x[q][u][j];
+            ds[q] += xv * double(s4[j]);
+            dy[q] += xv * double(y4[j]);
+            dg[q] += xv * double(g4[j]);
+          }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      double t = ds[q] + 2.0 * dy[q] + 3.0 * dg[q];
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+      if (lane == 0 && v0 + 8 * q < k) out[(long long)blockIdx.x * 128 + v0 + 8 * q] = t;
+    }
+  }
+}
+
 int main() {
   const long long n = 10489857, n4 = (n + 3) & ~3LL;
   const int k = 100;
@@ -116,8 +171,9 @@ int main() {
     if (pad == -1) ld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4;
     if (pad == -2) ld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4 + 1024;
     const double bytes = double(k) * n * 4;
-    const char *names[] = {"combine", "gram_u4v1", "gram_u8v1", "gram_u16v1", "gram_u8v2"};
-    for (int kind = 0; kind < 5; ++kind) {
+    const char *names[] = {"combine", "gram_u4v1", "gram_u8v1", "gram_u16v1", "gram_u8v2", "gram3_u4v1", "gram3_u4v2",
+                           "gram3_u8v1"};
+    for (int kind = 0; kind < 8; ++kind) {
       if (kind > 1 && pad != 0 && pad != -2) continue; // the in-flight variants at two strides only
       float best = 1e30f, sum = 0.0f;
       for (int it = 0; it < 6; ++it) {
@@ -127,7 +183,10 @@ int main() {
         else if (kind == 1) hipLaunchKernelGGL((gram_k<4, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         else if (kind == 2) hipLaunchKernelGGL((gram_k<8, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         else if (kind == 3) hipLaunchKernelGGL((gram_k<16, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
-        else hipLaunchKernelGGL((gram_k<8, 2>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else if (kind == 4) hipLaunchKernelGGL((gram_k<8, 2>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else if (kind == 5) hipLaunchKernelGGL((gram3_k<4, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else if (kind == 6) hipLaunchKernelGGL((gram3_k<4, 2>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else hipLaunchKernelGGL((gram3_k<8, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms = 0;
