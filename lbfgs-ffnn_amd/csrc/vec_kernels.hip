@@ -853,7 +853,9 @@ int gram_nwg(long long n) {
   // 2561 chunks of 4096 were 3.33 rounds of 768 resident workgroups, the last a third full; now 3072 of
   // 3416), chunks still <= 4096.
   const long long slots = gram_slots();
-  static const int whole_rounds = env_int("LBF_GRAM_ROUNDS", 1); // A/B: 0 keeps the 4096-element chunks
+  // (whole rounds of workgroups measured no faster than 4096-element chunks, 5.35-5.41 against 5.44-5.47 TB/s at
+  // n = 10.49M, profiles/r06/h/; LBF_GRAM_ROUNDS=1 for the A/B)
+  static const int whole_rounds = env_int("LBF_GRAM_ROUNDS", 0);
   if (whole_rounds && w > slots) w = cdiv(need, slots) * slots;
   return int(w < 1 ? 1 : w);
 }

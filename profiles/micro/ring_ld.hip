@@ -90,7 +90,7 @@ __global__ __launch_bounds__(512) void gram_k(const float *H, long long ld, int 
 // The engine's Gram sweep arithmetic on the same pattern: three fp32 vectors (s, y, g) of the chunk in LDS (48 KB:
 // three workgroups per CU, as gram_kernel), three fp64 dots per history vector, V history vectors per pass sharing
 // each LDS read, U quads of each in flight.
-template <int U, int V>
+template <int U, int V, int TR = -1>
 __global__ __launch_bounds__(512) void gram3_k(const float *H, long long ld, int k, double *out, long long n) {
   __shared__ float ls[4096], ly[4096], lg[4096];
   const long long e0 = (long long)blockIdx.x * 4096;
@@ -135,9 +135,19 @@ __global__ __launch_bounds__(512) void gram3_k(const float *H, long long ld, int
     }
 #pragma unroll
     for (int q = 0; q < V; ++q) {
-      double t = ds[q] + 2.0 * dy[q] + 3.0 * dg[q];
-      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
-      if (lane == 0 && v0 + 8 * q < k) out[(long long)blockIdx.x * 128 + v0 + 8 * q] = t;
+      if (TR < 0) {
+        double t = ds[q] + 2.0 * dy[q] + 3.0 * dg[q];
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+        if (lane == 0 && v0 + 8 * q < k) out[(long long)blockIdx.x * 128 + v0 + 8 * q] = t;
+      } else { // the engine's three partials per vector: transposed [col][block] (TR = 1) or [block][col] (TR = 0)
+        double d3[3] = {ds[q], dy[q], dg[q]};
+        for (int c = 0; c < 3; ++c)
+          for (int o = 32; o > 0; o >>= 1) d3[c] += __shfl_xor(d3[c], o);
+        const int col = 3 * (v0 + 8 * q);
+        if (lane == 0 && v0 + 8 * q < k)
+          for (int c = 0; c < 3; ++c)
+            out[TR ? (long long)(col + c) * gridDim.x + blockIdx.x : (long long)blockIdx.x * 384 + col + c] = d3[c];
+      }
     }
   }
 }
@@ -158,7 +168,7 @@ int main() {
   CK(hipMalloc(&flush, size_t(512) << 20));
   CK(hipMalloc(&c, 128 * 8));
   const int nch = int((n + 4095) / 4096);
-  CK(hipMalloc(&gout, size_t(nch) * 128 * 8));
+  CK(hipMalloc(&gout, size_t(nch) * 384 * 8));
   CK(hipMemset(H, 0, size_t(maxld) * k * 4));
   std::vector<double> hc(128, 0.01);
   CK(hipMemcpy(c, hc.data(), 128 * 8, hipMemcpyHostToDevice));
@@ -172,8 +182,8 @@ int main() {
     if (pad == -2) ld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4 + 1024;
     const double bytes = double(k) * n * 4;
     const char *names[] = {"combine", "gram_u4v1", "gram_u8v1", "gram_u16v1", "gram_u8v2", "gram3_u4v1", "gram3_u4v2",
-                           "gram3_u8v1"};
-    for (int kind = 0; kind < 8; ++kind) {
+                           "gram3_u8v1", "gram3_tr1", "gram3_tr0"};
+    for (int kind = 0; kind < 10; ++kind) {
       if (kind > 1 && pad != 0 && pad != -2) continue; // the in-flight variants at two strides only
       float best = 1e30f, sum = 0.0f;
       for (int it = 0; it < 6; ++it) {
@@ -186,7 +196,9 @@ int main() {
         else if (kind == 4) hipLaunchKernelGGL((gram_k<8, 2>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         else if (kind == 5) hipLaunchKernelGGL((gram3_k<4, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         else if (kind == 6) hipLaunchKernelGGL((gram3_k<4, 2>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
-        else hipLaunchKernelGGL((gram3_k<8, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else if (kind == 7) hipLaunchKernelGGL((gram3_k<8, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else if (kind == 8) hipLaunchKernelGGL((gram3_k<4, 1, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else hipLaunchKernelGGL((gram3_k<4, 1, 0>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms = 0;
