@@ -265,17 +265,25 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs 
   __shared__ double ws[4];
   __shared__ int s_last;
   __shared__ int ist_l[IST_ORDER + GRAM_FIN_MAXM + 4];
-  const int c = blockIdx.x, t = threadIdx.x;
+  const int t = threadIdx.x;
+  // row-major partials (the Gram sweep's, gram_fin): column c's values are ncols apart, so each XCD (blocks b and
+  // b + 8 share one, xcd_tile's bijection) takes a contiguous range of columns and fetches their lines once
+  int c = blockIdx.x;
+  if (a.row_major) {
+    const int q = ncols >> 3, r8 = ncols & 7, x = c & 7;
+    c = (x < r8 ? x * (q + 1) : r8 * (q + 1) + (x - r8) * q) + (c >> 3);
+  }
   const int count0 = a.g.reset ? 0 : h.ist[IST_COUNT];
   if (!(c < 6 * h.m && c >= 6 * count0)) { // only the columns in use (live pairs and the self block)
-    const double *colp = a.rows + (long long)c * a.nb;
+    const double *colp = a.rows + (a.row_major ? (long long)c : (long long)c * a.nb);
+    const long long rs = a.row_major ? ncols : 1;
     double v[8];
     double s = 0.0;
     for (int r0 = t; r0 < a.nb; r0 += DF_THREADS * 8) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) { // unconditional loads from clamped rows: all eight in flight at once
         const int r = r0 + DF_THREADS * u;
-        v[u] = colp[r < a.nb ? r : 0];
+        v[u] = colp[(r < a.nb ? r : 0) * rs];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += (r0 + DF_THREADS * u < a.nb) ? v[u] : 0.0;

@@ -420,7 +420,8 @@ struct DirArgs {
   int want_dir = 1;         // 0 (pair only) or 1
   int iter = 1;
   double dsign = 1.0;
-  double *rows = nullptr;   // [dir_ncols(m)][nb]
+  double *rows = nullptr;   // [dir_ncols(m)][nb], or [nb][dir_ncols(m)] when row_major (gram_fin)
+  int row_major = 0;
   double *dots = nullptr;   // [dir_ncols(m)]
   int nb = 0;               // cdiv(n, dir_cols_per_block(m, n))
   unsigned *cols_done = nullptr; // arrival counter, zero between launches

@@ -1182,9 +1182,13 @@ bool History::update_impl(const GramArgs &g0, int want_dir, int iter, double dsi
     d.dots = gdots_.get();
     d.nb = gram_nwg(v_.n);
     d.cols_done = gcount_.get();
+    // the sweep's partial rows stored row-major (one contiguous row per workgroup): its transposed stores, three
+    // scattered doubles per history vector per workgroup, cost the sweep 13 % in profiles/micro/ring_ld.hip
+    // (gram3_tr1 / tr0) and 5.44 against 5.59 TB/s in the engine (LBF_GRAM_FIN=1 / 0, profiles/r06/i/)
+    d.row_major = 1;
     {
       ProfScope ps(ctx_, PK_GRAM);
-      gram_update(s, g, part_.get(), 1);
+      gram_update(s, g, part_.get(), 0);
     }
     ProfScope ps(ctx_, PK_COEF);
     gram_fin(s, d);
