@@ -152,6 +152,89 @@ __global__ __launch_bounds__(512) void gram3_k(const float *H, long long ld, int
   }
 }
 
+// gram3 with the engine's first phase: per chunk the new vectors s = x - xp, y = g - gp and g formed from five
+// 16-B operand streams into LDS, s and y written to a ring slot, g to g_out, six self dots reduced over the block,
+// then the history phase (gram3_k<4, 1, 0>'s, row-major partials).
+__global__ __launch_bounds__(512) void gram3p_k(const float *H, long long ld, int k, double *out, long long n,
+                                                const float *x, const float *xp, const float *g, const float *gp,
+                                                float *sw, float *yw, float *gout) {
+  __shared__ __attribute__((aligned(16))) float ls[4096], ly[4096], lg[4096];
+  __shared__ double red[8][6];
+  const long long e0 = (long long)blockIdx.x * 4096;
+  double self[6] = {0, 0, 0, 0, 0, 0};
+  const int nq = int(min(4096LL, n - e0) >> 2);
+  for (int q0 = threadIdx.x; q0 < nq; q0 += 1024) {
+    f32x4 op[2][5];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = min(q0 + u * 512, nq - 1);
+      const long long e = e0 + 4LL * q;
+      const float *src[5] = {x, xp, g, gp, g};
+#pragma unroll
+      for (int j = 0; j < 5; ++j) op[u][j] = *reinterpret_cast<const f32x4 *>(src[j] + e);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = q0 + u * 512;
+      if (q >= nq) break;
+      const f32x4 s4 = op[u][0] - op[u][1], y4 = op[u][2] - op[u][3], g4 = op[u][4];
+      *reinterpret_cast<f32x4 *>(ls + 4 * q) = s4;
+      *reinterpret_cast<f32x4 *>(ly + 4 * q) = y4;
+      *reinterpret_cast<f32x4 *>(lg + 4 * q) = g4;
+      *reinterpret_cast<f32x4 *>(sw + e0 + 4 * q) = s4;
+      *reinterpret_cast<f32x4 *>(yw + e0 + 4 * q) = y4;
+      *reinterpret_cast<f32x4 *>(gout + e0 + 4 * q) = g4;
+      for (int c = 0; c < 4; ++c) {
+        const double sv = s4[c], yv = y4[c], gv = g4[c];
+        self[0] += sv * sv; self[1] += sv * yv; self[2] += yv * yv;
+        self[3] += gv * sv; self[4] += gv * yv; self[5] += gv * gv;
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int j = 0; j < 6; ++j) {
+    double t = self[j];
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if (lane == 0) red[wave][j] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    double t = 0;
+    for (int w = 0; w < 8; ++w) t += red[w][threadIdx.x];
+    out[(long long)blockIdx.x * 384 + 300 + threadIdx.x] = t;
+  }
+  for (int v0 = wave; v0 < k; v0 += 8) {
+    double ds = 0, dy = 0, dg = 0;
+    const float *Vp = H + (long long)v0 * ld + e0;
+    for (int i0 = lane * 4; i0 < 4096; i0 += 1024) {
+      f32x4 xv4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long ee = e0 + i0 + 256 * u;
+        xv4[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(Vp + (ee + 3 < n ? i0 + 256 * u : 0)));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 s4 = *reinterpret_cast<const f32x4 *>(ls + i0 + 256 * u);
+        const f32x4 y4 = *reinterpret_cast<const f32x4 *>(ly + i0 + 256 * u);
+        const f32x4 g4 = *reinterpret_cast<const f32x4 *>(lg + i0 + 256 * u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const double xv = xv4[u][j];
+          ds += xv * double(s4[j]);
+          dy += xv * double(y4[j]);
+          dg += xv * double(g4[j]);
+        }
+      }
+    }
+    double d3[3] = {ds, dy, dg};
+    for (int c = 0; c < 3; ++c)
+      for (int o = 32; o > 0; o >>= 1) d3[c] += __shfl_xor(d3[c], o);
+    if (lane == 0)
+      for (int c = 0; c < 3; ++c) out[(long long)blockIdx.x * 384 + 3 * v0 + c] = d3[c];
+  }
+}
+
 int main() {
   const long long n = 10489857, n4 = (n + 3) & ~3LL;
   const int k = 100;
@@ -169,6 +252,9 @@ int main() {
   CK(hipMalloc(&c, 128 * 8));
   const int nch = int((n + 4095) / 4096);
   CK(hipMalloc(&gout, size_t(nch) * 384 * 8));
+  float *V5 = nullptr; // gram3p's operand and output vectors (x, xp, g, gp, s slot, y slot, g_out)
+  CK(hipMalloc(&V5, size_t(7) * n4 * 4));
+  CK(hipMemset(V5, 0, size_t(7) * n4 * 4));
   CK(hipMemset(H, 0, size_t(maxld) * k * 4));
   std::vector<double> hc(128, 0.01);
   CK(hipMemcpy(c, hc.data(), 128 * 8, hipMemcpyHostToDevice));
@@ -180,12 +266,13 @@ int main() {
     long long ld = n4 + (pad > 0 ? pad : 0);
     if (pad == -1) ld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4;
     if (pad == -2) ld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4 + 1024;
-    const double bytes = double(k) * n * 4;
+    double bytes = double(k) * n * 4;
     const char *names[] = {"combine", "gram_u4v1", "gram_u8v1", "gram_u16v1", "gram_u8v2", "gram3_u4v1", "gram3_u4v2",
-                           "gram3_u8v1", "gram3_tr1", "gram3_tr0"};
-    for (int kind = 0; kind < 10; ++kind) {
+                           "gram3_u8v1", "gram3_tr1", "gram3_tr0", "gram3p"};
+    for (int kind = 0; kind < 11; ++kind) {
       if (kind > 1 && pad != 0 && pad != -2) continue; // the in-flight variants at two strides only
       float best = 1e30f, sum = 0.0f;
+      bytes = double(k + (kind == 10 ? 7 : 0)) * n * 4; // gram3p: + 4 operand reads and 3 writes (g read twice)
       for (int it = 0; it < 6; ++it) {
         CK(hipMemset(flush, it, size_t(512) << 20)); // evict the Infinity Cache between runs
         CK(hipEventRecord(a));
@@ -198,7 +285,9 @@ int main() {
         else if (kind == 6) hipLaunchKernelGGL((gram3_k<4, 2>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         else if (kind == 7) hipLaunchKernelGGL((gram3_k<8, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         else if (kind == 8) hipLaunchKernelGGL((gram3_k<4, 1, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
-        else hipLaunchKernelGGL((gram3_k<4, 1, 0>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else if (kind == 9) hipLaunchKernelGGL((gram3_k<4, 1, 0>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
+        else hipLaunchKernelGGL(gram3p_k, dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n, V5, V5 + n4, V5 + 2 * n4,
+                                V5 + 3 * n4, V5 + 4 * n4, V5 + 5 * n4, V5 + 6 * n4);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms = 0;
