@@ -155,6 +155,8 @@ __global__ __launch_bounds__(512) void gram3_k(const float *H, long long ld, int
 // gram3 with the engine's first phase: per chunk the new vectors s = x - xp, y = g - gp and g formed from five
 // 16-B operand streams into LDS, s and y written to a ring slot, g to g_out, six self dots reduced over the block,
 // then the history phase (gram3_k<4, 1, 0>'s, row-major partials).
+template <int VAR> // 0: the engine's phase 1; 1: without its three global stores; 2: without the block reduction;
+                   // 3: the new vectors read from three streams (s, y, g precomputed: a split sweep's second kernel)
 __global__ __launch_bounds__(512) void gram3p_k(const float *H, long long ld, int k, double *out, long long n,
                                                 const float *x, const float *xp, const float *g, const float *gp,
                                                 float *sw, float *yw, float *gout) {
@@ -170,20 +172,28 @@ __global__ __launch_bounds__(512) void gram3p_k(const float *H, long long ld, in
       const int q = min(q0 + u * 512, nq - 1);
       const long long e = e0 + 4LL * q;
       const float *src[5] = {x, xp, g, gp, g};
+      if (VAR == 3) {
+        src[0] = sw;
+        src[2] = yw;
+      }
 #pragma unroll
-      for (int j = 0; j < 5; ++j) op[u][j] = *reinterpret_cast<const f32x4 *>(src[j] + e);
+      for (int j = 0; j < 5; ++j)
+        if (VAR != 3 || j == 0 || j == 2 || j == 4) op[u][j] = *reinterpret_cast<const f32x4 *>(src[j] + e);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int q = q0 + u * 512;
       if (q >= nq) break;
-      const f32x4 s4 = op[u][0] - op[u][1], y4 = op[u][2] - op[u][3], g4 = op[u][4];
+      const f32x4 s4 = VAR == 3 ? op[u][0] : op[u][0] - op[u][1], y4 = VAR == 3 ? op[u][2] : op[u][2] - op[u][3];
+      const f32x4 g4 = op[u][4];
       *reinterpret_cast<f32x4 *>(ls + 4 * q) = s4;
       *reinterpret_cast<f32x4 *>(ly + 4 * q) = y4;
       *reinterpret_cast<f32x4 *>(lg + 4 * q) = g4;
-      *reinterpret_cast<f32x4 *>(sw + e0 + 4 * q) = s4;
-      *reinterpret_cast<f32x4 *>(yw + e0 + 4 * q) = y4;
-      *reinterpret_cast<f32x4 *>(gout + e0 + 4 * q) = g4;
+      if (VAR == 0 || VAR == 2) {
+        *reinterpret_cast<f32x4 *>(sw + e0 + 4 * q) = s4;
+        *reinterpret_cast<f32x4 *>(yw + e0 + 4 * q) = y4;
+        *reinterpret_cast<f32x4 *>(gout + e0 + 4 * q) = g4;
+      }
       for (int c = 0; c < 4; ++c) {
         const double sv = s4[c], yv = y4[c], gv = g4[c];
         self[0] += sv * sv; self[1] += sv * yv; self[2] += yv * yv;
@@ -192,16 +202,21 @@ __global__ __launch_bounds__(512) void gram3p_k(const float *H, long long ld, in
     }
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int j = 0; j < 6; ++j) {
-    double t = self[j];
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
-    if (lane == 0) red[wave][j] = t;
-  }
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    double t = 0;
-    for (int w = 0; w < 8; ++w) t += red[w][threadIdx.x];
-    out[(long long)blockIdx.x * 384 + 300 + threadIdx.x] = t;
+  if (VAR != 2 && VAR != 3) {
+    for (int j = 0; j < 6; ++j) {
+      double t = self[j];
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+      if (lane == 0) red[wave][j] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+      double t = 0;
+      for (int w = 0; w < 8; ++w) t += red[w][threadIdx.x];
+      out[(long long)blockIdx.x * 384 + 300 + threadIdx.x] = t;
+    }
+  } else {
+    __syncthreads();
+    if (self[0] == 1234.5) out[0] = self[1] + self[2] + self[3] + self[4] + self[5]; // keep the products
   }
   for (int v0 = wave; v0 < k; v0 += 8) {
     double ds = 0, dy = 0, dg = 0;
@@ -268,11 +283,13 @@ int main() {
     if (pad == -2) ld = ((n4 * 4 + (2 << 20) - 1) / (2 << 20)) * (2 << 20) / 4 + 1024;
     double bytes = double(k) * n * 4;
     const char *names[] = {"combine", "gram_u4v1", "gram_u8v1", "gram_u16v1", "gram_u8v2", "gram3_u4v1", "gram3_u4v2",
-                           "gram3_u8v1", "gram3_tr1", "gram3_tr0", "gram3p"};
-    for (int kind = 0; kind < 11; ++kind) {
+                           "gram3_u8v1", "gram3_tr1", "gram3_tr0", "gram3p", "gram3p_nost", "gram3p_nored",
+                           "gram3p_split"};
+    for (int kind = 0; kind < 14; ++kind) {
       if (kind > 1 && pad != 0 && pad != -2) continue; // the in-flight variants at two strides only
       float best = 1e30f, sum = 0.0f;
-      bytes = double(k + (kind == 10 ? 7 : 0)) * n * 4; // gram3p: + 4 operand reads and 3 writes (g read twice)
+      // gram3p: + 4 operand reads and 3 writes (g read twice); without the stores + 4; split: + 3 reads
+      bytes = double(k + (kind == 10 || kind == 12 ? 7 : (kind == 11 ? 4 : (kind == 13 ? 3 : 0)))) * n * 4;
       for (int it = 0; it < 6; ++it) {
         CK(hipMemset(flush, it, size_t(512) << 20)); // evict the Infinity Cache between runs
         CK(hipEventRecord(a));
@@ -286,8 +303,14 @@ int main() {
         else if (kind == 7) hipLaunchKernelGGL((gram3_k<8, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         else if (kind == 8) hipLaunchKernelGGL((gram3_k<4, 1, 1>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
         else if (kind == 9) hipLaunchKernelGGL((gram3_k<4, 1, 0>), dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n);
-        else hipLaunchKernelGGL(gram3p_k, dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n, V5, V5 + n4, V5 + 2 * n4,
-                                V5 + 3 * n4, V5 + 4 * n4, V5 + 5 * n4, V5 + 6 * n4);
+        else if (kind == 10) hipLaunchKernelGGL(gram3p_k<0>, dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n, V5, V5 + n4,
+                                                V5 + 2 * n4, V5 + 3 * n4, V5 + 4 * n4, V5 + 5 * n4, V5 + 6 * n4);
+        else if (kind == 11) hipLaunchKernelGGL(gram3p_k<1>, dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n, V5, V5 + n4,
+                                                V5 + 2 * n4, V5 + 3 * n4, V5 + 4 * n4, V5 + 5 * n4, V5 + 6 * n4);
+        else if (kind == 12) hipLaunchKernelGGL(gram3p_k<2>, dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n, V5, V5 + n4,
+                                                V5 + 2 * n4, V5 + 3 * n4, V5 + 4 * n4, V5 + 5 * n4, V5 + 6 * n4);
+        else hipLaunchKernelGGL(gram3p_k<3>, dim3(nch), dim3(512), 0, 0, H, ld, k, gout, n, V5, V5 + n4,
+                                V5 + 2 * n4, V5 + 3 * n4, V5 + 4 * n4, V5 + 5 * n4, V5 + 6 * n4);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms = 0;
