@@ -829,7 +829,7 @@ static constexpr int GRAM_THREADS = 512;
 static long long gram_max_chunk() { return 4096; }
 
 int gram_ncols(int m) { return 6 * m + 6; }
-template <int U, bool NT>
+template <int U, bool NT, int MODE = 0>
 __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, long long chunk, double *partials, int tr,
                                                             int vec);
 // Workgroups of the Gram sweep resident on the whole chip at the largest chunk (LDS-bound: 3 per CU), once.
@@ -885,7 +885,13 @@ __device__ __forceinline__ GramNew gram_new(const GramArgs &a, float sa, float s
 // tr: partials stored transposed, [ncols][gridDim.x] (each column contiguous for gram_fin's column sums);
 // else [gridDim.x][ncols] (hist_step / fold_rows). vec: every operand and the ring 16-B aligned (host
 // check), so the new vectors are formed from 16-B loads, all issued before the first use.
-template <int U, bool NT>
+// MODE 0: the fused sweep (the new vectors formed into LDS and the ring, then the history). The split sweep
+// (large n, gram_update): MODE 1 forms the new vectors, writes s, y into the ring slot (and g_out), and stores the
+// self dots' partial row entries, with the same chunks, threads and block sum as MODE 0 (bitwise its self dots);
+// MODE 2 then stages s, y, g of its chunk from memory into LDS and runs the history phase. The fused form's
+// phase-1 stores, made between the history streams, cost the sweep far more than their bytes (5.2-5.7 TB/s
+// against 5.8-6.0 split, profiles/micro/ring_ld.hip gram3p_*, profiles/r06/k2/).
+template <int U, bool NT, int MODE>
 __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, long long chunk, double *partials, int tr,
                                                             int vec) {
   if (a.h.abort && *a.h.abort) return;
@@ -909,9 +915,11 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
   float *Yw = h.Y + (long long)w * h.ld + e0;
   const float ysc = float(a.yscale);
   auto put = [&](int i, const GramNew &r) {
-    ls[i] = r.sv;
-    ly[i] = r.yv;
-    lg[i] = r.gv;
+    if (MODE == 0) {
+      ls[i] = r.sv;
+      ly[i] = r.yv;
+      lg[i] = r.gv;
+    }
     const double s = r.sv, y = r.yv, g = r.gv;
     self[0] += s * s;
     self[1] += s * y;
@@ -921,7 +929,28 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
     self[5] += g * g;
   };
   int i_scalar = 0;
-  if (vec) { // two quads per thread per round, all seven operand loads of both issued up front
+  if (MODE == 2) { // staged: s, y from the ring slot MODE 1 wrote, g from g_out / ga (zeros where MODE 0 has them)
+    const float *gsrc = (a.gb || a.gc) ? a.g_out : a.ga;
+    if (vec) {
+      const int nq = len >> 2;
+      for (int q = threadIdx.x; q < nq; q += GRAM_THREADS) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 s4 = a.has_pair ? *reinterpret_cast<const f32x4 *>(Sw + 4 * q) : z;
+        const f32x4 y4 = a.has_pair ? *reinterpret_cast<const f32x4 *>(Yw + 4 * q) : z;
+        const f32x4 g4 = a.has_g ? *reinterpret_cast<const f32x4 *>(gsrc + e0 + 4 * q) : z;
+        *reinterpret_cast<f32x4 *>(ls + 4 * q) = s4;
+        *reinterpret_cast<f32x4 *>(ly + 4 * q) = y4;
+        *reinterpret_cast<f32x4 *>(lg + 4 * q) = g4;
+      }
+      i_scalar = 4 * nq;
+    }
+    for (int i = i_scalar + int(threadIdx.x); i < len; i += blockDim.x) {
+      ls[i] = a.has_pair ? Sw[i] : 0.f;
+      ly[i] = a.has_pair ? Yw[i] : 0.f;
+      lg[i] = a.has_g ? gsrc[e0 + i] : 0.f;
+    }
+    __syncthreads();
+  } else if (vec) { // two quads per thread per round, all seven operand loads of both issued up front
     const int nq = len >> 2;
     const float *dflt = a.ga ? a.ga : a.sa; // null operands read this and are masked
     for (int q0 = threadIdx.x; q0 < nq; q0 += 2 * GRAM_THREADS) {
@@ -957,25 +986,29 @@ __global__ __launch_bounds__(GRAM_THREADS) void gram_kernel(const GramArgs a, lo
     }
     i_scalar = 4 * nq;
   }
-  for (int i = i_scalar + int(threadIdx.x); i < len; i += blockDim.x) {
-    const long long e = e0 + i;
-    const GramNew r = gram_new(a, a.has_pair ? a.sa[e] : 0.f, a.has_pair ? a.sb[e] : 0.f, a.has_pair ? a.ya[e] : 0.f,
-                               a.has_pair ? a.yb[e] : 0.f, a.has_g ? a.ga[e] : 0.f, a.gb ? a.gb[e] : 0.f,
-                               a.gc ? a.gc[e] : 0.f, ysc);
-    if (a.has_pair) {
-      Sw[i] = r.sv;
-      Yw[i] = r.yv;
+  if (MODE != 2)
+    for (int i = i_scalar + int(threadIdx.x); i < len; i += blockDim.x) {
+      const long long e = e0 + i;
+      const GramNew r = gram_new(a, a.has_pair ? a.sa[e] : 0.f, a.has_pair ? a.sb[e] : 0.f, a.has_pair ? a.ya[e] : 0.f,
+                                 a.has_pair ? a.yb[e] : 0.f, a.has_g ? a.ga[e] : 0.f, a.gb ? a.gb[e] : 0.f,
+                                 a.gc ? a.gc[e] : 0.f, ysc);
+      if (a.has_pair) {
+        Sw[i] = r.sv;
+        Yw[i] = r.yv;
+      }
+      if (a.has_g && a.g_out) a.g_out[e] = r.gv;
+      put(i, r);
     }
-    if (a.has_g && a.g_out) a.g_out[e] = r.gv;
-    put(i, r);
-  }
   KT(17);
-  block_sum<6>(self, scratch); // includes __syncthreads: LDS vectors complete after this
-  KT(18);
   const long long rs = tr ? (long long)gridDim.x : 1LL; // column stride of the partial table
   double *out = partials + (tr ? (long long)blockIdx.x : (long long)blockIdx.x * ncols);
-  if (threadIdx.x == 0)
-    for (int j = 0; j < 6; ++j) out[(6 * h.m + j) * rs] = self[j];
+  if (MODE != 2) {
+    block_sum<6>(self, scratch); // includes __syncthreads: LDS vectors complete after this
+    KT(18);
+    if (threadIdx.x == 0)
+      for (int j = 0; j < 6; ++j) out[(6 * h.m + j) * rs] = self[j];
+    if (MODE == 1) return;
+  }
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int v = wave; v < 2 * count; v += nw) {
@@ -1046,7 +1079,9 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials, int transpo
   if (shmem > 64 * 1024) { // once per process, thread-safe
     static const bool attr_set = [] {
       for (const void *f : {reinterpret_cast<const void *>(gram_kernel<4, false>),
-                            reinterpret_cast<const void *>(gram_kernel<4, true>)})
+                            reinterpret_cast<const void *>(gram_kernel<4, true>),
+                            reinterpret_cast<const void *>(gram_kernel<4, false, 2>),
+                            reinterpret_cast<const void *>(gram_kernel<4, true, 2>)})
         LBF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
       return true;
     }();
@@ -1058,6 +1093,20 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials, int transpo
                   al16(a.sa) && al16(a.sb) && al16(a.ya) && al16(a.yb) && al16(a.ga) && al16(a.gb) && al16(a.gc) &&
                   al16(a.g_out);
   const int tr = transposed ? 1 : 0;
+  // the split sweep (MODE 1 then 2) for the large-n history, where g is readable afterwards (ga, or g_out when formed)
+  static const int split_on = env_int("LBF_GRAM_SPLIT", 1); // A/B: 0 keeps the fused sweep
+  if (split_on && vec && a.h.n >= (1LL << 21) && !(a.has_g && (a.gb || a.gc) && !a.g_out)) {
+    const dim3 g1{unsigned(nwg), 1, 1}, b1{unsigned(GRAM_THREADS), 1, 1};
+    if (nt) {
+      hipLaunchKernelGGL((gram_kernel<4, true, 1>), g1, b1, 0, s, a, chunk, partials, tr, vec);
+      hipLaunchKernelGGL((gram_kernel<4, true, 2>), g1, b1, shmem, s, a, chunk, partials, tr, vec);
+    } else {
+      hipLaunchKernelGGL((gram_kernel<4, false, 1>), g1, b1, 0, s, a, chunk, partials, tr, vec);
+      hipLaunchKernelGGL((gram_kernel<4, false, 2>), g1, b1, shmem, s, a, chunk, partials, tr, vec);
+    }
+    LBF_KERNEL_CHECK();
+    return;
+  }
   if (nt)
     hipLaunchKernelGGL((gram_kernel<4, true>), dim3(nwg), dim3(GRAM_THREADS), shmem, s, a, chunk, partials, tr, vec);
   else
