@@ -1106,7 +1106,11 @@ History::History(Ctx *ctx, int m, long long n) : ctx_(ctx) {
     dcount_.resize(1);
     LBF_HIP(hipMemsetAsync(dcount_.get(), 0, sizeof(unsigned), ctx_->stream));
   }
-  gfin_on_ = gram_fin_supported(m) && env_int("LBF_GRAM_FIN", 1) != 0;
+  // Column sums + last-block step (gram_fin) for short histories; for m > 20 the fold_rows + hist_step route, which
+  // measured faster there (two-loop at n = 10.49M: m = 10 58.0 against 57.5 %, m = 50 67.7 against 68.1 %,
+  // profiles/r06/j/). LBF_GRAM_FIN=1 / 0 forces either route (tests compare them).
+  const int gf = env_int("LBF_GRAM_FIN", -1);
+  gfin_on_ = gram_fin_supported(m) && (gf == 1 || (gf < 0 && m <= 20));
   if (gfin_on_) {
     gdots_.resize(size_t(gram_ncols(m)));
     gcount_.resize(1);

@@ -1095,7 +1095,9 @@ void gram_update(hipStream_t s, const GramArgs &a, double *partials, int transpo
   const int tr = transposed ? 1 : 0;
   // the split sweep (MODE 1 then 2) for the large-n history, where g is readable afterwards (ga, or g_out when formed)
   static const int split_on = env_int("LBF_GRAM_SPLIT", 1); // A/B: 0 keeps the fused sweep
-  if (split_on && vec && a.h.n >= (1LL << 21) && !(a.has_g && (a.gb || a.gc) && !a.g_out)) {
+  // (long histories only: at m = 10 the extra launch and the three staged reads cost what the split saves, two-loop
+  // 56.9-57.5 % split against 57.1-58.1 % fused; m = 50 68.9-69.6 % against 67.2-67.3 %, profiles/r06/m/)
+  if (split_on && vec && a.h.n >= (1LL << 21) && a.h.m >= 20 && !(a.has_g && (a.gb || a.gc) && !a.g_out)) {
     const dim3 g1{unsigned(nwg), 1, 1}, b1{unsigned(GRAM_THREADS), 1, 1};
     if (nt) {
       hipLaunchKernelGGL((gram_kernel<4, true, 1>), g1, b1, 0, s, a, chunk, partials, tr, vec);
