@@ -1350,7 +1350,7 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineArgs a) {
 // c0 + 1024 w .., lane l the quads 256 u + 4 l (u < 4), so each vector is read as 4 KB contiguous per wave and
 // 16 KB per workgroup, V vectors' quads (2 V x 4 loads) in flight per lane. Per element the same fp64 sum in the
 // same order as combine_kernel (cg g, then cs_i S_i + cy_i Y_i for i = 0 .. k - 1).
-template <int V, bool NT>
+template <int V, bool NT, int Q = 4>
 __global__ __launch_bounds__(256) void combine_chunk_kernel(const CombineArgs a) {
   if (a.h.abort && *a.h.abort) return;
   __shared__ double cs[COEF_MAXK], cy[COEF_MAXK];
@@ -1368,30 +1368,31 @@ __global__ __launch_bounds__(256) void combine_chunk_kernel(const CombineArgs a)
   const double alpha = a.alpha_from_state ? h.scal[SC_ALPHA0] : a.alpha;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float *xsrc = a.x_out ? a.x_in : a.g;
-  for (long long c0 = (long long)blockIdx.x * 4096; c0 < h.n; c0 += (long long)gridDim.x * 4096) {
-    long long e[4], ec[4];
-    bool full[4];
+  constexpr int CH = 1024 * Q; // elements per chunk: wave w the 256 Q contiguous elements c0 + 256 Q w ..
+  for (long long c0 = (long long)blockIdx.x * CH; c0 < h.n; c0 += (long long)gridDim.x * CH) {
+    long long e[Q], ec[Q];
+    bool full[Q];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      e[u] = c0 + wave * 1024 + u * 256 + 4 * lane;
+    for (int u = 0; u < Q; ++u) {
+      e[u] = c0 + wave * 256 * Q + u * 256 + 4 * lane;
       full[u] = e[u] + 3 < h.n;
       ec[u] = full[u] ? e[u] : 0; // clamped: loads unconditional, results masked
     }
-    double acc[4][4];
+    double acc[Q][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < Q; ++u) {
       const f32x4 g4 = *reinterpret_cast<const f32x4 *>(a.g + ec[u]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[u][j] = cg * double(g4[j]);
     }
     int i = 0;
     for (; i + V <= k; i += V) {
-      f32x4 s4[V][4], y4[V][4];
+      f32x4 s4[V][Q], y4[V][Q];
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const long long sb = (long long)L[i + v] * h.ld;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < Q; ++u) {
           s4[v][u] = hist_load<NT>(h.S + sb + ec[u]);
           y4[v][u] = hist_load<NT>(h.Y + sb + ec[u]);
         }
@@ -1399,14 +1400,14 @@ __global__ __launch_bounds__(256) void combine_chunk_kernel(const CombineArgs a)
 #pragma unroll
       for (int v = 0; v < V; ++v)
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < Q; ++u)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[u][j] += cs[i + v] * double(s4[v][u][j]) + cy[i + v] * double(y4[v][u][j]);
     }
     for (; i < k; ++i) {
       const long long sb = (long long)L[i] * h.ld;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < Q; ++u) {
         const f32x4 s4 = hist_load<NT>(h.S + sb + ec[u]);
         const f32x4 y4 = hist_load<NT>(h.Y + sb + ec[u]);
 #pragma unroll
@@ -1414,7 +1415,7 @@ __global__ __launch_bounds__(256) void combine_chunk_kernel(const CombineArgs a)
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < Q; ++u) {
       if (full[u]) {
         f32x4 d4;
 #pragma unroll
@@ -1504,19 +1505,30 @@ void hist_combine(hipStream_t s, const CombineArgs &a) {
   }
   static const int chunked = env_int("LBF_COMBINE_CHUNK", 1); // A/B: 0 keeps combine_kernel
   if (chunked) {
-    static const long long res_c = [] { // workgroups of combine_chunk_kernel the chip holds at once, once
-      int dev = 0, cus = 0, p1 = 0, p2 = 0;
+    // A/B of the vectors in flight per lane (V) and the quads per lane (Q; chunk 1024 Q): V2 Q4 default
+    static const int vq = env_int("LBF_COMBINE_VQ", 24);
+    const bool nt = hist_nt(a.h);
+    const void *kf = vq == 14 ? reinterpret_cast<const void *>(combine_chunk_kernel<1, true, 4>)
+                   : vq == 22 ? reinterpret_cast<const void *>(combine_chunk_kernel<2, true, 2>)
+                   : vq == 42 ? reinterpret_cast<const void *>(combine_chunk_kernel<4, true, 2>)
+                              : reinterpret_cast<const void *>(combine_chunk_kernel<2, true, 4>);
+    static const long long res_c = [kf] { // workgroups of the variant the chip holds at once, once
+      int dev = 0, cus = 0, p = 0;
       LBF_HIP(hipGetDevice(&dev));
       LBF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-      LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p1, combine_chunk_kernel<2, true>, 256, 0));
-      LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p2, combine_chunk_kernel<2, false>, 256, 0));
-      return (long long)std::max(1, cus) * std::max(1, std::min(p1, p2));
+      LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, kf, 256, 0));
+      return (long long)std::max(1, cus) * std::max(1, p);
     }();
-    const dim3 grid(unsigned(std::min(cdiv(a.h.n, 4096LL), res_c)));
-    if (hist_nt(a.h))
-      hipLaunchKernelGGL((combine_chunk_kernel<2, true>), grid, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((combine_chunk_kernel<2, false>), grid, dim3(256), 0, s, a);
+    const long long ch = 1024LL * (vq % 10 == 2 ? 2 : 4);
+    const dim3 grid(unsigned(std::min(cdiv(a.h.n, ch), res_c)));
+    switch (vq) {
+    case 14: hipLaunchKernelGGL((combine_chunk_kernel<1, true, 4>), grid, dim3(256), 0, s, a); break;
+    case 22: hipLaunchKernelGGL((combine_chunk_kernel<2, true, 2>), grid, dim3(256), 0, s, a); break;
+    case 42: hipLaunchKernelGGL((combine_chunk_kernel<4, true, 2>), grid, dim3(256), 0, s, a); break;
+    default:
+      if (nt) hipLaunchKernelGGL((combine_chunk_kernel<2, true, 4>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((combine_chunk_kernel<2, false, 4>), grid, dim3(256), 0, s, a);
+    }
     LBF_KERNEL_CHECK();
     return;
   }
