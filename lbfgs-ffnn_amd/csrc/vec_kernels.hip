@@ -1505,30 +1505,21 @@ void hist_combine(hipStream_t s, const CombineArgs &a) {
   }
   static const int chunked = env_int("LBF_COMBINE_CHUNK", 1); // A/B: 0 keeps combine_kernel
   if (chunked) {
-    // A/B of the vectors in flight per lane (V) and the quads per lane (Q; chunk 1024 Q): V2 Q4 default
-    static const int vq = env_int("LBF_COMBINE_VQ", 24);
-    const bool nt = hist_nt(a.h);
-    const void *kf = vq == 14 ? reinterpret_cast<const void *>(combine_chunk_kernel<1, true, 4>)
-                   : vq == 22 ? reinterpret_cast<const void *>(combine_chunk_kernel<2, true, 2>)
-                   : vq == 42 ? reinterpret_cast<const void *>(combine_chunk_kernel<4, true, 2>)
-                              : reinterpret_cast<const void *>(combine_chunk_kernel<2, true, 4>);
-    static const long long res_c = [kf] { // workgroups of the variant the chip holds at once, once
-      int dev = 0, cus = 0, p = 0;
+    // 2 vectors x 4 quads in flight per lane: measured against 1 x 4, 2 x 2 and 4 x 2 (m = 50: 69.9-70.0 % against
+    // 69.5-69.9, 67.3-67.6, 66.7-66.8 %; profiles/r06/o/)
+    static const long long res_c = [] { // workgroups of combine_chunk_kernel the chip holds at once, once
+      int dev = 0, cus = 0, p1 = 0, p2 = 0;
       LBF_HIP(hipGetDevice(&dev));
       LBF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-      LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, kf, 256, 0));
-      return (long long)std::max(1, cus) * std::max(1, p);
+      LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p1, combine_chunk_kernel<2, true, 4>, 256, 0));
+      LBF_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&p2, combine_chunk_kernel<2, false, 4>, 256, 0));
+      return (long long)std::max(1, cus) * std::max(1, std::min(p1, p2));
     }();
-    const long long ch = 1024LL * (vq % 10 == 2 ? 2 : 4);
-    const dim3 grid(unsigned(std::min(cdiv(a.h.n, ch), res_c)));
-    switch (vq) {
-    case 14: hipLaunchKernelGGL((combine_chunk_kernel<1, true, 4>), grid, dim3(256), 0, s, a); break;
-    case 22: hipLaunchKernelGGL((combine_chunk_kernel<2, true, 2>), grid, dim3(256), 0, s, a); break;
-    case 42: hipLaunchKernelGGL((combine_chunk_kernel<4, true, 2>), grid, dim3(256), 0, s, a); break;
-    default:
-      if (nt) hipLaunchKernelGGL((combine_chunk_kernel<2, true, 4>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((combine_chunk_kernel<2, false, 4>), grid, dim3(256), 0, s, a);
-    }
+    const dim3 grid(unsigned(std::min(cdiv(a.h.n, 4096LL), res_c)));
+    if (hist_nt(a.h))
+      hipLaunchKernelGGL((combine_chunk_kernel<2, true, 4>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((combine_chunk_kernel<2, false, 4>), grid, dim3(256), 0, s, a);
     LBF_KERNEL_CHECK();
     return;
   }
