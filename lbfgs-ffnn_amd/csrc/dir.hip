@@ -266,6 +266,7 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs 
   __shared__ int s_last;
   __shared__ int ist_l[IST_ORDER + GRAM_FIN_MAXM + 4];
   const int t = threadIdx.x;
+  KT(49);
   // row-major partials (the Gram sweep's, gram_fin): column c's values are ncols apart, so each XCD (blocks b and
   // b + 8 share one, xcd_tile's bijection) takes a contiguous range of columns and fetches their lines once
   int c = blockIdx.x;
@@ -301,6 +302,7 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs 
   __syncthreads();
   if (!s_last) return;
   if (t == 0) *a.cols_done = 0u; // ready for the next launch (stream-ordered)
+  KTF(50);
   // ---- the history step, from LDS: dots, ring header, and (fused) SY, YY, rho ----
   const int m = h.m, S_ = h.slots;
   double *SYp = dyn + 3 * m * m, *YYp = SYp + S_ * S_, *rhop = YYp + S_ * S_;
@@ -316,6 +318,7 @@ __global__ __launch_bounds__(DF_THREADS) void dir_cols_fin_kernel(const DirArgs 
     if (t < S_) rhop[t] = h.rho[t];
   }
   lds_barrier();
+  KTF(51);
   HistStep st;
   st.h = h;
   st.has_pair = a.g.has_pair;
@@ -581,3 +584,9 @@ void gram_fin(hipStream_t s, const DirArgs &a) {
 }
 
 } // namespace lbf
+
+#ifdef LBF_KTRACE
+extern "C" int lbf_dbg_ktrace_dir(unsigned long long *host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(lbf::lbf_kt_buf), size_t(n) * 8) == hipSuccess ? 0 : 1;
+}
+#endif

@@ -32,6 +32,7 @@ struct HistSmem {
   double gS_l[COEF_MAXK], gY_l[COEF_MAXK], rho_l[COEF_MAXK], alpha_l[COEF_MAXK], c_l[COEF_MAXK];
   int L0[COEF_MAXK + 1], L[COEF_MAXK + 1], inv0[COEF_MAXK + 1];
   int count0, w, k, acc, fslot;
+  int iw; // the written slot's index in the new live order (-1: not live)
   double rhow;
 };
 
@@ -83,22 +84,23 @@ template <bool LDS> __device__ __forceinline__ int hc_ldi(const int *p, int i) {
 __device__ __forceinline__ void recur_fast(int k, int lane, const double *rho_l, const double *gS_l,
                                            const double *gY_l, const double *sy, const double *syT,
                                            const double *yyl, double gamma, double &al0, double &c0) {
+  // A lane's running sum is read once, at its own step, and is dead after it (backward: steps i < l; forward:
+  // steps i > l; lanes >= k never), so every lane updates unconditionally from unconditional (clamped) loads:
+  // the live lanes get exactly the masked update, and no select or exec mask sits on the step's chain.
+  const int lc = lane < k ? lane : (k > 0 ? k - 1 : 0);
   const double rho_me = lane < k ? rho_l[lane] : 0.0;
   double r = lane < k ? gS_l[lane] : 0.0;
   for (int i0 = k - 1; i0 >= 0; i0 -= 8) { // backward: alpha_i = rho_i (gS_i - sum_{j>i} alpha_j SY[i][j])
     double col[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 - u;
-      col[u] = (i >= 0 && lane < i) ? syT[i * k + lane] : 0.0;
-    }
+    for (int u = 0; u < 8; ++u) col[u] = syT[max(i0 - u, 0) * k + lc];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 - u;
       if (i >= 0) {
         const double ai = lane_f64(rho_me * r, i);
         if (lane == i) al0 = ai;
-        r = lane < i ? r - ai * col[u] : r;
+        r = r - ai * col[u];
       }
     }
   }
@@ -108,7 +110,7 @@ __device__ __forceinline__ void recur_fast(int k, int lane, const double *rho_l,
   for (int j0 = 0; j0 < k; j0 += 8) {
     double yv[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) yv[u] = (j0 + u < k && lane < k) ? yyl[(j0 + u) * k + lane] : 0.0;
+    for (int u = 0; u < 8; ++u) yv[u] = yyl[min(j0 + u, k - 1) * k + lc];
 #pragma unroll
     for (int u = 0; u < 8; ++u)
       if (j0 + u < k) acc -= lane_f64(al0, j0 + u) * yv[u];
@@ -117,10 +119,7 @@ __device__ __forceinline__ void recur_fast(int k, int lane, const double *rho_l,
   for (int i0 = 0; i0 < k; i0 += 8) { // forward: beta_i = rho_i t_i ; t_l += (alpha_i - beta_i) SY[i][l]
     double row[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u;
-      row[u] = (i < k && lane > i && lane < k) ? sy[i * k + lane] : 0.0;
-    }
+    for (int u = 0; u < 8; ++u) row[u] = sy[min(i0 + u, k - 1) * k + lc];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u;
@@ -128,7 +127,7 @@ __device__ __forceinline__ void recur_fast(int k, int lane, const double *rho_l,
         const double cand = rho_me * tv;
         const double ci = lane_f64(al0, i) - lane_f64(cand, i);
         if (lane == i) c0 = ci;
-        tv = (lane > i && lane < k) ? tv + ci * row[u] : tv;
+        tv = tv + ci * row[u];
       }
     }
   }
@@ -218,14 +217,17 @@ template <bool LDS = false> __device__ inline void hist_prologue(const HistStep 
   const HistView &h = a.h;
   const int t = threadIdx.x, nt = blockDim.x;
   const int *ist = LDS ? a.ist : h.ist;
+  // the count and the first nt order entries in one round trip (entries past the count are loaded and unused)
+  const int count0 = a.reset ? 0 : hc_ldi<LDS>(ist, IST_COUNT);
+  const int j0 = t < h.m ? hc_ldi<LDS>(ist, IST_ORDER + t) : 0;
   if (t == 0) {
-    sm.count0 = a.reset ? 0 : hc_ldi<LDS>(ist, IST_COUNT);
+    sm.count0 = count0;
     sm.w = w;
   }
   for (int i = t; i < h.slots; i += nt) sm.inv0[i] = -1;
   lds_barrier();
-  for (int i = t; i < sm.count0; i += nt) {
-    const int j = hc_ldi<LDS>(ist, IST_ORDER + i);
+  for (int i = t; i < count0; i += nt) {
+    const int j = i == t ? j0 : hc_ldi<LDS>(ist, IST_ORDER + i);
     sm.L0[i] = j;
     sm.L[i] = j;
     sm.inv0[j] = i;
@@ -328,6 +330,9 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
     }
     if (!FUSED) h.scal[SC_COUNT] = double(count);
     sm.k = count;
+    // a pushed pair is last in the live order; a rejected one stays live only where the CUDA semantics
+    // overwrite the oldest slot in place (then at its old index)
+    sm.iw = !a.has_pair ? -1 : sm.acc ? count - 1 : (w < S_ ? sm.inv0[w] : -1);
     KTF(57);
   }
   lds_barrier();
@@ -386,29 +391,62 @@ __device__ inline void hist_core(const HistStep &a, HistSmem &sm, double *sy, in
       }
     }
   }
-  for (int e0 = t; !big && e0 < k * k; e0 += nt * 4) { // independent loads in flight
-    double a4[4], b4[4];
+  if (!big) {
+    // Every entry not on the written slot's row / column from the sources, then that row and column from the
+    // fresh dots (disjoint entries: no barrier between). k <= 64: wave v takes rows v, v + nw, ..., lane j
+    // column j; the slot numbers of the rows come from the lanes' own (v_readlane), so the entries of RU rows
+    // are loaded in one LDS round trip, with no index division and no per-entry branch.
+    const int iw = sm.iw, nw = nt >> 6;
+    if (k <= 64) {
+      constexpr int RU = 4;
+      const int qme = lane < k ? L[lane] : 0;
+      for (int i0 = wave; i0 < k; i0 += nw * RU) {
+        double sv[RU], yv[RU];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + nt * u;
-      a4[u] = b4[u] = 0.0;
-      if (e < k * k) {
+        for (int u = 0; u < RU; ++u) {
+          const int p = __builtin_amdgcn_readlane(qme, min(i0 + nw * u, k - 1));
+          sv[u] = hc_ld<LDS>(SYsrc, p * S_ + qme);
+          yv[u] = yy_lds ? hc_ld<LDS>(YYsrc, p * S_ + qme) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int i = i0 + nw * u;
+          if (i < k && lane < k && i != iw && lane != iw) {
+            sy[i * k + lane] = sv[u];
+            if (sy_t) sy[k * k + lane * k + i] = sv[u]; // transposed copy
+            if (yy_lds) yyl[i * k + lane] = yv[u];
+          }
+        }
+      }
+    } else {
+      for (int e = t; e < k * k; e += nt) {
         const int i = e / k, j = e - i * k;
-        a4[u] = SYv(L[i], L[j]);
-        b4[u] = yy_lds ? YYv(L[i], L[j]) : 0.0;
+        if (i == iw || j == iw) continue;
+        const int pq = L[i] * S_ + L[j];
+        sy[e] = hc_ld<LDS>(SYsrc, pq);
+        if (sy_t) sy[k * k + j * k + i] = sy[e];
+        if (yy_lds) yyl[e] = hc_ld<LDS>(YYsrc, pq);
       }
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + nt * u;
-      if (e < k * k) {
-        sy[e] = a4[u];
-        if (sy_t) sy[k * k + (e % k) * k + e / k] = a4[u]; // transposed copy
-        if (yy_lds) yyl[e] = b4[u];
+    // (the row / column and the per-index loop below start on waves 1 and 2: their dependent LDS chains run
+    // beside wave 0's rows instead of after them)
+    for (int j = (t + nt - 64) % nt; iw >= 0 && j < k; j += nt) { // s_w . y_q, s_q . y_w, y_w . y_q (SYv / YYv)
+      const int d = j == iw ? 0 : 6 * inv0[L[j]]; // (the written slot has no old index)
+      const double srow = j == iw ? self[1] : dots[d + 1], scol = j == iw ? self[1] : dots[d + 2];
+      const double yv = j == iw ? self[2] : dots[d + 3];
+      sy[iw * k + j] = srow;
+      sy[j * k + iw] = scol;
+      if (sy_t) {
+        sy[k * k + j * k + iw] = srow;
+        sy[k * k + iw * k + j] = scol;
+      }
+      if (yy_lds) {
+        yyl[iw * k + j] = yv;
+        yyl[j * k + iw] = yv;
       }
     }
   }
-  for (int i = t; i < k; i += nt) {
+  for (int i = (t + nt - 128 % nt) % nt; i < k; i += nt) {
     const int j = L[i];
     const bool fresh = a.has_pair && j == w;
     if (a.has_g) {

@@ -1155,6 +1155,16 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
     }
     prho = h.rho[min(t, S_ - 1)];
   }
+  // Step A's partial rows in the same round trip when they fit one staging round (the folded table, History::
+  // update): every column, the live ones picked after the prologue
+  constexpr int AU = HIST_STAGE_DOUBLES / 256;
+  const int ncols = 6 * h.m + 6, tot_all = a.nwg * ncols;
+  const bool one_round = tot_all <= a.stage && tot_all <= 256 * AU;
+  double pa[AU];
+  if (one_round) {
+#pragma unroll
+    for (int u = 0; u < AU; ++u) pa[u] = a.partials[min(t + 256 * u, tot_all - 1)];
+  }
   hist_prologue(st, sm, h.ist[IST_WSLOT]);
   if (a.fused) {
 #pragma unroll
@@ -1171,14 +1181,28 @@ __global__ __launch_bounds__(256) void hist_step_kernel(const CoefArgs a) {
   const int count0 = sm.count0;
   // ---- A: reduce the columns in use. Tiles of partial rows are staged into LDS with every load in
   // flight at once (one global round trip per tile), then thread q sums column q in row order. ----
-  const int ncols = 6 * h.m + 6;
   const int nneed = 6 * count0 + 6;
   double *stage = sy + a.sy_cap; // dynamic LDS after the SY block(s)
   const int rt = max(1, min(a.nwg, a.stage / nneed));
   double colacc[(6 * COEF_MAXK + 6 + 255) / 256];
 #pragma unroll
   for (int i = 0; i < (6 * COEF_MAXK + 6 + 255) / 256; ++i) colacc[i] = 0.0;
-  for (int r0 = 0; r0 < a.nwg; r0 += rt) {
+  if (one_round) { // the same sums in the same row order as the rounds below
+#pragma unroll
+    for (int u = 0; u < AU; ++u)
+      if (t + 256 * u < tot_all) stage[t + 256 * u] = pa[u];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < (6 * COEF_MAXK + 6 + 255) / 256; ++i) {
+      const int q = t + 256 * i;
+      if (q < nneed) {
+        const int col = q < 6 * count0 ? q : 6 * h.m + (q - 6 * count0);
+        for (int r = 0; r < a.nwg; ++r) colacc[i] += stage[r * ncols + col];
+      }
+    }
+    __syncthreads();
+  }
+  for (int r0 = 0; !one_round && r0 < a.nwg; r0 += rt) {
     const int rows = min(rt, a.nwg - r0);
     const int tot = rows * nneed;
     for (int e0 = t; e0 < tot; e0 += 256 * 8) { // 8 independent loads in flight per thread
