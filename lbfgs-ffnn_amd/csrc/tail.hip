@@ -40,7 +40,7 @@ __device__ __forceinline__ double t_wave_sum(double v) { return wave_sum_f64(v);
 // per-vector 64-lane reductions. Rows are stored transposed, [nc][nb], so tail_cols reads each
 // column contiguously. 128-column groups halve the grid (n = 101,770: 796 blocks), which keeps every
 // block resident at once (this kernel's SGPR count admits 6 blocks per CU).
-template <int VPW>
+template <int VPW, int U>
 __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
   constexpr int TC = TAIL_COLS, C = TAIL_COLS / 64;
   const RedAllArgs &ra = a.ra;
@@ -116,7 +116,8 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
 #pragma unroll
   for (int c = 0; c < C; ++c) acc[c] = 0.0;
   if (S.splits > 0) {
-    constexpr int U = 8; // loads per column in flight per round (clamped duplicates past the end)
+    // U loads per column in flight per round (clamped duplicates past the end): every slab of the launch in one
+    // round where that fits the registers (tail_reduce: U = 24 for up to 96 splits at VPW <= 8)
     for (int k = stripe; k < S.splits; k += 4 * U) {
       float x[U][C];
 #pragma unroll
@@ -412,11 +413,27 @@ static size_t fin_shmem(const TailArgs &a) {
 
 void tail_reduce(hipStream_t s, const TailArgs &a) {
   if (a.nb <= 0) return;
+  int max_splits = 0;
+  for (int i = 0; i < a.ra.nseg; ++i) max_splits = std::max(max_splits, a.ra.seg[i].splits);
+  // more than 32 slabs: three rounds of 8 per stripe would be three serial round trips; 24 per stripe issue
+  // them in one (registers: VPW <= 8 only)
+  static const bool wide_on = env_int("LBF_TAIL_WIDE", 1) != 0; // A/B switch
+  const bool wide = max_splits > 32 && wide_on;
+  const dim3 g(unsigned(a.nb)), b(256);
   switch (tail_vpw(a.h.m)) {
-  case 2: hipLaunchKernelGGL(tail_reduce_kernel<2>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
-  case 4: hipLaunchKernelGGL(tail_reduce_kernel<4>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
-  case 8: hipLaunchKernelGGL(tail_reduce_kernel<8>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
-  case 16: hipLaunchKernelGGL(tail_reduce_kernel<16>, dim3(unsigned(a.nb)), dim3(256), 0, s, a); break;
+  case 2:
+    if (wide) hipLaunchKernelGGL((tail_reduce_kernel<2, 24>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((tail_reduce_kernel<2, 8>), g, b, 0, s, a);
+    break;
+  case 4:
+    if (wide) hipLaunchKernelGGL((tail_reduce_kernel<4, 24>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((tail_reduce_kernel<4, 8>), g, b, 0, s, a);
+    break;
+  case 8:
+    if (wide) hipLaunchKernelGGL((tail_reduce_kernel<8, 24>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((tail_reduce_kernel<8, 8>), g, b, 0, s, a);
+    break;
+  case 16: hipLaunchKernelGGL((tail_reduce_kernel<16, 8>), g, b, 0, s, a); break;
   default: throw Error(2, "tail_reduce: history size not supported by the fused tail");
   }
   LBF_KERNEL_CHECK();
