@@ -7,6 +7,7 @@
 // floats, and rounded up to 2 MiB (+ 4 KiB).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <vector>
 
@@ -250,6 +251,98 @@ __global__ __launch_bounds__(512) void gram3p_k(const float *H, long long ld, in
   }
 }
 
+// gram3p_k<0> as a persistent, software-pipelined sweep: a resident grid, each workgroup taking chunks
+// blockIdx.x, blockIdx.x + gridDim.x, ...; the next chunk's four operand quads per thread are requested into
+// registers before the current chunk's history phase, so phase 1 of the next chunk finds them landed.
+__global__ __launch_bounds__(512) void gram3pp_k(const float *H, long long ld, int k, double *out, long long n,
+                                                 const float *x, const float *xp, const float *g, const float *gp,
+                                                 float *sw, float *yw, float *gout, int nch) {
+  __shared__ __attribute__((aligned(16))) float ls[4096], ly[4096], lg[4096];
+  __shared__ double red[8][6];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  f32x4 op[2][4];
+  auto fetch = [&](int ch) {
+    const long long e0 = (long long)ch * 4096;
+    const int nq = int(min(4096LL, n - e0) >> 2);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = min(int(threadIdx.x) + u * 512, nq - 1);
+      const long long e = e0 + 4LL * q;
+      op[u][0] = *reinterpret_cast<const f32x4 *>(x + e);
+      op[u][1] = *reinterpret_cast<const f32x4 *>(xp + e);
+      op[u][2] = *reinterpret_cast<const f32x4 *>(g + e);
+      op[u][3] = *reinterpret_cast<const f32x4 *>(gp + e);
+    }
+  };
+  int ch = blockIdx.x;
+  if (ch < nch) fetch(ch);
+  for (; ch < nch; ch += gridDim.x) {
+    const long long e0 = (long long)ch * 4096;
+    const int nq = int(min(4096LL, n - e0) >> 2);
+    double self[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = int(threadIdx.x) + u * 512;
+      if (q >= nq) break;
+      const f32x4 s4 = op[u][0] - op[u][1], y4 = op[u][2] - op[u][3], g4 = op[u][2];
+      *reinterpret_cast<f32x4 *>(ls + 4 * q) = s4;
+      *reinterpret_cast<f32x4 *>(ly + 4 * q) = y4;
+      *reinterpret_cast<f32x4 *>(lg + 4 * q) = g4;
+      *reinterpret_cast<f32x4 *>(sw + e0 + 4 * q) = s4;
+      *reinterpret_cast<f32x4 *>(yw + e0 + 4 * q) = y4;
+      *reinterpret_cast<f32x4 *>(gout + e0 + 4 * q) = g4;
+      for (int c = 0; c < 4; ++c) {
+        const double sv = s4[c], yv = y4[c], gv = g4[c];
+        self[0] += sv * sv; self[1] += sv * yv; self[2] += yv * yv;
+        self[3] += gv * sv; self[4] += gv * yv; self[5] += gv * gv;
+      }
+    }
+    for (int j = 0; j < 6; ++j) {
+      double t = self[j];
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+      if (lane == 0) red[wave][j] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+      double t = 0;
+      for (int w = 0; w < 8; ++w) t += red[w][threadIdx.x];
+      out[(long long)ch * 384 + 300 + threadIdx.x] = t;
+    }
+    if (ch + int(gridDim.x) < nch) fetch(ch + gridDim.x); // in flight during the history phase
+    for (int v0 = wave; v0 < k; v0 += 8) {
+      double ds = 0, dy = 0, dg = 0;
+      const float *Vp = H + (long long)v0 * ld + e0;
+      for (int i0 = lane * 4; i0 < 4096; i0 += 1024) {
+        f32x4 xv4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const long long ee = e0 + i0 + 256 * u;
+          xv4[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(Vp + (ee + 3 < n ? i0 + 256 * u : 0)));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const f32x4 s4 = *reinterpret_cast<const f32x4 *>(ls + i0 + 256 * u);
+          const f32x4 y4 = *reinterpret_cast<const f32x4 *>(ly + i0 + 256 * u);
+          const f32x4 g4 = *reinterpret_cast<const f32x4 *>(lg + i0 + 256 * u);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const double xv = xv4[u][j];
+            ds += xv * double(s4[j]);
+            dy += xv * double(y4[j]);
+            dg += xv * double(g4[j]);
+          }
+        }
+      }
+      double d3[3] = {ds, dy, dg};
+      for (int c = 0; c < 3; ++c)
+        for (int o = 32; o > 0; o >>= 1) d3[c] += __shfl_xor(d3[c], o);
+      if (lane == 0)
+        for (int c = 0; c < 3; ++c) out[(long long)ch * 384 + 3 * v0 + c] = d3[c];
+    }
+    __syncthreads(); // the LDS vectors are rewritten by the next chunk
+  }
+}
+
 int main() {
   const long long n = 10489857, n4 = (n + 3) & ~3LL;
   const int k = 100;
@@ -323,6 +416,42 @@ int main() {
       printf("%-10s ld = n4 %+6lld floats (%s)  best %7.1f us %6.0f GB/s  avg %7.1f us %6.0f GB/s\n",
              names[kind], ld - n4, pad == -1 ? "2 MiB" : (pad == -2 ? "2 MiB + 4 KiB" : "plain"),
              best * 1e3, bytes / best / 1e6, sum / 5 * 1e3, bytes / (sum / 5) / 1e6);
+    }
+  }
+  // the fused sweep against its persistent, pipelined form, at m = 10 and m = 50 (k = 20, 100 history vectors)
+  {
+    int pp = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pp, gram3pp_k, 512, 0));
+    for (int kk : {20, 100}) {
+      const long long ld = n4;
+      for (int kind = 0; kind < 4; ++kind) { // gram3p, gram3pp at 1x / 2x the resident grid, gram3p_split
+        float best = 1e30f, sum = 0.0f;
+        const double bytes = double(kk + (kind == 3 ? 3 : 7)) * n * 4;
+        for (int it = 0; it < 6; ++it) {
+          CK(hipMemset(flush, it, size_t(512) << 20));
+          CK(hipEventRecord(a));
+          if (kind == 0)
+            hipLaunchKernelGGL(gram3p_k<0>, dim3(nch), dim3(512), 0, 0, H, ld, kk, gout, n, V5, V5 + n4, V5 + 2 * n4,
+                               V5 + 3 * n4, V5 + 4 * n4, V5 + 5 * n4, V5 + 6 * n4);
+          else if (kind == 3)
+            hipLaunchKernelGGL(gram3p_k<3>, dim3(nch), dim3(512), 0, 0, H, ld, kk, gout, n, V5, V5 + n4, V5 + 2 * n4,
+                               V5 + 3 * n4, V5 + 4 * n4, V5 + 5 * n4, V5 + 6 * n4);
+          else
+            hipLaunchKernelGGL(gram3pp_k, dim3(std::min(nch, cus * pp * kind)), dim3(512), 0, 0, H, ld, kk, gout, n, V5,
+                               V5 + n4, V5 + 2 * n4, V5 + 3 * n4, V5 + 4 * n4, V5 + 5 * n4, V5 + 6 * n4, nch);
+          CK(hipEventRecord(b));
+          CK(hipEventSynchronize(b));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, a, b));
+          if (it > 0) {
+            best = ms < best ? ms : best;
+            sum += ms;
+          }
+        }
+        const char *nm[] = {"gram3p", "gram3pp_x1", "gram3pp_x2", "gram3p_split"};
+        printf("k = %3d %-12s (%d per CU) best %7.1f us %6.0f GB/s  avg %7.1f us %6.0f GB/s\n", kk, nm[kind], pp,
+               best * 1e3, bytes / best / 1e6, sum / 5 * 1e3, bytes / (sum / 5) / 1e6);
+      }
     }
   }
   CK(hipFree(H));
