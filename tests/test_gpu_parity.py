@@ -282,6 +282,32 @@ def test_lbfgs_armijo_trajectory(ctx, pkg, O):
     assert np.array_equal(hist["ls_trials"][:8], rec[:8, 4].astype(int))
 
 
+@pytest.mark.parametrize("case", [([4, 8, 2], ["tanh", "tanh"], 23), ([5, 5, 5, 2], ["tanh", "tanh", "tanh"], 15)],
+                         ids=["4-8-2", "5-5-5-2"])
+def test_lbfgs_armijo_rejected_pair_full_ring(ctx, pkg, O, case):
+    """CUDA semantics with a full ring and a rejected pair (lbfgs.cuh:149-169: the oldest slot is overwritten
+    in place, its rho left stale, and stays live): the history step's live Gram block then takes that slot's
+    row and column from the fresh dots at its old index. Smooth tanh nets on 16 rows whose fp32 oracle rejects
+    a pair at iteration 3-4 with m = 3 (found by a search over seeds); the device follows it through the
+    rejection: same accept / reject record, same line-search trials, losses within 1e-3."""
+    dims, acts, seed = case
+    rng = np.random.default_rng(seed)
+    Xh = rng.standard_normal((16, dims[0])).astype(np.float32)
+    Yh = rng.standard_normal((16, dims[-1])).astype(np.float32)
+    net = pkg.Mlp(ctx, dims, acts)
+    P = net.init_params(seed + 1, "cuda")
+    P0 = host(P)
+    hist, _ = pkg.lbfgs_solve(net, P, dev(Xh), dev(Yh), line_search="armijo", m=3, max_iters=12, tol=0.0)
+    _, rec = O.Net(dims, acts).lbfgs_armijo(P0, Xh.astype(np.float64), Yh.astype(np.float64), m=3, max_iters=12,
+                                            fp32=True)
+    acc_ref = rec[:, 3].astype(int)
+    assert (acc_ref[3:8] == 0).any(), "the case must reject a pair with the ring full"
+    assert np.array_equal(hist["accepted"][:10], acc_ref[:10]), (hist["accepted"][:10], acc_ref[:10])
+    assert np.array_equal(hist["ls_trials"][:10], rec[:10, 4].astype(int))
+    r = np.abs(hist["loss"][:10] - rec[:10, 0]) / np.abs(rec[:10, 0])
+    assert r.max() <= 1e-3, r
+
+
 def test_slbfgs_matches_oracle(ctx, pkg, O):
     """S-LBFGS (s_lbfgs.hpp:165-290): same host RNG stream, same sampled batches, same curvature pairs."""
     dims, acts = [784, 16, 10], ["relu", "linear"]
