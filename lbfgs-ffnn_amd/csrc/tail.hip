@@ -415,8 +415,8 @@ void tail_reduce(hipStream_t s, const TailArgs &a) {
   if (a.nb <= 0) return;
   int max_splits = 0;
   for (int i = 0; i < a.ra.nseg; ++i) max_splits = std::max(max_splits, a.ra.seg[i].splits);
-  // more than 32 slabs: three rounds of 8 per stripe would be three serial round trips; 24 per stripe issue
-  // them in one (registers: VPW <= 8 only)
+  // more than 32 slabs (cfg 2: 82): 24 per stripe in one round instead of rounds of 8 (registers: VPW <= 8 only;
+  // 13.6 -> 12.8 us at cfg 2, profiles/r06/s/)
   static const bool wide_on = env_int("LBF_TAIL_WIDE", 1) != 0; // A/B switch
   const bool wide = max_splits > 32 && wide_on;
   const dim3 g(unsigned(a.nb)), b(256);
