@@ -317,6 +317,7 @@ struct LsCtlArgs {
   float foldf = 0.0f;
   double c1 = 0.0, c2 = 0.0, tol = 0.0;
   float alphaf = 1.0f;       // Armijo trial step
+  double alpha = 1.0;        // Wolfe trial step (1: a speculative first trial; else a host-finished search's)
 };
 void ls_ctl(hipStream_t s, const LsCtlArgs &a);
 

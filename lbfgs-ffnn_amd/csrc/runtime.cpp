@@ -532,13 +532,13 @@ void Mlp::loss_grad_local(const float *P, float *G, const float *X, const float 
 }
 
 void Mlp::grad_after_loss(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
-                          double lambda, const float *pdir, double *scal) {
+                          double lambda, const float *pdir, double *scal, const TailFuse *tf) {
   LBF_REQUIRE(B == 0 || fs_.B == B, "grad_after_loss: no forward phase of this batch");
   ++gal_;
   // the reduced route reports the loss of the loss-only trial's own all-reduced words, so the Armijo
   // decision and the recorded loss are one value whatever order the collective sums the two buffers in
   const bool reduced = ctx_->dp() || B == 0;
-  backward_phase(P, G, X, idx, B, inv_scale, lambda, pdir, scal, nullptr, false, reduced ? hilo_.get() : nullptr);
+  backward_phase(P, G, X, idx, B, inv_scale, lambda, pdir, scal, tf, false, reduced ? hilo_.get() : nullptr);
 }
 
 // Backward phase: the dW / dX GEMMs below the head, every layer's slab reduction, the gradient

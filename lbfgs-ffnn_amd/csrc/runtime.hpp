@@ -143,7 +143,7 @@ public:
   void loss_only(const float *P, const float *X, const float *Y, const int *idx, long long B, double inv_scale,
                  double *scal);
   void grad_after_loss(const float *P, float *G, const float *X, const int *idx, long long B, double inv_scale,
-                       double lambda, const float *pdir, double *scal);
+                       double lambda, const float *pdir, double *scal, const TailFuse *tf = nullptr);
   // Packed data-parallel evaluation in two halves: loss_grad_local stops before the all-reduce, leaving
   // this rank's gradient (no lambda w) and its SSE as fp32 (hi, lo) words in G[0 .. n+2); the caller
   // all-reduces one or more such blocks in a single collective and then finishes each with

@@ -212,10 +212,48 @@ float LbfgsSolver::begin_iteration(const LsCtlArgs *ls) {
 // fused evaluation: line_search's f(x), Gradient(x) are the previous accepted trial, the trial's
 // Gradient(x+ap) comes with its f, the post-search Gradient(x_new) and the recorder's f(x) are the
 // accepted trial's. Only an exhausted search (returns an alpha it never evaluated) costs one more.
-void LbfgsSolver::finish_wolfe(lbf_record *rec) {
+// finish_wolfe's gradient phase on the speculative route: the backward of the loss-only trial just taken,
+// then the fused tail with the host's decision rule at this alpha (tail.hip): on acceptance it pushes the pair
+// and computes the next direction's coefficients, as a speculative iteration's tail does, so the next
+// iteration speculates at once on the fused route. Returns the record's status; anything but SPEC_ACCEPT has
+// raised the abort flag, which is cleared here (stream-ordered), and leaves the history untouched.
+int LbfgsSolver::grad_fused(double alpha, SpecRecord *r) {
+  LsCtlArgs a;
+  a.scal = hist_.scal();
+  a.abort = abort_.get();
+  a.seq = seq_++;
+  a.rec = spec_rec_ + a.seq % kSpecRing;
+  a.armijo = 0;
+  a.first = 0;
+  a.host_fold = 1;
+  a.fold = loss_;
+  a.foldf = lossf_;
+  a.c1 = prm_.c1;
+  a.c2 = prm_.c2;
+  a.tol = prm_.tol;
+  a.alpha = alpha;
+  TailFuse tf;
+  tf.h = hist_.view();
+  tf.has_pair = prm_.m > 0;
+  tf.x_prev = x_;
+  tf.g_prev = g_;
+  tf.policy = POL_CPU;
+  tf.iter_next = iter_ + 1;
+  tf.ls = a;
+  tf.ls.alphaf = float(alpha);
+  obj_->eval_grad_after_loss_fused(xt_, gt_, p_.get(), hist_.scal(), tf);
+  wait_record(a.seq, r);
+  if (r->seq != a.seq) throw Error(2, "speculative line search: record out of sequence");
+  if (r->status != SPEC_ACCEPT) LBF_HIP(hipMemsetAsync(abort_.get(), 0, sizeof(int), ctx_->stream));
+  return r->status;
+}
+
+void LbfgsSolver::finish_wolfe(lbf_record *rec, bool spec) {
   const double inf = std::numeric_limits<double>::infinity();
   double alpha = hs_[SC_ALPHA0];
   int trials = 0;
+  bool fused_done = false; // the accepted trial's tail pushed the pair and built the next direction
+  SpecRecord fr{};
   if (iter_ > 0) {
     const double f_old = loss_, gfo = hs_[SC_GTP];
     double amin = 0.0, amax = inf;
@@ -246,9 +284,17 @@ void LbfgsSolver::finish_wolfe(lbf_record *rec) {
         continue;
       }
       if (!have_grad) { // backward phase of the forward pass just taken: bitwise the full evaluation
-        obj_->eval_grad_after_loss(xt_, gt_, p_.get(), hist_.scal());
-        read_status();
         have_grad = true;
+        if (spec && fuse_) {
+          if (grad_fused(alpha, &fr) == SPEC_ACCEPT) { // the host's tests below would pass alike
+            fused_done = true;
+            break;
+          }
+          read_status(); // rejected on curvature (or converged): the host's search goes on from the status
+        } else {
+          obj_->eval_grad_after_loss(xt_, gt_, p_.get(), hist_.scal());
+          read_status();
+        }
       }
       const double gnp = hs_[SC_TGP];
       if (gnp < prm_.c2 * gfo) {
@@ -269,8 +315,9 @@ void LbfgsSolver::finish_wolfe(lbf_record *rec) {
     }
   }
   accept_roles();
-  loss_ = hs_[SC_LOSS];
-  gg_ = hs_[SC_TGG];
+  loss_ = fused_done ? fr.loss : hs_[SC_LOSS];
+  gg_ = fused_done ? fr.tgg : hs_[SC_TGG];
+  dir_ready_ = fused_done;
   record(rec, loss_, std::sqrt(gg_), alpha, trials, -1);
 }
 
@@ -478,7 +525,7 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
       if (armijo)
         finish_armijo(f.alpha, rec);
       else
-        finish_wolfe(rec);
+        finish_wolfe(rec, true);
       ++done;
       issued = done;
       host_fold = true;

@@ -41,6 +41,8 @@ struct Objective {
   // Evaluation followed by the fused optimizer tail (tail.hip); only when fused_tail() is true.
   virtual bool fused_tail() const { return false; }
   virtual void eval_fused(const float *, float *, const float *, double *, const TailFuse &) {}
+  // eval_grad_after_loss followed by the fused tail (fused_tail() objectives)
+  virtual void eval_grad_after_loss_fused(const float *, float *, const float *, double *, const TailFuse &) {}
 };
 
 // The MLP's fused loss+grad over the rank's shard (mean over n_global samples).
@@ -71,6 +73,10 @@ struct MlpObjective : Objective {
   bool fused_tail() const override { return true; }
   void eval_fused(const float *x, float *g, const float *pdir, double *scal, const TailFuse &tf) override {
     net->loss_grad(x, g, X, Y, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal, &tf);
+  }
+  void eval_grad_after_loss_fused(const float *x, float *g, const float *pdir, double *scal,
+                                  const TailFuse &tf) override {
+    net->grad_after_loss(x, g, X, nullptr, nloc, 1.0 / double(nglob), 0.0, pdir, scal, &tf);
   }
 };
 
@@ -120,7 +126,8 @@ private:
   float begin_iteration(const LsCtlArgs *ls = nullptr);
   // Rest of the iteration once hs_ holds the first trial's status: further trials, role rotation,
   // record.
-  void finish_wolfe(lbf_record *rec);
+  void finish_wolfe(lbf_record *rec, bool spec = false);
+  int grad_fused(double alpha, SpecRecord *r); // finish_wolfe's gradient phase through the fused tail
   void finish_armijo(float alpha, lbf_record *rec);
   void accept_roles();
   void mark_prev_accepted(lbf_record *rec, double flag);

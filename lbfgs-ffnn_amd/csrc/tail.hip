@@ -314,7 +314,7 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
     bool ok, conv;
     if (!L.armijo) {
       const double fo = L.host_fold ? L.fold : fold;
-      ok = L.first || (!(fn > __dadd_rn(fo, __dmul_rn(__dmul_rn(L.c1, 1.0), gfo))) && !(tgp < __dmul_rn(L.c2, gfo)));
+      ok = L.first || (!(fn > __dadd_rn(fo, __dmul_rn(__dmul_rn(L.c1, L.alpha), gfo))) && !(tgp < __dmul_rn(L.c2, gfo)));
       conv = sqrt(tgg) < L.tol;
       s_sc[5] = fn;
     } else {

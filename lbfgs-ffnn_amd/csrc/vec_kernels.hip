@@ -1635,7 +1635,7 @@ __global__ __launch_bounds__(64) void ls_ctl_kernel(const LsCtlArgs a) {
   bool ok, conv;
   if (!a.armijo) {
     const double fold = a.host_fold ? a.fold : sc[SC_FOLD];
-    ok = a.first || (!(fn > __dadd_rn(fold, __dmul_rn(__dmul_rn(a.c1, 1.0), gfo))) && !(gnp < __dmul_rn(a.c2, gfo)));
+    ok = a.first || (!(fn > __dadd_rn(fold, __dmul_rn(__dmul_rn(a.c1, a.alpha), gfo))) && !(gnp < __dmul_rn(a.c2, gfo)));
     conv = sqrt(tgg) < a.tol;
     if (ok) sc[SC_FOLD] = fn;
   } else {
