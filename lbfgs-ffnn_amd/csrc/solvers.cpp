@@ -212,18 +212,20 @@ float LbfgsSolver::begin_iteration(const LsCtlArgs *ls) {
 // fused evaluation: line_search's f(x), Gradient(x) are the previous accepted trial, the trial's
 // Gradient(x+ap) comes with its f, the post-search Gradient(x_new) and the recorder's f(x) are the
 // accepted trial's. Only an exhausted search (returns an alpha it never evaluated) costs one more.
-// finish_wolfe's gradient phase on the speculative route: the backward of the loss-only trial just taken,
-// then the fused tail with the host's decision rule at this alpha (tail.hip): on acceptance it pushes the pair
+// The host-finished search's gradient phase on the speculative route (finish_wolfe / finish_armijo): the backward
+// of the loss-only trial just taken, then the fused tail with the host's decision rule at this alpha
+// (tail.hip): on acceptance it pushes the pair
 // and computes the next direction's coefficients, as a speculative iteration's tail does, so the next
 // iteration speculates at once on the fused route. Returns the record's status; anything but SPEC_ACCEPT has
 // raised the abort flag, which is cleared here (stream-ordered), and leaves the history untouched.
 int LbfgsSolver::grad_fused(double alpha, SpecRecord *r) {
+  const bool armijo = prm_.line_search == LBF_LS_ARMIJO;
   LsCtlArgs a;
   a.scal = hist_.scal();
   a.abort = abort_.get();
   a.seq = seq_++;
   a.rec = spec_rec_ + a.seq % kSpecRing;
-  a.armijo = 0;
+  a.armijo = armijo ? 1 : 0;
   a.first = 0;
   a.host_fold = 1;
   a.fold = loss_;
@@ -237,10 +239,10 @@ int LbfgsSolver::grad_fused(double alpha, SpecRecord *r) {
   tf.has_pair = prm_.m > 0;
   tf.x_prev = x_;
   tf.g_prev = g_;
-  tf.policy = POL_CPU;
+  tf.policy = armijo ? POL_CUDA : POL_CPU;
   tf.iter_next = iter_ + 1;
   tf.ls = a;
-  tf.ls.alphaf = float(alpha);
+  tf.ls.alphaf = float(alpha); // Armijo: the fp32 trial step itself
   obj_->eval_grad_after_loss_fused(xt_, gt_, p_.get(), hist_.scal(), tf);
   wait_record(a.seq, r);
   if (r->seq != a.seq) throw Error(2, "speculative line search: record out of sequence");
@@ -338,7 +340,7 @@ int LbfgsSolver::iterate_wolfe(int iters, lbf_record *rec) {
 }
 
 // CUDA semantics: CudaLBFGS::solve (lbfgs.cuh:39-194), host scalars in fp32 like the reference.
-void LbfgsSolver::finish_armijo(float alpha, lbf_record *rec) {
+void LbfgsSolver::finish_armijo(float alpha, lbf_record *rec, bool spec) {
   const float c1 = float(prm_.c1), rho = float(prm_.rho);
   const float gdp = float(hs_[SC_GTP]);
   bool ok = false;
@@ -375,15 +377,22 @@ void LbfgsSolver::finish_armijo(float alpha, lbf_record *rec) {
     }
     if (fb) alpha *= rho;
   }
+  bool fused_done = false; // the accepted trial's tail pushed the pair and built the next direction
+  SpecRecord fr{};
   if (!have_grad) {
-    obj_->eval_grad_after_loss(xt_, gt_, p_.get(), hist_.scal());
-    read_status();
+    if (spec && fuse_ && ok && grad_fused(double(a_eval), &fr) == SPEC_ACCEPT) {
+      fused_done = true;
+    } else {
+      if (!(spec && fuse_ && ok)) obj_->eval_grad_after_loss(xt_, gt_, p_.get(), hist_.scal());
+      read_status(); // (after a fused tail that did not accept: its status block)
+    }
   }
   accept_roles();
   pending_reset_ = !ok; // lbfgs.cuh:147
   lossf_ = lnew;
-  loss_ = hs_[SC_LOSS];
-  gg_ = hs_[SC_TGG];
+  loss_ = fused_done ? fr.loss : hs_[SC_LOSS];
+  gg_ = fused_done ? fr.tgg : hs_[SC_TGG];
+  dir_ready_ = fused_done;
   record(rec, double(lnew), double(float(std::sqrt(gg_))), double(a_eval), trials, -1);
 }
 
@@ -523,7 +532,7 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
       dir_ready_ = false;         // the host finishes this iteration; the next one builds its direction
       restore(f.roles);
       if (armijo)
-        finish_armijo(f.alpha, rec);
+        finish_armijo(f.alpha, rec, true);
       else
         finish_wolfe(rec, true);
       ++done;

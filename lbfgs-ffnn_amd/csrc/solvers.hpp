@@ -128,7 +128,7 @@ private:
   // record.
   void finish_wolfe(lbf_record *rec, bool spec = false);
   int grad_fused(double alpha, SpecRecord *r); // finish_wolfe's gradient phase through the fused tail
-  void finish_armijo(float alpha, lbf_record *rec);
+  void finish_armijo(float alpha, lbf_record *rec, bool spec = false);
   void accept_roles();
   void mark_prev_accepted(lbf_record *rec, double flag);
   void record(lbf_record *rec, double loss, double gnorm, double alpha, int trials, int accepted);
