@@ -59,15 +59,8 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
 #ifdef LBF_KTRACE
   if (t == 0 && blockIdx.x >= 1024 && blockIdx.x < 2048) lbf_kt_blk[5 * 1024 + blockIdx.x - 1024] = wall_clock64();
 #endif
-  // the ring header in one round trip (count, free slot, order)
-  if (t < IST_ORDER + h.m) ist[t] = h.ist[t];
-  lds_barrier();
-  if (aborted(abf)) return; // uniform for the launch: no store, no arrival
-  KTB(1);
-  // wave-uniform scalars (SGPRs): the loads below then need no per-lane select or branch
-  const int count0 = __builtin_amdgcn_readfirstlane(ist[IST_COUNT]);
-  const int w = __builtin_amdgcn_readfirstlane(hist_write_slot(ist, h.m, a.policy, 0));
-  const int nvec = 2 * count0;
+  // This block's column group and segment: kernel arguments only, so the loads that need no ring order (the
+  // operands and the first round of split-K slabs) go out right behind the ring header's, in the same round trip.
   const int cg = blockIdx.x;
   int si = 0;
   while (si + 1 < ra.nseg && a.tcg0[si + 1] <= cg) ++si;
@@ -84,7 +77,45 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
     colc[c] = live[c] ? col[c] : S.count - 1;
     e[c] = S.goff + colc[c];
   }
-  // ---- history values of this wave's vectors (in flight while the slabs load) ----
+  // the ring header (count, free slot, order): issued first, so waiting for it waits for nothing issued after
+  const int istv = t < IST_ORDER + h.m ? h.ist[t] : 0;
+  // ---- operands ----
+  // every wave loads them (same lines as wave 0's: L1 hits) so no branch merge forces an early wait;
+  // null operands read w instead and are masked where used
+  float wv[C], xp[C], gp[C], pv[C], gw[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    wv[c] = ra.w[e[c]];
+    xp[c] = (a.x_prev ? a.x_prev : ra.w)[e[c]];
+    gp[c] = (a.g_prev ? a.g_prev : ra.w)[e[c]];
+    pv[c] = (ra.p ? ra.p : ra.w)[e[c]];
+    gw[c] = (a.g_src ? a.g_src : ra.G)[e[c]];
+  }
+  // ---- gradient columns: split-K slabs in split order (4 stripes); U loads per column in flight per round
+  // (clamped duplicates past the end): every slab of the launch in one round where that fits the registers
+  // (tail_reduce: U = 24 for up to 96 splits at VPW <= 8). The first round of 8 is requested here; a round of 24
+  // held across the header's wait would take the kernel past 128 VGPRs (3 blocks per CU), so it goes out below. ----
+  constexpr bool EARLY = U <= 8;
+  float x0[EARLY ? U : 1][C];
+  if constexpr (EARLY) {
+    if (S.splits > 0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long sp = min(stripe + 4 * u, S.splits - 1);
+#pragma unroll
+        for (int c = 0; c < C; ++c) x0[u][c] = S.slab[colc[c] + sp * S.stride];
+      }
+    }
+  }
+  if (t < IST_ORDER + h.m) ist[t] = istv;
+  lds_barrier();
+  if (aborted(abf)) return; // uniform for the launch: no store, no arrival
+  KTB(1);
+  // wave-uniform scalars (SGPRs): the loads below then need no per-lane select or branch
+  const int count0 = __builtin_amdgcn_readfirstlane(ist[IST_COUNT]);
+  const int w = __builtin_amdgcn_readfirstlane(hist_write_slot(ist, h.m, a.policy, 0));
+  const int nvec = 2 * count0;
+  // ---- history values of this wave's vectors ----
   const float *Sb = h.S, *Yb = h.Y;
   float vv[VPW][C];
   unsigned zero_mask = 0; // bit j: vector j of this wave is the slot being overwritten (not live)
@@ -98,27 +129,21 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const TailArgs a) {
     for (int c = 0; c < C; ++c) vv[j][c] = base[e[c]];
     if (v >= nvec || (a.has_pair && slot == w)) zero_mask |= 1u << j;
   }
-  // ---- operands ----
-  // every wave loads them (same lines as wave 0's: L1 hits) so no branch merge forces an early wait;
-  // null operands read w instead and are masked where used
-  float wv[C], xp[C], gp[C], pv[C], gw[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    wv[c] = ra.w[e[c]];
-    xp[c] = (a.x_prev ? a.x_prev : ra.w)[e[c]];
-    gp[c] = (a.g_prev ? a.g_prev : ra.w)[e[c]];
-    pv[c] = (ra.p ? ra.p : ra.w)[e[c]];
-    gw[c] = (a.g_src ? a.g_src : ra.G)[e[c]];
-  }
   KT(49);
-  // ---- gradient columns: split-K slabs in split order (4 stripes) ----
   double acc[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) acc[c] = 0.0;
   if (S.splits > 0) {
-    // U loads per column in flight per round (clamped duplicates past the end): every slab of the launch in one
-    // round where that fits the registers (tail_reduce: U = 24 for up to 96 splits at VPW <= 8)
-    for (int k = stripe; k < S.splits; k += 4 * U) {
+    int k0 = stripe;
+    if constexpr (EARLY) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+          if (stripe + 4 * u < S.splits) acc[c] += double(x0[u][c]);
+      k0 += 4 * U;
+    }
+    for (int k = k0; k < S.splits; k += 4 * U) { // (EARLY: the rounds after the first)
       float x[U][C];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
