@@ -17,6 +17,7 @@
 #include "head_core.hpp"
 #include "internal.hpp"
 #include "kernels.hpp"
+#include "ls_rule.hpp"
 
 #include <hip/hip_runtime.h>
 
@@ -66,7 +67,61 @@ struct GemmK {
   int gx, gy;   // this problem's tile grid (the grouped launch's grid is the larger of two)
   int group_z;  // grouped launch: GEMM planes of the first problem (the second's follow)
   int xcd_swz;  // split-K: deal each split's tiles to one XCD (xcd_tile below)
+  EarlyLs early; // sse_part non-null: the speculative trial's Armijo test first (gemm_early_exit)
 };
+
+// EarlyLs (kernels.hpp): a speculative trial's sufficient-decrease test ahead of its backward. Threads 0..255
+// sum the forward's SSE partials in tail_fin_body's order (thread t: r = t, t + 256, ..; wave sums;
+// ((v0 + v1) + v2) + v3) and thread 0 applies ls_rule.hpp's test, so every block and the tail decide alike. The
+// abort flag is read by thread 0 in the same round trip and the block's verdict goes through LDS: block 0 of
+// this launch raises the flag while other blocks may be reading it, and one reader per block keeps the exit
+// uniform. Block 0 publishes a failure as tail_fin_body publishes a rejection (status block words, abort flag,
+// then the host record, its sequence word last). Runs before the kernel's first use of lds.
+__device__ __forceinline__ bool gemm_early_exit(const GemmK &g, float *lds) {
+  const EarlyLs &e = g.early;
+  const int t = threadIdx.x;
+  double *red = reinterpret_cast<double *>(lds);
+  double sse = 0.0;
+  if (t < 256)
+    for (int r = t; r < e.nsse; r += 256) sse += e.sse_part[r];
+  double gfo = 0.0, fold = 0.0, alpha0 = 0.0, accept_prev = 0.0;
+  int abf = 0;
+  if (t == 0) {
+    const double *sc = e.ls.scal;
+    gfo = sc[SC_GTP];
+    fold = e.ls.armijo ? sc[SC_FOLDF] : sc[SC_FOLD];
+    alpha0 = sc[SC_ALPHA0];
+    accept_prev = sc[SC_ACCEPT];
+    abf = abort_flag(g.abort);
+  }
+  sse = wave_sum_f64(sse);
+  if (t < 256 && (t & 63) == 0) red[t >> 6] = sse;
+  __syncthreads();
+  if (t == 0) {
+    const double sse_t = ((red[0] + red[1]) + red[2]) + red[3];
+    const double fn = 0.5 * sse_t * e.inv_scale; // tail_fin_body's loss (lambda = 0)
+    const bool fail = !ls_sufficient_decrease(e.ls, fn, fold, gfo);
+    if (fail && !abf && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+      double *sc = e.ls.scal;
+      sc[SC_SSE] = sse_t;
+      sc[SC_LOSS] = fn;
+      *e.ls.abort = 1;
+      SpecRecord *r = e.ls.rec;
+      __hip_atomic_store(&r->loss, fn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&r->tgg, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&r->alpha0, alpha0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&r->accept_prev, accept_prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&r->status, int(SPEC_REJECT_EARLY), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&r->seq, e.ls.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    red[4] = (abf || fail) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  const bool out = red[4] != 0.0;
+  __syncthreads(); // every wave has its verdict before any wave's first use of lds
+  return out;
+}
 
 // XCD-aware placement of a split-K GEMM's blocks (cdna_hip_programming.md §5.5 T1, bijective form): blocks
 // b and b + 8 are dealt to the same XCD (its own L2), so the GEMM blocks whose index e (past the side
@@ -416,7 +471,7 @@ __global__ __launch_bounds__(256 * KW, 2) void gemm_kernel(const GemmK g) {
   constexpr int HEAD_F = headc::smem_floats_epi(BN, BM > headc::TB ? BM : headc::TB);
   constexpr int LDS_F = (EPI == EPI_HEAD && HEAD_F > 2 * (ASZ + BSZ)) ? HEAD_F : 2 * (ASZ + BSZ);
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
-  if (g.abort && *g.abort) return;
+  if (g.early.sse_part ? gemm_early_exit(g, lds) : (g.abort && *g.abort)) return;
   if (int(blockIdx.z) < g.side_planes) {
     gemm_side_job(g, reinterpret_cast<double *>(lds));
     return;
@@ -888,7 +943,7 @@ __device__ __forceinline__ void glds_body(const GemmK &g, float *lds, int zsplit
 template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, bool GATHER, int NS, int KW = 1, bool ASUM = false>
 __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(const GemmK g) {
   __shared__ __attribute__((aligned(16))) float lds[GldsShape<WM, WN, TM, TN, EPI, NS>::LDS_F];
-  if (g.abort && *g.abort) return;
+  if (g.early.sse_part ? gemm_early_exit(g, lds) : (g.abort && *g.abort)) return;
   if (int(blockIdx.z) < g.side_planes) {
     gemm_side_job(g, reinterpret_cast<double *>(lds));
     return;
@@ -908,7 +963,7 @@ __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_kernel(co
 template <int WM, int WN, int TM, int TN, bool AKC, bool BKC, int EPI, int NS, int KW = 1>
 __global__ __launch_bounds__(256 * KW, KW == 1 ? 2 : 1) void gemm_glds_group_kernel(const GemmK g, const GemmK g2) {
   __shared__ __attribute__((aligned(16))) float lds[GldsShape<WM, WN, TM, TN, EPI, NS>::LDS_F];
-  if (g.abort && *g.abort) return;
+  if (g.early.sse_part ? gemm_early_exit(g, lds) : (g.abort && *g.abort)) return;
   if (int(blockIdx.z) < g.side_planes) {
     gemm_side_job(g, reinterpret_cast<double *>(lds));
     return;
@@ -954,7 +1009,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsk_kernel(const GemmK g) {
   constexpr int LDS_F = HEAD_F > WSK_RED_F ? HEAD_F : WSK_RED_F;
   constexpr int NA = ASUM ? WSK_MAX_ASPLITS : 1; // A quads per k-tile
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
-  if (g.abort && *g.abort) return;
+  if (g.early.sse_part ? gemm_early_exit(g, lds) : (g.abort && *g.abort)) return;
   if (int(blockIdx.z) < g.side_planes) {
     gemm_side_job(g, reinterpret_cast<double *>(lds));
     return;
@@ -1100,6 +1155,7 @@ template <int BM, int BN> GemmK make_gemmk(const GemmDesc &d) {
   k.ldaux = d.ldaux;
   k.aux_act = d.aux_act;
   k.abort = d.abort;
+  if (d.early) k.early = *d.early;
   const long long gx = (d.N + BN - 1) / BN, gy = (d.M + BM - 1) / BM;
   k.gx = int(gx);
   k.gy = int(gy);

@@ -27,6 +27,8 @@ enum Act : int { ACT_LINEAR = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_SIGMOID = 3 };
 enum GemmTile : int { TILE_AUTO = 0, TILE_32x128 = 1, TILE_64x64 = 2, TILE_64x128 = 3 };
 enum GemmEpi : int { EPI_FWD = 0, EPI_DX = 1, EPI_STORE = 2, EPI_HEAD = 3 };
 
+struct EarlyLs;
+
 struct GemmDesc {
   int M = 0, N = 0, K = 0;
   const float *A = nullptr;
@@ -48,6 +50,7 @@ struct GemmDesc {
   long long ldaux = 0;
   int aux_act = ACT_LINEAR;
   const int *abort = nullptr; // speculative execution: the kernel is a no-op when *abort != 0
+  const EarlyLs *early = nullptr; // the trial's first backward launch: its Armijo test first (EarlyLs)
   // A from the previous layer's forward split-K slabs (a_slab non-null; only where gemm_asum_ok): each
   // workgroup forms its A tiles as act(sum_s a_slab[s * a_slab_stride + .] + a_bias) (fwd_reduce_act's
   // arithmetic, splits in order) in its prologue, and the workgroups of column tile 0 also write them to
@@ -301,10 +304,12 @@ struct SpecRecord {
   double tgg;         // trial g.g  (SC_TGG)
   double alpha0;      // SC_ALPHA0 (first trial step computed on the device)
   double accept_prev; // SC_ACCEPT (whether the previous pair entered the ring)
-  int status;         // SPEC_ACCEPT / SPEC_CONVERGED / SPEC_REJECT
+  int status;         // SPEC_ACCEPT / SPEC_CONVERGED / SPEC_REJECT / SPEC_REJECT_EARLY
   int seq;            // written last
 };
-enum { SPEC_ACCEPT = 1, SPEC_CONVERGED = 2, SPEC_REJECT = 3 };
+// SPEC_REJECT_EARLY: rejected on sufficient decrease by the trial's first backward GEMM (EarlyLs), so the
+// trial's backward and tail never ran (tgg is 0; SC_LOSS / SC_SSE of the status block are written)
+enum { SPEC_ACCEPT = 1, SPEC_CONVERGED = 2, SPEC_REJECT = 3, SPEC_REJECT_EARLY = 4 };
 struct LsCtlArgs {
   double *scal = nullptr;
   int *abort = nullptr;
@@ -320,6 +325,19 @@ struct LsCtlArgs {
   double alpha = 1.0;        // Wolfe trial step (1: a speculative first trial; else a host-finished search's)
 };
 void ls_ctl(hipStream_t s, const LsCtlArgs &a);
+
+// Early Armijo test of a speculative first trial (single rank, lambda = 0; GemmDesc::early): every block of
+// the trial's first backward GEMM sums the forward's SSE partials exactly as the fused tail's decision does
+// (tail_fin_body), applies ls_rule.hpp's sufficient-decrease test and, when it fails, exits; block 0 then
+// publishes the rejection (SC_LOSS, SC_SSE, the abort flag, the host record as SPEC_REJECT_EARLY), so the
+// trial's backward GEMMs and tail are skipped. A rejected first trial needs no gradient
+// (full_batch_minimizer.hpp:138-141, lbfgs.cuh:159-163), so only the work changes, not the results.
+struct EarlyLs {
+  const double *sse_part = nullptr; // the forward's SSE partials (Mlp loss_part_)
+  int nsse = 0;
+  double inv_scale = 0.0;
+  LsCtlArgs ls;
+};
 
 struct HistView {
   int m = 0, slots = 0;

@@ -640,6 +640,24 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
     x.tile = dx_tile(B, L.in);
     return x;
   };
+  // A speculative first trial (tf->early: single rank, lambda = 0) takes its Armijo test in the first backward
+  // launch (EarlyLs, gemm.hip gemm_early_exit): on a failure that launch, the rest of the backward and the tail
+  // exit at entry, and the host finishes the search as after the tail's own rejection (LBF_NO_EARLY=1: off).
+  const bool early_on = env_int("LBF_NO_EARLY", 0) == 0; // read per evaluation: tests switch it in-process
+  EarlyLs early;
+  const EarlyLs *early_p = nullptr;
+  if (early_on && tf && tf->early && !reduced && lambda == 0.0 && nloss > 0) {
+    early.sse_part = loss_part_.get();
+    early.nsse = nloss;
+    early.inv_scale = inv_scale;
+    early.ls = tf->ls;
+    early_p = &early;
+  }
+  auto first_launch = [&](GemmDesc d) { // the early test rides on the first launch only
+    d.early = early_p;
+    early_p = nullptr;
+    return d;
+  };
   for (int l = lstart; l >= 0; --l) {
     if (l == 1 && group_dw_ && !side_reduced(1, fused, nloss)) {
       // the last two dW GEMMs in one launch (S-LBFGS minibatches: two small split-K grids that each
@@ -648,20 +666,20 @@ void Mlp::backward_phase(const float *P, float *G, const float *X, const int *id
       if (gemm_group_ok(d1, d0)) {
         {
           ProfScope ps(ctx_, PK_DX, 1, double(B));
-          gemm(s, dx_desc(1));
+          gemm(s, first_launch(dx_desc(1)));
         }
         ProfScope ps(ctx_, PK_DW, 1, double(B));
-        gemm_group(s, d1, d0);
+        gemm_group(s, first_launch(d1), d0);
         break;
       }
     }
     {
       ProfScope ps(ctx_, PK_DW, l, double(B));
-      gemm(s, dw_desc(l));
+      gemm(s, first_launch(dw_desc(l)));
     }
     if (l > 0) {
       ProfScope ps(ctx_, PK_DX, l, double(B));
-      gemm(s, dx_desc(l));
+      gemm(s, first_launch(dx_desc(l)));
     }
   }
   // every layer's partial slabs -> gradient (+ dots and the status block on a single rank)

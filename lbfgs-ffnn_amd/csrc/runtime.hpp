@@ -79,6 +79,7 @@ struct TailFuse {
   int policy = POL_CPU;
   int iter_next = 1;
   LsCtlArgs ls;
+  int early = 0; // a speculative first trial: its Armijo test in the first backward launch (EarlyLs)
 };
 
 struct Layer {
@@ -171,6 +172,10 @@ public:
   void discard_evals(long long k, long long B) { // speculative evaluations (B rows each) that were aborted
     evals_ -= k;
     rows_ -= k * B;
+  }
+  void backward_skipped() { // a trial rejected by EarlyLs ran its forward only: a loss-only trial
+    --evals_;
+    ++loss_only_;
   }
 
 private:

@@ -167,6 +167,7 @@ float LbfgsSolver::begin_iteration(const LsCtlArgs *ls) {
     tf.iter_next = iter_ + 1;
     tf.ls = *ls;
     tf.ls.alphaf = alpha;
+    tf.early = ls->first ? 0 : 1; // (Wolfe iteration 0 takes its trial without a test)
     obj_->eval_fused(xt_, gt_, p_.get(), hist_.scal(), tf);
     return alpha;
   }
@@ -200,6 +201,7 @@ float LbfgsSolver::begin_iteration(const LsCtlArgs *ls) {
     tf.iter_next = iter_ + 1;
     tf.ls = *ls;
     tf.ls.alphaf = alpha;
+    tf.early = ls->first ? 0 : 1; // (Wolfe iteration 0 takes its trial without a test)
     obj_->eval_fused(xt_, gt_, p_.get(), hist_.scal(), tf);
   } else {
     eval(xt_, gt_, p_.get());
@@ -527,7 +529,8 @@ int LbfgsSolver::iterate_spec(int iters, lbf_record *rec) {
     }
     if (r.seq != f.seq) throw Error(2, "speculative line search: record out of sequence");
     if (f.roles.pair) mark_prev_accepted(rec, r.accept_prev);
-    if (r.status == SPEC_REJECT) {
+    if (r.status == SPEC_REJECT || r.status == SPEC_REJECT_EARLY) {
+      if (r.status == SPEC_REJECT_EARLY) obj_->backward_skipped();
       drain(q, f.prof_end, true); // + the status block as the rejected trial left it (one wait)
       dir_ready_ = false;         // the host finishes this iteration; the next one builds its direction
       restore(f.roles);

@@ -31,6 +31,7 @@ struct Objective {
   // Asynchronous objectives can be enqueued ahead of the host's line-search decisions.
   virtual bool async() const { return false; }
   virtual void discard_evals(long long) {}
+  virtual void backward_skipped() {} // the last trial's backward was skipped (SPEC_REJECT_EARLY)
   // Two-step evaluation of a line-search trial (split_eval()): the loss alone (SC_LOSS, SC_SSE), then the
   // gradient and dots of that same point; together bitwise equal to eval().
   virtual bool split_eval() const { return false; }
@@ -61,6 +62,7 @@ struct MlpObjective : Objective {
   long long rows() const override { return net->rows(); }
   bool async() const override { return true; }
   void discard_evals(long long k) override { net->discard_evals(k, nloc); }
+  void backward_skipped() override { net->backward_skipped(); }
   bool split_eval() const override { return true; }
   void eval_loss(const float *x, double *scal) override {
     net->loss_only(x, X, Y, nullptr, nloc, 1.0 / double(nglob), scal);

@@ -15,6 +15,7 @@
 #include "hist_core.hpp"
 #include "internal.hpp"
 #include "kernels.hpp"
+#include "ls_rule.hpp"
 #include "wave.hpp"
 
 #include <hip/hip_runtime.h>
@@ -337,17 +338,16 @@ __device__ __forceinline__ void tail_fin_body(const TailArgs &a) {
     const LsCtlArgs &L = a.ls;
     const double fn = loss;
     bool ok, conv;
+    // (the sufficient-decrease half is ls_rule.hpp's, which the trial's first backward GEMM applied already
+    // when EarlyLs was on: a trial that reaches this block passed it there)
+    ok = ls_sufficient_decrease(L, fn, fold, gfo);
     if (!L.armijo) {
-      const double fo = L.host_fold ? L.fold : fold;
-      ok = L.first || (!(fn > __dadd_rn(fo, __dmul_rn(__dmul_rn(L.c1, L.alpha), gfo))) && !(tgp < __dmul_rn(L.c2, gfo)));
+      ok = L.first || (ok && !(tgp < __dmul_rn(L.c2, gfo)));
       conv = sqrt(tgg) < L.tol;
       s_sc[5] = fn;
     } else {
-      const float foldf = L.host_fold ? L.foldf : float(fold);
-      const float lnew = float(fn), gdp = float(gfo);
-      ok = lnew <= __fadd_rn(foldf, __fmul_rn(__fmul_rn(float(L.c1), L.alphaf), gdp));
       conv = float(sqrt(tgg)) < float(L.tol);
-      s_sc[5] = double(lnew);
+      s_sc[5] = double(float(fn));
     }
     s_ok = ok ? 1 : 0;
     s_rec[0] = fn;

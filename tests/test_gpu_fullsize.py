@@ -384,3 +384,33 @@ def test_cfg4_slbfgs_epoch_forced_pairs_full_size(ctx, pkg, O, mnist, cfg4_epoch
     assert max(ew) <= 1e-4, ew
     assert dl <= 1e-4, dl
     assert int(r["hist"]["accepted"][0]) == int(rec_f[0, 3])
+
+
+@pytest.mark.parametrize("line_search", ["wolfe", "armijo"])
+def test_early_armijo_exit_bitwise(ctx, pkg, mnist, monkeypatch, line_search):
+    """EarlyLs (csrc/kernels.hpp, gemm.hip gemm_early_exit): a speculative first trial that fails sufficient
+    decrease (full_batch_minimizer.hpp:138-141 / lbfgs.cuh:159-163) is rejected by its first backward GEMM, which
+    skips the trial's backward and tail. Over 60 cfg-2 iterations at N = 60000 the trajectory and the final
+    parameters are bitwise those with the test left to the fused tail (LBF_NO_EARLY=1), and each skipped backward
+    is one full evaluation fewer and one loss-only trial more."""
+    _, _, _, _, X, Y = mnist
+    dims, acts = CFG2
+    net = pkg.Mlp(ctx, dims, acts)
+    runs = {}
+    for off in (True, False):
+        if off:
+            monkeypatch.setenv("LBF_NO_EARLY", "1")
+        else:
+            monkeypatch.delenv("LBF_NO_EARLY", raising=False)
+        P = net.init_params(123, "cpu")
+        hist, info = pkg.lbfgs_solve(net, P, X, Y, m=10, max_iters=60, tol=0.0, line_search=line_search)
+        runs[off] = (hist, int(info.n_evals), int(info.n_loss_only), host(P))
+    (h0, e0, l0, p0), (h1, e1, l1, p1) = runs[True], runs[False]
+    for k in ("loss", "grad_norm", "alpha", "ls_trials", "accepted"):
+        assert np.array_equal(h0[k], h1[k]), k
+    assert np.array_equal(p0, p1)
+    skipped = l1 - l0
+    print(f"{line_search}: {skipped} first trials rejected early in 60 iterations ({e0} -> {e1} full evaluations)")
+    assert e0 - e1 == skipped >= 0
+    if line_search == "wolfe":
+        assert skipped > 0  # cfg 2 rejects ~5 % of its first trials on sufficient decrease (DESIGN.md §8)
